@@ -1,0 +1,205 @@
+#!/usr/bin/env python3
+"""Throughput benchmark of the MI355X ViT training step (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--arch b16]
+
+One step = forward + cross-entropy + backward + (N>1: gradient all-reduce over RCCL) + fused
+SGD-momentum update with OneCycleLR scalars, on a synthetic batch already resident in HBM.
+Weak scaling: every rank processes --batch images (256 = BASELINE config #2 per GPU).
+For N>1 launch with torch.distributed.run (one process per GPU); rank 0 prints one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "vit-of-pytorch_amd"))
+sys.path.insert(0, REPO)
+
+import torch  # noqa: E402
+
+PEAK_BF16_TFLOPS = 2516.6  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md; 256 CU x 2.4 GHz x 4096)
+PEAK_HBM_GBS = 8000.0
+
+ARCHS = {
+    "b16": dict(patch_size=16, emb_dim=768, mlp_dim=3072, num_heads=12, num_layers=12),
+    "b32": dict(patch_size=32, emb_dim=768, mlp_dim=3072, num_heads=12, num_layers=12),
+    "l16": dict(patch_size=16, emb_dim=1024, mlp_dim=4096, num_heads=16, num_layers=24),
+    "l32": dict(patch_size=32, emb_dim=1024, mlp_dim=4096, num_heads=16, num_layers=24),
+}
+
+
+def train_flops_per_image(a, image_size, num_classes):
+    D, M, P, L = a["emb_dim"], a["mlp_dim"], a["patch_size"], a["num_layers"]
+    n = (image_size // P) ** 2
+    N = n + 1
+    patch = 2 * n * 3 * P * P * D
+    fwd = patch + L * 2 * (3 * N * D * D + 2 * N * N * D + N * D * D + 2 * N * D * M) + 2 * D * num_classes
+    return 3 * fwd - patch
+
+
+def cpu_baseline(arch, image_size, num_classes, seconds_budget=20.0):
+    """Time the CPU oracle (restatement of reference src/train.py:train_epoch's step) on the host."""
+    from oracle.vit_oracle import OneCycle, ViTConfig, init_params, loss_and_grads, sgd_step, tame_params
+    cfg = ViTConfig(image_size=image_size, num_classes=num_classes, **arch)
+    params = tame_params(init_params(cfg, seed=42))
+    bs = 8
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(bs, 3, image_size, image_size, generator=g)
+    y = torch.randint(0, num_classes, (bs,), generator=g)
+    sched = OneCycle(0.03, 15000, 500 / 15000)
+    bufs = {}
+    # warm-up step (not timed)
+    _, _, grads = loss_and_grads(params, x, y, cfg)
+    params, bufs = sgd_step(params, grads, bufs, *sched.at(0), 0.0, first=True)
+    steps, t0 = 0, time.perf_counter()
+    while True:
+        _, _, grads = loss_and_grads(params, x, y, cfg)
+        params, bufs = sgd_step(params, grads, bufs, *sched.at(steps + 1), 0.0, first=False)
+        steps += 1
+        if time.perf_counter() - t0 > seconds_budget or steps >= 20:
+            break
+    dt = time.perf_counter() - t0
+    return dict(value=round(steps * bs / dt, 3), unit="images/sec", cores=torch.get_num_threads(), kind="port",
+                sample=f"oracle fp32 CPU train step (fwd+CE+bwd+SGD, tamed init), batch {bs}, {steps} timed steps "
+                       f"after 1 warm-up, {dt:.1f} s")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=256, help="images per GPU")
+    ap.add_argument("--arch", default="b16", choices=sorted(ARCHS))
+    ap.add_argument("--image-size", type=int, default=224)
+    ap.add_argument("--num-classes", type=int, default=1000)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=20.0)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+
+    from vitmi import ops
+    from vitmi.dist import GradAllReducer
+    from vitmi.model import VisionTransformer
+
+    arch = ARCHS[args.arch]
+    # random-init weights of the named architecture, drawn exactly like the reference ctor
+    # (src/model.py:161-194, seed 42), then bound to the HIP engine on this GPU
+    torch.manual_seed(42)
+    model = VisionTransformer(image_size=(args.image_size, args.image_size),
+                              patch_size=(arch["patch_size"], arch["patch_size"]), emb_dim=arch["emb_dim"],
+                              mlp_dim=arch["mlp_dim"], num_heads=arch["num_heads"], num_layers=arch["num_layers"],
+                              num_classes=args.num_classes, attn_dropout_rate=0.0, dropout_rate=0.0).to(dev)
+    eng = model.engine()
+    eng.refresh_mirror()
+    cfg = eng.cfg
+    b = args.batch
+    g = torch.Generator(device=dev).manual_seed(1000 + rank)
+    x = torch.randn(b, 3, args.image_size, args.image_size, device=dev, generator=g)
+    y = torch.randint(0, args.num_classes, (b,), device=dev, generator=g)
+    mom_buf = torch.zeros_like(eng.flat)
+    reducer = GradAllReducer(eng).attach() if world > 1 else None
+    total_steps = args.warmup + args.steps
+    # OneCycleLR schedule scalars as configured by reference src/train.py:159-163 (lr .03, 500 warmup/15000)
+    from torch.optim.lr_scheduler import OneCycleLR
+    _p = torch.nn.Parameter(torch.zeros(1))
+    _opt = torch.optim.SGD([_p], lr=0.03, momentum=0.9)
+    sched = OneCycleLR(_opt, max_lr=0.03, pct_start=500 / 15000, total_steps=15000)
+    hp = []
+    for _ in range(total_steps):
+        hp.append((_opt.param_groups[0]["lr"], _opt.param_groups[0]["momentum"]))
+        _opt.step()
+        sched.step()
+
+    def step(k):
+        eng.forward(x)
+        dl, _ = eng.cross_entropy(y, grad_scale=1.0 / (b * world))
+        eng.backward(dl)
+        if reducer is not None:
+            reducer.finish()
+        lr, mom = hp[k]
+        ops.sgd_step(eng.flat, eng.grad, mom_buf, eng.mirror, eng.layout.numel, lr, mom, 0.0, k == 0)
+        eng.refresh_mirror(full=False)
+
+    def barrier():
+        if world > 1:
+            import torch.distributed as dist
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    for k in range(args.warmup):
+        step(k)
+    barrier()
+    eng.probe = []
+    t0 = time.perf_counter()
+    for k in range(args.warmup, total_steps):
+        step(k)
+    barrier()
+    dt = time.perf_counter() - t0
+    probe = eng.probe
+    eng.probe = None
+    if world > 1:
+        import torch.distributed as dist
+        t = torch.tensor([dt], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t)
+    fc1_ms = sum(s.elapsed_time(e) for s, e in probe) / max(1, len(probe))
+    T = b * cfg.tokens
+    fc1_flop = 2.0 * T * cfg.emb_dim * cfg.mlp_dim
+    fc1_tflops = fc1_flop / (fc1_ms * 1e-3) / 1e12
+    imgs = args.steps * b * world
+    value = imgs / dt
+    fpi = train_flops_per_image(arch, args.image_size, args.num_classes)
+    step_tflops_per_gpu = value / world * fpi / 1e12
+    out = {
+        "metric": "images/sec training step, ViT-B/16 224px bf16, 1/2/4/8 MI355X" if args.arch == "b16" and
+        args.image_size == 224 else f"images/sec training step, ViT-{args.arch} {args.image_size}px bf16",
+        "value": round(value, 2),
+        "unit": "images/sec",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(dt / args.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "bf16",
+        "data": "synthetic (N(0,1) images, uniform labels, seed-42 reference-order random init)",
+        "config": {"workload": f"ViT-{args.arch.upper()} @{args.image_size} train step (fwd+CE+bwd+"
+                               f"{'RCCL all-reduce+' if world > 1 else ''}SGD-momentum/OneCycleLR)",
+                   "model": f"ViT-{args.arch.upper()}", "image_size": args.image_size, "per_gpu_batch": b,
+                   "global_batch": b * world, "seq_len": cfg.tokens, "num_classes": args.num_classes,
+                   "parallelism": f"dp{world}"},
+        "roofline": {"bound": "mfma", "kernel": "gemm_bf16 fc1 fwd (bias+GELU epilogue), "
+                                                f"M={T} N={cfg.mlp_dim} K={cfg.emb_dim}",
+                     "achieved": round(fc1_tflops, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+                     "frac": round(fc1_tflops / PEAK_BF16_TFLOPS, 4), "traffic": None,
+                     "avg_launch_ms": round(fc1_ms, 4), "launches": len(probe)},
+        "step_mfma_frac": round(step_tflops_per_gpu / PEAK_BF16_TFLOPS, 4),
+        "train_gflop_per_image": round(fpi / 1e9, 3),
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(arch, args.image_size, args.num_classes, args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,187 @@
+/*
+ * vit_hip.h — C ABI of the MI355X (gfx950) ViT training-step kernels.
+ *
+ * The reference (sea-with-sakura/ViT-of-Pytorch) has no native code and no FFI: every op
+ * on its hot path is a PyTorch ATen call made from src/model.py / src/train.py. Each entry
+ * point below replaces the ATen op(s) named in its comment (reference file:line), so the
+ * drop-in Python surface (vitmi.model.VisionTransformer etc.) can run the training step on
+ * hand-written CDNA4 kernels.
+ *
+ * Conventions
+ *   - all pointers are device pointers; sizes/strides are element counts (int64_t);
+ *   - bf16 tensors are passed as `void*` / `const void*` holding IEEE bfloat16 bit patterns;
+ *   - `stream` is a hipStream_t passed as an opaque pointer (NULL = default stream);
+ *   - the library never allocates or frees device memory: callers own every buffer,
+ *     including workspaces; no call synchronises the host;
+ *   - every entry point returns VIT_OK (0) or an error code; vit_last_error() returns a
+ *     thread-local description of the last failure on the calling thread;
+ *   - calls are reentrant and keep no global mutable device state.
+ */
+#ifndef VIT_HIP_H_
+#define VIT_HIP_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* vit_stream_t;
+
+enum vit_status {
+  VIT_OK = 0,
+  VIT_ERR_INVALID_ARG = 1,
+  VIT_ERR_HIP = 2,
+  VIT_ERR_UNSUPPORTED = 3,
+};
+
+const char* vit_last_error(void);
+int vit_abi_version(void);
+
+/* ------------------------------------------------------------------------------------------
+ * bf16 MFMA GEMM with fused epilogues.
+ *   C[m, n] = sum_k A(m, k) * B(k, n)
+ * A(m,k) is A[m*lda + k] when a_layout == VIT_K_CONTIG, A[k*lda + m] when VIT_MN_CONTIG.
+ * B(k,n) is B[n*ldb + k] when b_layout == VIT_K_CONTIG, B[k*ldb + n] when VIT_MN_CONTIG.
+ * K must be a multiple of 64 (callers zero-pad). M, N are arbitrary.
+ * gridDim.z batching: every pointer advances by its *_batch_stride per batch index.
+ *
+ * Replaces (reference): LinearGeneral.forward tensordot+bias   src/model.py:61-63,86-88,99
+ *                       MlpBlock fc1 -> GELU, fc2                src/model.py:43-48
+ *                       Conv2d patch embedding + cls + pos-emb  src/model.py:179,197-204, :16-17
+ *                       and the autograd dgrad/wgrad of all of them (src/train.py:23)
+ * ---------------------------------------------------------------------------------------- */
+enum vit_layout { VIT_K_CONTIG = 0, VIT_MN_CONTIG = 1 };
+
+enum vit_epilogue {
+  VIT_EPI_F32 = 0,            /* C(f32)  = acc                                                */
+  VIT_EPI_BF16 = 1,           /* C(bf16) = acc                                                */
+  VIT_EPI_BIAS_BF16 = 2,      /* C(bf16) = acc + bias[n]                                       */
+  VIT_EPI_BIAS_GELU = 3,      /* u = acc + bias[n]; C(bf16) = u; C2(bf16) = gelu_erf(u)        */
+  VIT_EPI_BIAS_RESID_F32 = 4, /* C(f32) = acc + bias[n] + aux_f32[m*ldaux + n] (C may == aux) */
+  VIT_EPI_GELU_BWD = 5,       /* C(bf16) = acc * gelu_erf'(aux_bf16[m*ldaux + n])              */
+  VIT_EPI_PATCH = 6,          /* C(f32) = (m % tokens == 0) ? aux2[n] + pos[0][n]
+                                            : acc + bias[n] + pos[m % tokens][n],
+                                 pos = aux_f32 with row stride ldaux                          */
+  VIT_EPI_SPLITK = 7,         /* split-K partial: C(f32)[(z*split_k + s)*M*N + m*N + n] = acc  */
+};
+
+typedef struct vit_gemm_args {
+  int64_t M, N, K;
+  const void* A;
+  int64_t lda;
+  int64_t a_batch_stride;
+  int32_t a_layout;
+  int32_t b_layout;
+  const void* B;
+  int64_t ldb;
+  int64_t b_batch_stride;
+  void* C;
+  int64_t ldc;
+  int64_t c_batch_stride;
+  void* C2;
+  int64_t ldc2;
+  const float* bias;
+  int64_t bias_batch_stride;
+  const void* aux;
+  int64_t ldaux;
+  const float* aux2;
+  int64_t batch;   /* >= 1 */
+  int64_t split_k; /* >= 1; > 1 only with VIT_EPI_SPLITK */
+  int64_t tokens;  /* VIT_EPI_PATCH: tokens per image */
+  int32_t epilogue;
+  int32_t tile;    /* 0 = auto */
+} vit_gemm_args;
+
+int vit_gemm_bf16(const vit_gemm_args* args, vit_stream_t stream);
+
+/* out[z*out_batch_stride + m*ldo + n] (+)= sum_s ws[((z*split + s)*M + m)*N + n]  (f32) */
+int vit_splitk_reduce(const float* ws, int64_t batch, int64_t split, int64_t M, int64_t N,
+                      float* out, int64_t ldo, int64_t out_batch_stride, int32_t accumulate,
+                      vit_stream_t stream);
+
+/* ------------------------------------------------------------------------------------------
+ * LayerNorm over the last dim (eps, biased variance, affine).  nn.LayerNorm src/model.py:108,114,146
+ * fwd: y = (x - mean) * rstd * gamma + beta; saves mean/rstd (f32). y is bf16 or f32 (y_f32).
+ * bwd: dx = rstd*(g - mean(g) - xhat*mean(g*xhat)), g = dy*gamma; dx_out = dres + dx (dres may
+ *      be NULL); optional bf16 copy of dx_out. Writes per-block partial [nblk][2*D] sums of
+ *      (dy*xhat, dy) into `partial` (>= vit_layernorm_bwd_partial_rows(rows) rows) and, when
+ *      dgamma_dbeta != NULL, reduces them into dgamma_dbeta[0:D] (dgamma), [D:2D] (dbeta).
+ * ---------------------------------------------------------------------------------------- */
+int vit_layernorm_fwd(const float* x, int64_t ldx, const float* gamma, const float* beta,
+                      void* y, int64_t ldy, int32_t y_f32, float* mean, float* rstd,
+                      int64_t rows, int64_t D, float eps, vit_stream_t stream);
+int64_t vit_layernorm_bwd_partial_rows(int64_t rows);
+int vit_layernorm_bwd(const void* dy, int64_t lddy, int32_t dy_f32, const float* x, int64_t ldx,
+                      const float* mean, const float* rstd, const float* gamma,
+                      const float* dres, int64_t lddres, float* dx, int64_t lddx,
+                      void* dx_bf16, int64_t lddxb, float* partial, float* dgamma_dbeta,
+                      int32_t accumulate_params, int64_t rows, int64_t D, vit_stream_t stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Fused multi-head self-attention, one (image, head) per workgroup, all keys in LDS.
+ * qkv: bf16 [B*N, 3, H, hd] (q | k | v);  o: bf16 [B*N, H, hd];  lse: f32 [B, H, N]
+ * S = (q k^T) * scale (scale = 1/sqrt(hd)), P = softmax(S), O = P v.
+ * Replaces SelfAttention.forward src/model.py:90-97 (matmul, /scale, softmax, matmul, permutes)
+ * bwd: dqkv (bf16 [B*N, 3, H, hd]) from dO, recomputing P from lse.
+ * Limits: N <= 320, hd in {32, 64, 80(padded to 96)}.
+ * ---------------------------------------------------------------------------------------- */
+int vit_attention_fwd(const void* qkv, void* o, float* lse, int64_t B, int64_t N, int64_t H,
+                      int64_t hd, float scale, vit_stream_t stream);
+int vit_attention_bwd(const void* qkv, const void* o, const void* dout, const float* lse, void* dqkv,
+                      int64_t B, int64_t N, int64_t H, int64_t hd, float scale, vit_stream_t stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Patch embedding im2col (Conv2d k=s=P as a GEMM, src/model.py:179,197-200):
+ * x f32 NCHW [B,3,img,img] -> out bf16 [B*N, Kpad], N = (img/P)^2 + 1, row b*N (cls) is 0,
+ * row b*N+1+(py*g+px), col c*P*P + ky*P + kx; cols >= 3P^2 are 0.
+ * ---------------------------------------------------------------------------------------- */
+int vit_im2col(const float* x, void* out, int64_t B, int64_t img, int64_t P, int64_t Kpad,
+               vit_stream_t stream);
+
+/* token-level grads of the embedding (src/model.py:17,203-204): from dh0 f32 [B*N, D]:
+ * dpos[n][d] = sum_b dh0[b*N+n][d]; dcls = dpos[0]; dconv_bias = sum_{n>=1} dpos[n]. */
+int vit_embed_grad(const float* dh0, int64_t B, int64_t N, int64_t D, float* dpos, float* dcls,
+                   float* dconv_bias, vit_stream_t stream);
+
+/* column sums: out[n] (+)= sum_r in[r*ld + n], in bf16 (in_bf16=1) or f32. `partial` needs
+ * vit_colsum_partial_rows(rows) * cols floats. (bias grads, src/train.py:23 autograd) */
+int64_t vit_colsum_partial_rows(int64_t rows);
+int vit_colsum(const void* in, int32_t in_bf16, int64_t rows, int64_t cols, int64_t ld,
+               float* partial, float* out, int32_t accumulate, vit_stream_t stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Classifier head helpers (tiny, f32): C = op(A) op(B) (+ bias) (+ C if accumulate).
+ * a_trans: A(m,k) = A[k*lda+m]; b_trans: B(k,n) = B[n*ldb+k].  nn.Linear src/model.py:194,210
+ * ---------------------------------------------------------------------------------------- */
+int vit_gemm_f32(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda, int32_t a_trans,
+                 const float* B, int64_t ldb, int32_t b_trans, float* C, int64_t ldc,
+                 const float* bias, int32_t accumulate, vit_stream_t stream);
+
+/* Cross entropy (mean over the global batch), CrossEntropyLoss src/train.py:151,22, plus
+ * accuracy counts (src/utils.py:28-41). dlogits = (softmax - onehot) * grad_scale.
+ * row_stats[b] = {loss_b, top1_hit, top5_hit}. */
+int vit_cross_entropy(const float* logits, const int64_t* labels, int64_t B, int64_t C,
+                      float* dlogits, float grad_scale, float* row_stats, vit_stream_t stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Optimizer / parameter mirrors.  torch.optim.SGD step, src/train.py:24,154-158:
+ *   d = g + wd*p; buf = first ? d : momentum*buf + d; p -= lr*buf; p_bf16 = bf16(p) (if != NULL)
+ * ---------------------------------------------------------------------------------------- */
+int vit_sgd_step(float* p, const float* g, float* buf, void* p_bf16, int64_t n, float lr,
+                 float momentum, float weight_decay, int32_t first, vit_stream_t stream);
+int vit_cast_f32_bf16(const float* in, void* out, int64_t n, vit_stream_t stream);
+/* out bf16 [rows][ldo] <- in f32 [rows][cols]; columns cols..ldo-1 are zeroed. */
+int vit_cast_pad_rows(const float* in, int64_t rows, int64_t cols, void* out, int64_t ldo,
+                      vit_stream_t stream);
+/* out[r*ldo + z*cols + c] = in[z*zstride + r*ldi + c]  (z < Z), as bf16 (out_bf16) or f32.
+ * Packs q/k/v LinearGeneral weights [D][H,hd] (src/model.py:73-75) into one [D][3D] operand. */
+int vit_pack_cols(const float* in, int64_t zstride, int64_t ldi, int64_t rows, int64_t cols, int64_t Z,
+                  void* out, int64_t ldo, int32_t out_bf16, vit_stream_t stream);
+/* y = a*x + b*y (f32), used for gradient scaling / accumulation. */
+int vit_axpby(const float* x, float* y, int64_t n, float a, float b, vit_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VIT_HIP_H_ */

@@ -1,0 +1,74 @@
+"""Host-side logic that needs no GPU: the C-ABI library exports, parameter layout, module surface."""
+import ctypes
+import os
+import re
+
+import pytest
+import torch
+
+from oracle.vit_oracle import ViTConfig, init_params, param_names
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(REPO, "include", "vit_hip.h")
+
+
+def test_library_exports_every_header_symbol():
+    from vitmi import _lib
+    if not os.path.exists(_lib.LIB_PATH):
+        pytest.skip("libvit_hip.so not built (run __graft_entry__.build())")
+    text = open(HEADER).read()
+    declared = set(re.findall(r"^\s*(?:const char\*|int64_t|int)\s+(vit_\w+)\s*\(", text, flags=re.M))
+    assert declared, "no declarations parsed"
+    lib = ctypes.CDLL(_lib.LIB_PATH)
+    for name in declared:
+        assert hasattr(lib, name), name
+    assert declared == set(_lib.EXPORTED), declared ^ set(_lib.EXPORTED)
+    assert lib.vit_abi_version() == 1
+
+
+def test_flat_layout_and_buckets():
+    from vitmi.engine import ArchConfig, FlatLayout
+    cfg = ArchConfig()
+    lay = FlatLayout(cfg)
+    assert set(lay.offsets) == set(param_names(ViTConfig()))
+    # every parameter 256-B aligned and non-overlapping
+    spans = sorted((o, o + int(torch.tensor(lay.shapes[k]).prod())) for k, o in lay.offsets.items())
+    for (a0, a1), (b0, _) in zip(spans, spans[1:]):
+        assert a1 <= b0
+    assert all(o % 64 == 0 for o in lay.offsets.values())
+    # buckets tile [0, numel) contiguously in backward order: head, layer L-1 .. 0, embed
+    assert lay.buckets[0][1] == 0 and lay.buckets[-1][2] == lay.numel
+    for (_, _, e), (_, s, _) in zip(lay.buckets, lay.buckets[1:]):
+        assert e == s
+    assert [b[0] for b in lay.buckets[1:-1]] == [f"layer{i}" for i in reversed(range(12))]
+    # q/k/v weights are equally strided (the batched wgrad / pack kernels rely on it)
+    p = "transformer.encoder_layers.3.attn."
+    q, k, v = (lay.offsets[p + s + ".weight"] for s in ("query", "key", "value"))
+    assert k - q == v - k
+    assert lay.offsets[p + "key.bias"] - lay.offsets[p + "query.bias"] == k - q
+
+
+def test_module_surface_and_rng_order():
+    from vitmi.model import MLPBlock, MlpBlock, VisionTransformer
+    assert MLPBlock is MlpBlock
+    cfg = ViTConfig(image_size=32, patch_size=8, emb_dim=64, mlp_dim=128, num_heads=2, num_layers=2, num_classes=10)
+    torch.manual_seed(42)
+    m = VisionTransformer(image_size=(32, 32), patch_size=(8, 8), emb_dim=64, mlp_dim=128, num_heads=2, num_layers=2,
+                          num_classes=10, attn_dropout_rate=0.0, dropout_rate=0.0)
+    ref = init_params(cfg, seed=42)
+    sd = m.state_dict()
+    assert list(sd.keys()) == list(ref.keys())
+    for k in ref:
+        assert torch.equal(sd[k], ref[k]), k
+    # default ctor keeps the reference's dropout modules (src/model.py defaults)
+    d = VisionTransformer(image_size=(32, 32), patch_size=(8, 8), emb_dim=64, mlp_dim=128, num_heads=2, num_layers=1,
+                          num_classes=10)
+    assert sum(isinstance(x, torch.nn.Dropout) for x in d.modules()) == 4
+
+
+def test_cpu_forward_refuses():
+    from vitmi.model import VisionTransformer
+    m = VisionTransformer(image_size=(32, 32), patch_size=(8, 8), emb_dim=64, mlp_dim=128, num_heads=2, num_layers=1,
+                          num_classes=10, dropout_rate=0.0)
+    with pytest.raises(RuntimeError, match="MI355X HIP path only"):
+        m(torch.randn(1, 3, 32, 32))

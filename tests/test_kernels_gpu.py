@@ -1,0 +1,253 @@
+"""Per-kernel numerics of libvit_hip.so against plain PyTorch fp32 references (GPU only)."""
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from vitmi import ops
+from vitmi._lib import (EPI_BF16, EPI_BIAS_BF16, EPI_BIAS_GELU, EPI_BIAS_RESID_F32, EPI_F32, EPI_GELU_BWD,
+                        EPI_PATCH, EPI_SPLITK, K_CONTIG, MN_CONTIG)
+
+DEV = "cuda"
+
+
+def rel(a, b):
+    a = a.double()
+    b = b.double()
+    return float((a - b).norm() / b.norm().clamp_min(1e-30))
+
+
+def _mats(M, N, K, al, bl, ints=False, gen=None):
+    if ints:
+        A = torch.randint(-4, 5, (M, K), device=DEV).float()
+        B = torch.randint(-4, 5, (K, N), device=DEV).float()
+    else:
+        A = torch.randn(M, K, device=DEV)
+        B = torch.randn(K, N, device=DEV)
+    A = A.bfloat16()
+    B = B.bfloat16()
+    # MN-contiguous operands get their rows padded to a multiple of 8 elements (16 B)
+    pad = lambda n: (n + 7) // 8 * 8
+    if al == K_CONTIG:
+        Am, lda = A.contiguous(), K                                  # [M][K]
+    else:
+        lda = pad(M)
+        Am = torch.zeros(K, lda, device=DEV, dtype=torch.bfloat16)   # [K][lda]
+        Am[:, :M] = A.t()
+    if bl == K_CONTIG:
+        Bm, ldb = B.t().contiguous(), K                              # [N][K]
+    else:
+        ldb = pad(N)
+        Bm = torch.zeros(K, ldb, device=DEV, dtype=torch.bfloat16)   # [K][ldb]
+        Bm[:, :N] = B
+    return A, B, Am, Bm, lda, ldb
+
+
+LAYOUTS = [(K_CONTIG, K_CONTIG), (K_CONTIG, MN_CONTIG), (MN_CONTIG, MN_CONTIG), (MN_CONTIG, K_CONTIG)]
+
+
+@pytest.mark.parametrize("al,bl", LAYOUTS)
+@pytest.mark.parametrize("M,N,K", [(128, 128, 64), (256, 384, 192), (200, 136, 128), (37, 300, 64)])
+def test_gemm_exact_integers(al, bl, M, N, K):
+    A, B, Am, Bm, lda, ldb = _mats(M, N, K, al, bl, ints=True)
+    C = torch.full((M, N), float("nan"), device=DEV)
+    ops.gemm(Am, Bm, C, M, N, K, a_layout=al, b_layout=bl, lda=lda, ldb=ldb, ldc=N, epilogue=EPI_F32)
+    ref = A.float() @ B.float()
+    assert torch.equal(C, ref)
+
+
+@pytest.mark.parametrize("al,bl", LAYOUTS)
+def test_gemm_random_f32(al, bl):
+    M, N, K = 1000, 768, 768
+    A, B, Am, Bm, lda, ldb = _mats(M, N, K, al, bl)
+    C = torch.empty(M, N, device=DEV)
+    ops.gemm(Am, Bm, C, M, N, K, a_layout=al, b_layout=bl, lda=lda, ldb=ldb, ldc=N, epilogue=EPI_F32)
+    assert rel(C, A.float() @ B.float()) < 1e-5
+
+
+def test_gemm_epilogues():
+    M, N, K = 300, 256, 128
+    A, B, Am, Bm, lda, ldb = _mats(M, N, K, K_CONTIG, K_CONTIG)
+    ref = A.float() @ B.float()
+    bias = torch.randn(N, device=DEV)
+    kw = dict(a_layout=K_CONTIG, b_layout=K_CONTIG, lda=lda, ldb=ldb, ldc=N)
+    C = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    ops.gemm(Am, Bm, C, M, N, K, epilogue=EPI_BF16, **kw)
+    assert rel(C.float(), ref) < 5e-3
+    ops.gemm(Am, Bm, C, M, N, K, epilogue=EPI_BIAS_BF16, bias=bias, **kw)
+    assert rel(C.float(), ref + bias) < 5e-3
+    C2 = torch.empty_like(C)
+    ops.gemm(Am, Bm, C, M, N, K, epilogue=EPI_BIAS_GELU, bias=bias, C2=C2, ldc2=N, **kw)
+    assert rel(C.float(), ref + bias) < 5e-3
+    assert rel(C2.float(), torch.nn.functional.gelu(ref + bias)) < 5e-3
+    R = torch.randn(M, N, device=DEV)
+    Cf = R.clone()
+    ops.gemm(Am, Bm, Cf, M, N, K, epilogue=EPI_BIAS_RESID_F32, bias=bias, aux=Cf, ldaux=N, **kw)
+    assert rel(Cf, ref + bias + R) < 1e-5
+    U = torch.randn(M, N, device=DEV).bfloat16()
+    ops.gemm(Am, Bm, C, M, N, K, epilogue=EPI_GELU_BWD, aux=U, ldaux=N, **kw)
+    u = U.float().requires_grad_(True)
+    gref, = torch.autograd.grad(torch.nn.functional.gelu(u), u, ref)
+    assert rel(C.float(), gref) < 5e-3
+
+
+def test_gemm_patch_epilogue():
+    tokens, D, Kp = 5, 128, 64
+    M = 3 * tokens
+    A = torch.randn(M, Kp, device=DEV).bfloat16()
+    A[::tokens] = 0
+    W = torch.randn(D, Kp, device=DEV).bfloat16()
+    bias, pos, cls = torch.randn(D, device=DEV), torch.randn(tokens, D, device=DEV), torch.randn(D, device=DEV)
+    C = torch.empty(M, D, device=DEV)
+    ops.gemm(A, W, C, M, D, Kp, a_layout=K_CONTIG, b_layout=K_CONTIG, lda=Kp, ldb=Kp, ldc=D, epilogue=EPI_PATCH,
+             bias=bias, aux=pos, ldaux=D, aux2=cls, tokens=tokens)
+    ref = A.float() @ W.float().t() + bias + pos.repeat(3, 1)
+    ref[::tokens] = cls + pos[0]
+    assert rel(C, ref) < 1e-5
+
+
+def test_gemm_batched_splitk():
+    M, N, K, Z, S = 256, 192, 1024, 3, 4
+    A = torch.randn(Z, K, M, device=DEV).bfloat16()      # MN-contig A (wgrad style)
+    B = torch.randn(Z, K, N, device=DEV).bfloat16()
+    ws = torch.empty(Z, S, M, N, device=DEV)
+    ops.gemm(A, B, ws, M, N, K, a_layout=MN_CONTIG, b_layout=MN_CONTIG, lda=M, ldb=N, ldc=N, epilogue=EPI_SPLITK,
+             batch=Z, a_bs=K * M, b_bs=K * N, split_k=S)
+    out = torch.empty(Z, M, N + 8, device=DEV)
+    ops.splitk_reduce(ws, Z, S, M, N, out, N + 8, M * (N + 8))
+    ref = torch.einsum("zkm,zkn->zmn", A.float(), B.float())
+    assert rel(out[..., :N], ref) < 1e-5
+
+
+@pytest.mark.parametrize("D", [64, 768, 1024, 1280])
+def test_layernorm(D):
+    rows = 333
+    x = (torch.randn(rows, D, device=DEV) * 3 + 1).requires_grad_(True)
+    g = torch.randn(D, device=DEV).requires_grad_(True)
+    b = torch.randn(D, device=DEV).requires_grad_(True)
+    y = torch.empty(rows, D, device=DEV, dtype=torch.bfloat16)
+    mean = torch.empty(rows, device=DEV)
+    rstd = torch.empty(rows, device=DEV)
+    ops.layernorm_fwd(x.detach(), D, g.detach(), b.detach(), y, D, mean, rstd, rows, D)
+    ref = torch.nn.functional.layer_norm(x, (D,), g, b, 1e-5)
+    assert rel(y.float(), ref.detach()) < 5e-3
+    dy = torch.randn(rows, D, device=DEV).bfloat16()
+    dres = torch.randn(rows, D, device=DEV)
+    gx, gg, gb = torch.autograd.grad(ref, (x, g, b), dy.float())
+    dx = torch.empty(rows, D, device=DEV)
+    dxb = torch.empty(rows, D, device=DEV, dtype=torch.bfloat16)
+    part = torch.empty(ops.layernorm_bwd_partial_rows(rows), 2 * D, device=DEV)
+    dgb = torch.empty(2 * D, device=DEV)
+    ops.layernorm_bwd(dy, D, x.detach(), D, mean, rstd, g.detach(), dx, D, part, rows, D, dres=dres, lddres=D,
+                      dx_bf16=dxb, lddxb=D, dgamma_dbeta=dgb)
+    assert rel(dx, gx + dres) < 1e-4
+    assert rel(dxb.float(), gx + dres) < 5e-3
+    assert rel(dgb[:D], gg) < 1e-4
+    assert rel(dgb[D:], gb) < 1e-4
+
+
+def _attn_ref(qkv, B, N, H, hd):
+    q, k, v = qkv.float().view(B, N, 3, H, hd).permute(2, 0, 3, 1, 4)
+    s = (q @ k.transpose(-1, -2)) / math.sqrt(hd)
+    p = torch.softmax(s, -1)
+    o = (p @ v).permute(0, 2, 1, 3).reshape(B * N, H * hd)
+    lse = torch.logsumexp(s, -1)
+    return o, lse
+
+
+@pytest.mark.parametrize("B,N,H,hd", [(2, 197, 12, 64), (3, 17, 2, 32), (2, 50, 4, 64), (1, 5, 3, 64), (2, 257, 2, 64)])
+def test_attention(B, N, H, hd):
+    D = H * hd
+    qkv = (torch.randn(B * N, 3 * D, device=DEV) * 1.5).bfloat16().requires_grad_(True)
+    o = torch.empty(B * N, D, device=DEV, dtype=torch.bfloat16)
+    lse = torch.empty(B, H, N, device=DEV)
+    ops.attention_fwd(qkv.detach(), o, lse, B, N, H, hd, 1.0 / math.sqrt(hd))
+    qf = qkv.float().detach().requires_grad_(True)
+    oref, lref = _attn_ref(qf, B, N, H, hd)
+    assert rel(o.float(), oref.detach()) < 1e-2
+    assert rel(lse, lref.detach()) < 1e-4
+    dout = torch.randn(B * N, D, device=DEV).bfloat16()
+    dqkv = torch.full((B * N, 3 * D), float("nan"), device=DEV, dtype=torch.bfloat16)
+    ops.attention_bwd(qkv.detach(), o, dout, lse, dqkv, B, N, H, hd, 1.0 / math.sqrt(hd))
+    gref, = torch.autograd.grad(oref, qf, dout.float())
+    gq, gk, gv = gref.view(B * N, 3, D).unbind(1)
+    mq, mk, mv = dqkv.float().view(B * N, 3, D).unbind(1)
+    assert rel(mq, gq) < 2e-2
+    assert rel(mk, gk) < 2e-2
+    assert rel(mv, gv) < 2e-2
+
+
+def test_im2col_and_embed_grad():
+    B, img, P, D = 2, 32, 8, 64
+    g = img // P
+    N = g * g + 1
+    K = 3 * P * P
+    x = torch.randn(B, 3, img, img, device=DEV)
+    out = torch.empty(B * N, K, device=DEV, dtype=torch.bfloat16)
+    ops.im2col(x, out, B, img, P, K)
+    cols = x.unfold(2, P, P).unfold(3, P, P)  # B,3,g,g,P,P
+    cols = cols.permute(0, 2, 3, 1, 4, 5).reshape(B, g * g, K)
+    ref = torch.zeros(B, N, K, device=DEV)
+    ref[:, 1:] = cols
+    assert torch.equal(out.float(), ref.reshape(B * N, K).bfloat16().float())
+    dh0 = torch.randn(B * N, D, device=DEV)
+    dpos = torch.empty(N, D, device=DEV)
+    dcls = torch.empty(D, device=DEV)
+    dcb = torch.empty(D, device=DEV)
+    ops.embed_grad(dh0, B, N, D, dpos, dcls, dcb)
+    r = dh0.view(B, N, D).sum(0)
+    assert rel(dpos, r) < 1e-6
+    assert rel(dcls, r[0]) < 1e-6
+    assert rel(dcb, r[1:].sum(0)) < 1e-6
+
+
+def test_colsum_ce_gemm_f32_sgd():
+    x = torch.randn(5000, 300, device=DEV)
+    part = torch.empty(ops.colsum_partial_rows(5000), 300, device=DEV)
+    out = torch.empty(300, device=DEV)
+    ops.colsum(x, 5000, 300, 300, part, out)
+    assert rel(out, x.sum(0)) < 1e-5
+    xb = x.bfloat16()
+    ops.colsum(xb, 5000, 300, 300, part, out)
+    assert rel(out, xb.float().sum(0)) < 1e-5
+
+    logits = torch.randn(64, 1000, device=DEV) * 3
+    y = torch.randint(0, 1000, (64,), device=DEV)
+    dl = torch.empty_like(logits)
+    st = torch.empty(64, 3, device=DEV)
+    ops.cross_entropy(logits, y, dl, 1.0 / 64, st)
+    lr = logits.clone().requires_grad_(True)
+    loss = torch.nn.functional.cross_entropy(lr, y)
+    loss.backward()
+    assert abs(float(st[:, 0].mean()) - float(loss.detach())) < 1e-5
+    assert rel(dl, lr.grad) < 1e-5
+    top5 = logits.topk(5, 1).indices
+    assert float(st[:, 1].sum()) == float((top5[:, 0] == y).sum())
+    assert float(st[:, 2].sum()) == float((top5 == y[:, None]).any(1).sum())
+
+    A = torch.randn(70, 33, device=DEV)
+    Bm = torch.randn(50, 33, device=DEV)
+    bias = torch.randn(50, device=DEV)
+    C = torch.empty(70, 50, device=DEV)
+    ops.gemm_f32(70, 50, 33, A, 33, False, Bm, 33, True, C, 50, bias)
+    assert rel(C, A @ Bm.t() + bias) < 1e-5
+    C2 = torch.empty(33, 50, device=DEV)
+    ops.gemm_f32(33, 50, 70, A, 33, True, C, 50, False, C2, 50)
+    assert rel(C2, A.t() @ C) < 1e-5
+
+    n = 1003
+    p = torch.randn(n, device=DEV)
+    g = torch.randn(n, device=DEV)
+    buf = torch.zeros(n, device=DEV)
+    pb = torch.empty(n, device=DEV, dtype=torch.bfloat16)
+    p0 = p.clone()
+    ops.sgd_step(p, g, buf, pb, n, 0.1, 0.9, 1e-2, True)
+    d = g + 1e-2 * p0
+    assert rel(p, p0 - 0.1 * d) < 1e-6 and rel(buf, d) < 1e-6
+    assert torch.equal(pb, p.bfloat16())
+    p1 = p.clone()
+    ops.sgd_step(p, g, buf, pb, n, 0.1, 0.9, 1e-2, False)
+    d2 = 0.9 * d + g + 1e-2 * p1
+    assert rel(p, p1 - 0.1 * d2) < 1e-6

@@ -1,0 +1,67 @@
+// Shared device helpers for the gfx950 (CDNA4) ViT training kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+#include <stdio.h>
+#include <string>
+
+#include "../../include/vit_hip.h"
+
+typedef short v4s __attribute__((ext_vector_type(4)));
+typedef short v8s __attribute__((ext_vector_type(8)));
+typedef float v4f __attribute__((ext_vector_type(4)));
+typedef __bf16 v8bf __attribute__((ext_vector_type(8)));
+typedef unsigned short bf16_t;  // storage type for bf16 in HBM
+
+#define LDS_PTR(T, p) ((__attribute__((address_space(3))) T*)(p))
+
+__device__ __forceinline__ bf16_t f2bf(float x) {
+  __bf16 b = (__bf16)x;  // RNE, lowers to v_cvt_pk_bf16_f32 (NaN-preserving)
+  return __builtin_bit_cast(bf16_t, b);
+}
+__device__ __forceinline__ float bf2f(bf16_t u) { return __uint_as_float(((unsigned)u) << 16); }
+
+__device__ __forceinline__ unsigned pack2bf(float a, float b) {
+  return (unsigned)f2bf(a) | ((unsigned)f2bf(b) << 16);
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Exact-erf GELU (nn.GELU() default, reference src/model.py:33) and its derivative.
+__device__ __forceinline__ float gelu_f(float u) { return 0.5f * u * (1.0f + erff(u * 0.70710678118654752f)); }
+__device__ __forceinline__ float gelu_grad_f(float u) {
+  const float cdf = 0.5f * (1.0f + erff(u * 0.70710678118654752f));
+  const float pdf = 0.39894228040143268f * __expf(-0.5f * u * u);
+  return cdf + u * pdf;
+}
+
+// Buffer resource descriptor for raw buffer loads (out-of-range lanes read 0).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
+
+// ---- host-side error plumbing (thread-local last error, int status returns) ----
+namespace vit {
+void set_error(const char* fmt, ...);
+int check_hip(hipError_t e, const char* what);
+}  // namespace vit
+
+#define VIT_CHECK_ARG(cond, ...)                 \
+  do {                                           \
+    if (!(cond)) {                               \
+      vit::set_error(__VA_ARGS__);               \
+      return VIT_ERR_INVALID_ARG;                \
+    }                                            \
+  } while (0)
+
+#define VIT_LAUNCH_CHECK(what) return vit::check_hip(hipGetLastError(), what)

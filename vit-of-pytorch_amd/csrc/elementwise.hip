@@ -1,0 +1,334 @@
+// HBM-bound helper kernels of the ViT training step: patch im2col, embedding grads, column sums
+// (bias / LayerNorm-affine grads), the small f32 classifier GEMM, fused cross entropy + accuracy,
+// fused SGD-momentum with the bf16 weight mirror, and casts.
+#include "common.h"
+
+namespace {
+
+// ---- im2col for Conv2d(3, D, k=P, s=P) (reference src/model.py:179,197-200) ----------------------
+// out[b*N + 1 + py*g + px][c*P*P + ky*P + kx] = x[b][c][py*P+ky][px*P+kx]; cls rows and pad cols = 0.
+__global__ void im2col_kernel(const float* __restrict__ x, bf16_t* __restrict__ out, int B, int img, int P, int Kpad) {
+  const int g = img / P;
+  const int N = g * g + 1;
+  const long total = (long)B * N * Kpad;
+  const int K = 3 * P * P;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int col = (int)(i % Kpad);
+    const long row = i / Kpad;
+    const int t = (int)(row % N);
+    const int b = (int)(row / N);
+    float v = 0.f;
+    if (t > 0 && col < K) {
+      const int patch = t - 1, py = patch / g, px = patch % g;
+      const int c = col / (P * P), rem = col % (P * P), ky = rem / P, kx = rem % P;
+      v = x[(((long)b * 3 + c) * img + (py * P + ky)) * img + (px * P + kx)];
+    }
+    out[i] = f2bf(v);
+  }
+}
+
+// dpos[n][d] = sum_b dh0[(b*N+n)*D + d]
+__global__ void pos_grad_kernel(const float* __restrict__ dh0, int B, int N, int D, float* __restrict__ dpos) {
+  const int n = blockIdx.y;
+  const int d = blockIdx.x * blockDim.x + threadIdx.x;
+  if (d >= D) return;
+  float s = 0.f;
+  for (int b = 0; b < B; ++b) s += dh0[((long)b * N + n) * D + d];
+  dpos[(long)n * D + d] = s;
+}
+// dcls = dpos[0]; dconv_bias = sum_{n>=1} dpos[n]
+__global__ void cls_bias_grad_kernel(const float* __restrict__ dpos, int N, int D, float* __restrict__ dcls,
+                                     float* __restrict__ dbias) {
+  const int d = blockIdx.x * blockDim.x + threadIdx.x;
+  if (d >= D) return;
+  float s = 0.f;
+  for (int n = 1; n < N; ++n) s += dpos[(long)n * D + d];
+  dcls[d] = dpos[d];
+  dbias[d] = s;
+}
+
+// ---- column sums --------------------------------------------------------------------------------
+constexpr int COLSUM_ROWS_PER_CHUNK = 64;
+constexpr int COLSUM_MAX_CHUNKS = 512;
+
+__device__ __forceinline__ float ld_elem(const void* p, long i, int is_bf16) {
+  return is_bf16 ? bf2f(((const bf16_t*)p)[i]) : ((const float*)p)[i];
+}
+
+__global__ void colsum_partial_kernel(const void* __restrict__ in, int in_bf16, long rows, int cols, long ld,
+                                      int chunks, float* __restrict__ partial) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= cols) return;
+  const int ch = blockIdx.y;
+  const long per = (rows + chunks - 1) / chunks;
+  const long r0 = ch * per, r1 = r0 + per < rows ? r0 + per : rows;
+  float s = 0.f;
+  for (long r = r0; r < r1; ++r) s += ld_elem(in, r * ld + c, in_bf16);
+  partial[(long)ch * cols + c] = s;
+}
+__global__ void colsum_final_kernel(const float* __restrict__ partial, int chunks, int cols, float* __restrict__ out,
+                                    int accumulate) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= cols) return;
+  float s = 0.f;
+  for (int k = 0; k < chunks; ++k) s += partial[(long)k * cols + c];
+  out[c] = accumulate ? out[c] + s : s;
+}
+
+// ---- small f32 GEMM (classifier head) -----------------------------------------------------------
+__global__ void gemm_f32_kernel(int M, int N, int K, const float* __restrict__ A, long lda, int at,
+                                const float* __restrict__ B, long ldb, int bt, float* __restrict__ C, long ldc,
+                                const float* __restrict__ bias, int accumulate) {
+  __shared__ float As[16][17], Bs[16][17];
+  const int tx = threadIdx.x, ty = threadIdx.y;
+  const int m = blockIdx.y * 16 + ty, n = blockIdx.x * 16 + tx;
+  float acc = 0.f;
+  for (int k0 = 0; k0 < K; k0 += 16) {
+    {  // A tile: As[ty][tx] = A(m0+ty, k0+tx)
+      const int mm = blockIdx.y * 16 + ty, kk = k0 + tx;
+      As[ty][tx] = (mm < M && kk < K) ? (at ? A[(long)kk * lda + mm] : A[(long)mm * lda + kk]) : 0.f;
+    }
+    {  // B tile: Bs[ty][tx] = B(k0+ty, n0+tx)
+      const int kk = k0 + ty, nn = blockIdx.x * 16 + tx;
+      Bs[ty][tx] = (kk < K && nn < N) ? (bt ? B[(long)nn * ldb + kk] : B[(long)kk * ldb + nn]) : 0.f;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 16; ++k) acc += As[ty][k] * Bs[k][tx];
+    __syncthreads();
+  }
+  if (m < M && n < N) {
+    float v = acc + (bias ? bias[n] : 0.f);
+    float* dst = C + (long)m * ldc + n;
+    *dst = accumulate ? *dst + v : v;
+  }
+}
+
+// ---- cross entropy + top-1/top-5 (src/train.py:22, src/utils.py:28-41) -------------------------
+__global__ void __launch_bounds__(256) ce_kernel(const float* __restrict__ logits, const int64_t* __restrict__ labels,
+                                                 int C, float* __restrict__ dlogits, float grad_scale,
+                                                 float* __restrict__ row_stats) {
+  __shared__ float red[4];
+  __shared__ float red2[4];
+  const int b = blockIdx.x;
+  const float* x = logits + (long)b * C;
+  const int y = (int)labels[b];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float mx = -INFINITY;
+  for (int c = threadIdx.x; c < C; c += 256) mx = fmaxf(mx, x[c]);
+  mx = wave_max(mx);
+  if (lane == 0) red[wave] = mx;
+  __syncthreads();
+  mx = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  __syncthreads();
+  const float xy = x[y];
+  float s = 0.f, gt = 0.f;
+  for (int c = threadIdx.x; c < C; c += 256) {
+    s += __expf(x[c] - mx);
+    gt += x[c] > xy ? 1.f : 0.f;
+  }
+  s = wave_sum(s);
+  gt = wave_sum(gt);
+  if (lane == 0) {
+    red[wave] = s;
+    red2[wave] = gt;
+  }
+  __syncthreads();
+  s = red[0] + red[1] + red[2] + red[3];
+  gt = red2[0] + red2[1] + red2[2] + red2[3];
+  const float lse = mx + logf(s);
+  if (dlogits) {
+    for (int c = threadIdx.x; c < C; c += 256) {
+      const float p = __expf(x[c] - lse);
+      dlogits[(long)b * C + c] = (p - (c == y ? 1.f : 0.f)) * grad_scale;
+    }
+  }
+  if (threadIdx.x == 0 && row_stats) {
+    row_stats[b * 3 + 0] = lse - xy;
+    row_stats[b * 3 + 1] = gt < 1.f ? 1.f : 0.f;
+    row_stats[b * 3 + 2] = gt < 5.f ? 1.f : 0.f;
+  }
+}
+
+// ---- SGD momentum (torch.optim.SGD, dampening 0, no nesterov), src/train.py:154-158 -------------
+__global__ void sgd_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ buf,
+                           bf16_t* __restrict__ pb, long n, float lr, float mom, float wd, int first) {
+  const long n4 = n / 4;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
+    float4 pv = reinterpret_cast<float4*>(p)[i];
+    const float4 gv = reinterpret_cast<const float4*>(g)[i];
+    float4 d = make_float4(gv.x + wd * pv.x, gv.y + wd * pv.y, gv.z + wd * pv.z, gv.w + wd * pv.w);
+    if (!first) {
+      const float4 bv = reinterpret_cast<float4*>(buf)[i];
+      d = make_float4(mom * bv.x + d.x, mom * bv.y + d.y, mom * bv.z + d.z, mom * bv.w + d.w);
+    }
+    reinterpret_cast<float4*>(buf)[i] = d;
+    pv = make_float4(pv.x - lr * d.x, pv.y - lr * d.y, pv.z - lr * d.z, pv.w - lr * d.w);
+    reinterpret_cast<float4*>(p)[i] = pv;
+    if (pb) {
+      uint2 u;
+      u.x = pack2bf(pv.x, pv.y);
+      u.y = pack2bf(pv.z, pv.w);
+      reinterpret_cast<uint2*>(pb)[i] = u;
+    }
+  }
+  // tail
+  const long t = n4 * 4 + (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (blockIdx.x == 0 && t < n) {
+    float d = g[t] + wd * p[t];
+    if (!first) d = mom * buf[t] + d;
+    buf[t] = d;
+    p[t] -= lr * d;
+    if (pb) pb[t] = f2bf(p[t]);
+  }
+}
+
+__global__ void cast_kernel(const float* __restrict__ in, bf16_t* __restrict__ out, long n) {
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) out[i] = f2bf(in[i]);
+}
+__global__ void cast_pad_kernel(const float* __restrict__ in, long rows, long cols, bf16_t* __restrict__ out, long ldo) {
+  const long total = rows * ldo;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const long r = i / ldo, c = i % ldo;
+    out[i] = c < cols ? f2bf(in[r * cols + c]) : (bf16_t)0;
+  }
+}
+__global__ void axpby_kernel(const float* __restrict__ x, float* __restrict__ y, long n, float a, float b) {
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    y[i] = a * x[i] + (b == 0.f ? 0.f : b * y[i]);
+}
+
+unsigned grid_for(long n, int per_thread = 1) {
+  long b = (n / per_thread + 255) / 256;
+  if (b < 1) b = 1;
+  if (b > 8192) b = 8192;
+  return (unsigned)b;
+}
+
+}  // namespace
+
+extern "C" int vit_im2col(const float* x, void* out, int64_t B, int64_t img, int64_t P, int64_t Kpad,
+                          vit_stream_t stream) {
+  VIT_CHECK_ARG(x && out && B > 0 && P > 0 && img >= P && Kpad >= 3 * P * P, "vit_im2col: bad args");
+  const int64_t g = img / P, N = g * g + 1;
+  hipLaunchKernelGGL(im2col_kernel, dim3(grid_for(B * N * Kpad)), dim3(256), 0, (hipStream_t)stream, x, (bf16_t*)out,
+                     (int)B, (int)img, (int)P, (int)Kpad);
+  VIT_LAUNCH_CHECK("vit_im2col");
+}
+
+extern "C" int vit_embed_grad(const float* dh0, int64_t B, int64_t N, int64_t D, float* dpos, float* dcls,
+                              float* dconv_bias, vit_stream_t stream) {
+  VIT_CHECK_ARG(dh0 && dpos && dcls && dconv_bias && B > 0 && N > 0 && D > 0, "vit_embed_grad: bad args");
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(pos_grad_kernel, dim3((unsigned)((D + 255) / 256), (unsigned)N), dim3(256), 0, s, dh0, (int)B,
+                     (int)N, (int)D, dpos);
+  hipLaunchKernelGGL(cls_bias_grad_kernel, dim3((unsigned)((D + 255) / 256)), dim3(256), 0, s, dpos, (int)N, (int)D,
+                     dcls, dconv_bias);
+  VIT_LAUNCH_CHECK("vit_embed_grad");
+}
+
+extern "C" int64_t vit_colsum_partial_rows(int64_t rows) {
+  int64_t c = (rows + COLSUM_ROWS_PER_CHUNK - 1) / COLSUM_ROWS_PER_CHUNK;
+  if (c > COLSUM_MAX_CHUNKS) c = COLSUM_MAX_CHUNKS;
+  return c < 1 ? 1 : c;
+}
+
+extern "C" int vit_colsum(const void* in, int32_t in_bf16, int64_t rows, int64_t cols, int64_t ld, float* partial,
+                          float* out, int32_t accumulate, vit_stream_t stream) {
+  VIT_CHECK_ARG(in && partial && out && cols > 0 && ld >= cols, "vit_colsum: bad args");
+  hipStream_t s = (hipStream_t)stream;
+  const int chunks = (int)vit_colsum_partial_rows(rows);
+  const unsigned gx = (unsigned)((cols + 255) / 256);
+  hipLaunchKernelGGL(colsum_partial_kernel, dim3(gx, chunks), dim3(256), 0, s, in, (int)in_bf16, (long)rows, (int)cols,
+                     (long)ld, chunks, partial);
+  hipLaunchKernelGGL(colsum_final_kernel, dim3(gx), dim3(256), 0, s, partial, chunks, (int)cols, out, (int)accumulate);
+  VIT_LAUNCH_CHECK("vit_colsum");
+}
+
+extern "C" int vit_gemm_f32(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda, int32_t a_trans,
+                            const float* B, int64_t ldb, int32_t b_trans, float* C, int64_t ldc, const float* bias,
+                            int32_t accumulate, vit_stream_t stream) {
+  VIT_CHECK_ARG(A && B && C && M >= 0 && N >= 0 && K >= 0, "vit_gemm_f32: bad args");
+  if (M == 0 || N == 0) return VIT_OK;
+  dim3 grid((unsigned)((N + 15) / 16), (unsigned)((M + 15) / 16)), block(16, 16);
+  hipLaunchKernelGGL(gemm_f32_kernel, grid, block, 0, (hipStream_t)stream, (int)M, (int)N, (int)K, A, (long)lda,
+                     (int)a_trans, B, (long)ldb, (int)b_trans, C, (long)ldc, bias, (int)accumulate);
+  VIT_LAUNCH_CHECK("vit_gemm_f32");
+}
+
+extern "C" int vit_cross_entropy(const float* logits, const int64_t* labels, int64_t B, int64_t C, float* dlogits,
+                                 float grad_scale, float* row_stats, vit_stream_t stream) {
+  VIT_CHECK_ARG(logits && labels && B > 0 && C > 0, "vit_cross_entropy: bad args");
+  hipLaunchKernelGGL(ce_kernel, dim3((unsigned)B), dim3(256), 0, (hipStream_t)stream, logits, labels, (int)C, dlogits,
+                     grad_scale, row_stats);
+  VIT_LAUNCH_CHECK("vit_cross_entropy");
+}
+
+extern "C" int vit_sgd_step(float* p, const float* g, float* buf, void* p_bf16, int64_t n, float lr, float momentum,
+                            float weight_decay, int32_t first, vit_stream_t stream) {
+  VIT_CHECK_ARG(p && g && buf && n >= 0, "vit_sgd_step: bad args");
+  VIT_CHECK_ARG(((uintptr_t)p | (uintptr_t)g | (uintptr_t)buf) % 16 == 0 && ((uintptr_t)p_bf16 % 8 == 0),
+                "vit_sgd_step: buffers must be 16-B aligned (bf16 mirror 8-B)");
+  if (n == 0) return VIT_OK;
+  hipLaunchKernelGGL(sgd_kernel, dim3(grid_for(n, 4)), dim3(256), 0, (hipStream_t)stream, p, g, buf, (bf16_t*)p_bf16,
+                     (long)n, lr, momentum, weight_decay, (int)first);
+  VIT_LAUNCH_CHECK("vit_sgd_step");
+}
+
+extern "C" int vit_cast_f32_bf16(const float* in, void* out, int64_t n, vit_stream_t stream) {
+  VIT_CHECK_ARG(in && out && n >= 0, "vit_cast_f32_bf16: bad args");
+  if (n == 0) return VIT_OK;
+  hipLaunchKernelGGL(cast_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, in, (bf16_t*)out, (long)n);
+  VIT_LAUNCH_CHECK("vit_cast_f32_bf16");
+}
+
+extern "C" int vit_cast_pad_rows(const float* in, int64_t rows, int64_t cols, void* out, int64_t ldo,
+                                 vit_stream_t stream) {
+  VIT_CHECK_ARG(in && out && ldo >= cols, "vit_cast_pad_rows: bad args");
+  if (rows * ldo == 0) return VIT_OK;
+  hipLaunchKernelGGL(cast_pad_kernel, dim3(grid_for(rows * ldo)), dim3(256), 0, (hipStream_t)stream, in, (long)rows,
+                     (long)cols, (bf16_t*)out, (long)ldo);
+  VIT_LAUNCH_CHECK("vit_cast_pad_rows");
+}
+
+extern "C" int vit_axpby(const float* x, float* y, int64_t n, float a, float b, vit_stream_t stream) {
+  VIT_CHECK_ARG(x && y && n >= 0, "vit_axpby: bad args");
+  if (n == 0) return VIT_OK;
+  hipLaunchKernelGGL(axpby_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, x, y, (long)n, a, b);
+  VIT_LAUNCH_CHECK("vit_axpby");
+}
+
+// ---- column-block gather/cast: out[r][z*cols + c] = in[z*zstride + r*ldi + c] ------------------
+// Packs the q/k/v LinearGeneral weights [D][H,hd] x 3 into one [D][3D] bf16 operand (and the
+// biases into [3D] f32) so the fused QKV projection is a single GEMM.
+namespace {
+template <bool BF16OUT>
+__global__ void pack_cols_kernel(const float* __restrict__ in, long zstride, long ldi, int rows, int cols, int Z,
+                                 void* __restrict__ out, long ldo) {
+  const long total = (long)rows * Z * cols;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const long r = i / ((long)Z * cols);
+    const int zc = (int)(i % ((long)Z * cols));
+    const int z = zc / cols, c = zc % cols;
+    const float v = in[z * zstride + r * ldi + c];
+    if constexpr (BF16OUT)
+      ((bf16_t*)out)[r * ldo + zc] = f2bf(v);
+    else
+      ((float*)out)[r * ldo + zc] = v;
+  }
+}
+}  // namespace
+
+extern "C" int vit_pack_cols(const float* in, int64_t zstride, int64_t ldi, int64_t rows, int64_t cols, int64_t Z,
+                             void* out, int64_t ldo, int32_t out_bf16, vit_stream_t stream) {
+  VIT_CHECK_ARG(in && out && rows >= 0 && cols >= 0 && Z >= 1 && ldo >= Z * cols, "vit_pack_cols: bad args");
+  const long total = rows * Z * cols;
+  if (total == 0) return VIT_OK;
+  if (out_bf16)
+    hipLaunchKernelGGL(pack_cols_kernel<true>, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, in,
+                       (long)zstride, (long)ldi, (int)rows, (int)cols, (int)Z, out, (long)ldo);
+  else
+    hipLaunchKernelGGL(pack_cols_kernel<false>, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, in,
+                       (long)zstride, (long)ldi, (int)rows, (int)cols, (int)Z, out, (long)ldo);
+  VIT_LAUNCH_CHECK("vit_pack_cols");
+}

@@ -1,0 +1,338 @@
+// bf16 MFMA GEMM for gfx950 with fused ViT epilogues.
+//
+// Replaces the ATen GEMMs of the reference hot path (LinearGeneral tensordot src/model.py:61-63,
+// nn.Linear fc1/fc2 src/model.py:43-48, Conv2d patch embedding src/model.py:179,197) and their
+// autograd dgrad / wgrad (src/train.py:23).
+//
+// Design:
+//   * BM x BN x 64 workgroup tile, WM x WN waves, each wave a (BM/WM) x (BN/WN) sub-tile of
+//     v_mfma_f32_16x16x32_bf16 accumulators (fp32).
+//   * Operands are staged HBM -> LDS with LDS-DMA (buffer_load ... lds, 16 B per lane), two LDS
+//     stages: the load of k-tile t+1 is in flight while k-tile t is multiplied.
+//   * A K-contiguous operand is kept [rows][64] (128-B rows) with a 16-B-chunk XOR swizzle and is
+//     read with ds_read_b128. An M/N-contiguous operand is kept [64][rows] and read with the
+//     gfx950 transpose read ds_read_b64_tr_b16, with a 32-B-granule XOR swizzle. The swizzles are
+//     applied to the per-lane global SOURCE address (LDS-DMA writes lane-linearly).
+//   * Buffer descriptors bound every operand, so M/N tails read zeros instead of faulting.
+//   * XCD-aware bijective block remap so consecutive tiles (same A rows) share an XCD's L2.
+#include "common.h"
+
+namespace {
+
+struct GemmDev {
+  int M, N, K;
+  const char* A;
+  long lda;
+  long a_bs;
+  uint32_t a_bytes;  // valid bytes of one batch of A
+  const char* B;
+  long ldb;
+  long b_bs;
+  uint32_t b_bytes;
+  void* C;
+  long ldc;
+  long c_bs;
+  void* C2;
+  long ldc2;
+  const float* bias;
+  long bias_bs;
+  const void* aux;
+  long ldaux;
+  const float* aux2;
+  int split_k;
+  int tokens;
+};
+
+__device__ __forceinline__ int swz_k(int row) { return (row >> 1) & 7; }          // 16-B chunk xor
+__device__ __forceinline__ int swz_mn(int row) { return (row & 3) | (((row >> 3) & 1) << 2); }  // 32-B granule xor
+
+// Stage one operand tile (ROWS rows of the M/N dim x 64 k) into LDS at byte offset `lds_off`.
+template <int ROWS, bool KC, int NWAVE>
+__device__ __forceinline__ void stage_tile(char* smem, int lds_off, __amdgpu_buffer_rsrc_t rs, long ld,
+                                           int kt, int wave, int lane) {
+  constexpr int BYTES = ROWS * 128;
+  constexpr int INSTR = BYTES / 1024 / NWAVE;
+  static_assert(INSTR * 1024 * NWAVE == BYTES, "tile must split evenly over waves");
+#pragma unroll
+  for (int i = 0; i < INSTR; ++i) {
+    const int piece = i * NWAVE + wave;  // 1 KiB piece of the LDS image
+    const int c = piece * 64 + lane;     // 16-B chunk index in the image
+    int voff;
+    if constexpr (KC) {
+      // image [ROWS][64 k] : 8 chunks per row
+      const int r = c >> 3, pc = c & 7;
+      const int lc = pc ^ swz_k(r);
+      voff = (int)(r * ld * 2) + kt * 128 + lc * 16;
+    } else {
+      // image [64 k][ROWS] : ROWS*2 bytes per row
+      constexpr int CPR = ROWS * 2 / 16;
+      const int r = c / CPR, pc = c % CPR;
+      const int lb = (pc * 16) ^ (swz_mn(r) << 5);
+      voff = (int)((long)(kt * 64 + r) * ld * 2) + lb;
+    }
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, LDS_PTR(void, smem + lds_off + piece * 1024), 16, voff, 0, 0, 0);
+  }
+}
+
+// Read the 16x32 MFMA fragment (rows r0..r0+15, k = kk*32 .. kk*32+31) for this lane.
+template <int ROWS, bool KC>
+__device__ __forceinline__ v8s read_frag(const char* smem, int lds_off, int r0, int kk, int lane) {
+  if constexpr (KC) {
+    const int row = r0 + (lane & 15);
+    const int lc = kk * 4 + (lane >> 4);
+    const int pc = lc ^ swz_k(row);
+    return *reinterpret_cast<const v8s*>(smem + lds_off + row * 128 + pc * 16);
+  } else {
+    constexpr int RB = ROWS * 2;
+    const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+    const int col_b = (r0 + 4 * p) * 2;
+    const int ra = kk * 32 + 8 * g + q;
+    const int rb = ra + 4;
+    v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        LDS_PTR(v4s, smem + lds_off + ra * RB + (col_b ^ (swz_mn(ra) << 5))));
+    v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        LDS_PTR(v4s, smem + lds_off + rb * RB + (col_b ^ (swz_mn(rb) << 5))));
+    v8s r;
+    r.lo = lo;
+    r.hi = hi;
+    return r;
+  }
+}
+
+template <int EPI>
+__device__ __forceinline__ void epi_store(const GemmDev& p, int z, int split_idx, int m, int n, float v) {
+  if (m >= p.M || n >= p.N) return;
+  if constexpr (EPI == VIT_EPI_F32) {
+    float* C = (float*)p.C + z * p.c_bs;
+    C[(long)m * p.ldc + n] = v;
+  } else if constexpr (EPI == VIT_EPI_BF16) {
+    bf16_t* C = (bf16_t*)p.C + z * p.c_bs;
+    C[(long)m * p.ldc + n] = f2bf(v);
+  } else if constexpr (EPI == VIT_EPI_BIAS_BF16) {
+    bf16_t* C = (bf16_t*)p.C + z * p.c_bs;
+    const float b = p.bias ? p.bias[z * p.bias_bs + n] : 0.f;
+    C[(long)m * p.ldc + n] = f2bf(v + b);
+  } else if constexpr (EPI == VIT_EPI_BIAS_GELU) {
+    bf16_t* C = (bf16_t*)p.C + z * p.c_bs;
+    bf16_t* C2 = (bf16_t*)p.C2 + z * p.c_bs;
+    const float u = v + (p.bias ? p.bias[z * p.bias_bs + n] : 0.f);
+    C[(long)m * p.ldc + n] = f2bf(u);
+    C2[(long)m * p.ldc2 + n] = f2bf(gelu_f(u));
+  } else if constexpr (EPI == VIT_EPI_BIAS_RESID_F32) {
+    float* C = (float*)p.C + z * p.c_bs;
+    const float* R = (const float*)p.aux;
+    const float b = p.bias ? p.bias[z * p.bias_bs + n] : 0.f;
+    C[(long)m * p.ldc + n] = v + b + R[(long)m * p.ldaux + n];
+  } else if constexpr (EPI == VIT_EPI_GELU_BWD) {
+    bf16_t* C = (bf16_t*)p.C + z * p.c_bs;
+    const bf16_t* U = (const bf16_t*)p.aux;
+    C[(long)m * p.ldc + n] = f2bf(v * gelu_grad_f(bf2f(U[(long)m * p.ldaux + n])));
+  } else if constexpr (EPI == VIT_EPI_PATCH) {
+    float* C = (float*)p.C;
+    const float* pos = (const float*)p.aux;
+    const int t = m % p.tokens;
+    float o;
+    if (t == 0)
+      o = p.aux2[n] + pos[n];
+    else
+      o = v + p.bias[n] + pos[(long)t * p.ldaux + n];
+    C[(long)m * p.ldc + n] = o;
+  } else if constexpr (EPI == VIT_EPI_SPLITK) {
+    float* C = (float*)p.C + ((long)z * p.split_k + split_idx) * (long)p.M * p.N;
+    C[(long)m * p.N + n] = v;
+  }
+}
+
+template <int BM, int BN, int WM, int WN, bool AK, bool BKC, int EPI>
+__global__ void __launch_bounds__(WM* WN * 64) gemm_bf16_kernel(const GemmDev p) {
+  constexpr int NWAVE = WM * WN;
+  constexpr int TM = BM / WM, TN = BN / WN;
+  constexpr int FM = TM / 16, FN = TN / 16;
+  constexpr int A_BYTES = BM * 128, B_BYTES = BN * 128;
+  constexpr int STAGE = A_BYTES + B_BYTES;
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave / WN, wn = wave % WN;
+
+  // ---- tile scheduling: XCD-aware bijective remap of blockIdx.x ----
+  const int tiles_m = (p.M + BM - 1) / BM, tiles_n = (p.N + BN - 1) / BN;
+  const int nwg = tiles_m * tiles_n;
+  const int orig = blockIdx.x;
+  const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  const int tm = wg / tiles_n, tn = wg % tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int z = blockIdx.z;
+  const int split_idx = blockIdx.y;
+
+  // ---- operand descriptors (base moved to the block's first row/col) ----
+  const char* Ab = p.A + (long)z * p.a_bs * 2;
+  const char* Bb = p.B + (long)z * p.b_bs * 2;
+  long a_shift = AK ? (long)m0 * p.lda * 2 : (long)m0 * 2;
+  long b_shift = BKC ? (long)n0 * p.ldb * 2 : (long)n0 * 2;
+  const uint32_t a_rec = (long)p.a_bytes > a_shift ? (uint32_t)(p.a_bytes - a_shift) : 0u;
+  const uint32_t b_rec = (long)p.b_bytes > b_shift ? (uint32_t)(p.b_bytes - b_shift) : 0u;
+  const __amdgpu_buffer_rsrc_t rsA = make_rsrc(Ab + a_shift, a_rec);
+  const __amdgpu_buffer_rsrc_t rsB = make_rsrc(Bb + b_shift, b_rec);
+
+  // ---- k range of this split ----
+  const int nkt = p.K / 64;
+  const int kt0 = (int)((long)nkt * split_idx / p.split_k);
+  const int kt1 = (int)((long)nkt * (split_idx + 1) / p.split_k);
+  const int nk = kt1 - kt0;
+
+  v4f acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+
+  const int wm0 = wm * TM, wn0 = wn * TN;
+
+  if (nk > 0) {
+    stage_tile<BM, AK, NWAVE>(smem, 0, rsA, p.lda, kt0, wave, lane);
+    stage_tile<BN, BKC, NWAVE>(smem, A_BYTES, rsB, p.ldb, kt0, wave, lane);
+  }
+  for (int t = 0; t < nk; ++t) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const int cur = (t & 1) * STAGE;
+    if (t + 1 < nk) {
+      const int nxt = ((t + 1) & 1) * STAGE;
+      stage_tile<BM, AK, NWAVE>(smem, nxt, rsA, p.lda, kt0 + t + 1, wave, lane);
+      stage_tile<BN, BKC, NWAVE>(smem, nxt + A_BYTES, rsB, p.ldb, kt0 + t + 1, wave, lane);
+    }
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      v8s af[FM], bfr[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) af[i] = read_frag<BM, AK>(smem, cur, wm0 + i * 16, kk, lane);
+#pragma unroll
+      for (int j = 0; j < FN; ++j) bfr[j] = read_frag<BN, BKC>(smem, cur + A_BYTES, wn0 + j * 16, kk, lane);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(v8bf, af[i]),
+                                                              __builtin_bit_cast(v8bf, bfr[j]), acc[i][j], 0, 0, 0);
+    }
+  }
+
+  // ---- epilogue: C[m0+wm0+16i+4g+r][n0+wn0+16j+(lane&15)] ----
+  const int g = lane >> 4, c = lane & 15;
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        epi_store<EPI>(p, z, split_idx, m0 + wm0 + i * 16 + 4 * g + r, n0 + wn0 + j * 16 + c, acc[i][j][r]);
+}
+
+template <int BM, int BN, int WM, int WN, bool AK, bool BKC, int EPI>
+hipError_t launch_t(const GemmDev& d, int batch, int split, hipStream_t s) {
+  const int tiles = ((d.M + BM - 1) / BM) * ((d.N + BN - 1) / BN);
+  dim3 grid(tiles, split, batch);
+  hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, WM, WN, AK, BKC, EPI>), grid, dim3(WM * WN * 64), 0, s, d);
+  return hipGetLastError();
+}
+
+template <int EPI>
+hipError_t launch_layout(const GemmDev& d, bool ak, bool bk, int batch, int split, hipStream_t s) {
+  if (ak && bk) return launch_t<128, 128, 2, 2, true, true, EPI>(d, batch, split, s);
+  if (ak && !bk) return launch_t<128, 128, 2, 2, true, false, EPI>(d, batch, split, s);
+  if (!ak && !bk) return launch_t<128, 128, 2, 2, false, false, EPI>(d, batch, split, s);
+  return launch_t<128, 128, 2, 2, false, true, EPI>(d, batch, split, s);
+}
+
+}  // namespace
+
+extern "C" int vit_gemm_bf16(const vit_gemm_args* a, vit_stream_t stream) {
+  VIT_CHECK_ARG(a != nullptr, "vit_gemm_bf16: null args");
+  VIT_CHECK_ARG(a->M >= 0 && a->N >= 0 && a->K >= 0, "vit_gemm_bf16: negative size");
+  VIT_CHECK_ARG(a->K % 64 == 0, "vit_gemm_bf16: K=%lld must be a multiple of 64", (long long)a->K);
+  VIT_CHECK_ARG(a->M < (1 << 30) && a->N < (1 << 30), "vit_gemm_bf16: M/N too large");
+  VIT_CHECK_ARG(a->A && a->B && a->C, "vit_gemm_bf16: null operand");
+  VIT_CHECK_ARG(a->batch >= 1 && a->split_k >= 1, "vit_gemm_bf16: batch/split_k must be >= 1");
+  VIT_CHECK_ARG(a->split_k == 1 || a->epilogue == VIT_EPI_SPLITK, "vit_gemm_bf16: split_k>1 needs VIT_EPI_SPLITK");
+  VIT_CHECK_ARG(a->a_layout == VIT_K_CONTIG || a->a_layout == VIT_MN_CONTIG, "vit_gemm_bf16: bad a_layout");
+  VIT_CHECK_ARG(a->b_layout == VIT_K_CONTIG || a->b_layout == VIT_MN_CONTIG, "vit_gemm_bf16: bad b_layout");
+  if (a->M == 0 || a->N == 0) return VIT_OK;
+  const bool ak = a->a_layout == VIT_K_CONTIG, bk = a->b_layout == VIT_K_CONTIG;
+  // valid extents (bytes) of one batch of each operand
+  const long a_rows = ak ? a->M : a->K, a_cols = ak ? a->K : a->M;
+  const long b_rows = bk ? a->N : a->K, b_cols = bk ? a->K : a->N;
+  VIT_CHECK_ARG(a->lda >= a_cols && a->ldb >= b_cols, "vit_gemm_bf16: leading dimension too small");
+  // 16-B granularity of the LDS-DMA loads: rows must start 16-B aligned, and the last row is read
+  // up to its next 16-B boundary (which lies inside the row stride).
+  VIT_CHECK_ARG(a->lda % 8 == 0 && a->ldb % 8 == 0, "vit_gemm_bf16: lda/ldb must be multiples of 8");
+  VIT_CHECK_ARG(((uintptr_t)a->A | (uintptr_t)a->B) % 16 == 0 && (a->a_batch_stride | a->b_batch_stride) % 8 == 0,
+                "vit_gemm_bf16: A/B must be 16-byte aligned");
+  const long a_bytes = ((a_rows - 1) * a->lda + ((a_cols + 7) & ~7L)) * 2;
+  const long b_bytes = ((b_rows - 1) * a->ldb + ((b_cols + 7) & ~7L)) * 2;
+  VIT_CHECK_ARG(a_bytes < (1L << 31) && b_bytes < (1L << 31), "vit_gemm_bf16: operand larger than 2 GiB");
+  switch (a->epilogue) {
+    case VIT_EPI_BIAS_GELU: VIT_CHECK_ARG(a->C2 != nullptr, "GELU epilogue needs C2"); break;
+    case VIT_EPI_BIAS_RESID_F32: VIT_CHECK_ARG(a->aux != nullptr, "RESID epilogue needs aux"); break;
+    case VIT_EPI_GELU_BWD: VIT_CHECK_ARG(a->aux != nullptr, "GELU_BWD epilogue needs aux"); break;
+    case VIT_EPI_PATCH:
+      VIT_CHECK_ARG(a->aux && a->aux2 && a->bias && a->tokens > 0 && a->batch == 1, "PATCH epilogue args");
+      break;
+    default: break;
+  }
+  GemmDev d;
+  d.M = (int)a->M; d.N = (int)a->N; d.K = (int)a->K;
+  d.A = (const char*)a->A; d.lda = a->lda; d.a_bs = a->a_batch_stride; d.a_bytes = (uint32_t)a_bytes;
+  d.B = (const char*)a->B; d.ldb = a->ldb; d.b_bs = a->b_batch_stride; d.b_bytes = (uint32_t)b_bytes;
+  d.C = a->C; d.ldc = a->ldc; d.c_bs = a->c_batch_stride;
+  d.C2 = a->C2; d.ldc2 = a->ldc2;
+  d.bias = a->bias; d.bias_bs = a->bias_batch_stride;
+  d.aux = a->aux; d.ldaux = a->ldaux; d.aux2 = a->aux2;
+  d.split_k = (int)a->split_k; d.tokens = (int)a->tokens;
+  hipStream_t s = (hipStream_t)stream;
+  const int batch = (int)a->batch, split = (int)a->split_k;
+  hipError_t e;
+  switch (a->epilogue) {
+    case VIT_EPI_F32: e = launch_layout<VIT_EPI_F32>(d, ak, bk, batch, split, s); break;
+    case VIT_EPI_BF16: e = launch_layout<VIT_EPI_BF16>(d, ak, bk, batch, split, s); break;
+    case VIT_EPI_BIAS_BF16: e = launch_layout<VIT_EPI_BIAS_BF16>(d, ak, bk, batch, split, s); break;
+    case VIT_EPI_BIAS_GELU: e = launch_layout<VIT_EPI_BIAS_GELU>(d, ak, bk, batch, split, s); break;
+    case VIT_EPI_BIAS_RESID_F32: e = launch_layout<VIT_EPI_BIAS_RESID_F32>(d, ak, bk, batch, split, s); break;
+    case VIT_EPI_GELU_BWD: e = launch_layout<VIT_EPI_GELU_BWD>(d, ak, bk, batch, split, s); break;
+    case VIT_EPI_PATCH: e = launch_layout<VIT_EPI_PATCH>(d, ak, bk, batch, split, s); break;
+    case VIT_EPI_SPLITK: e = launch_layout<VIT_EPI_SPLITK>(d, ak, bk, batch, split, s); break;
+    default: vit::set_error("vit_gemm_bf16: unknown epilogue %d", a->epilogue); return VIT_ERR_INVALID_ARG;
+  }
+  return vit::check_hip(e, "vit_gemm_bf16 launch");
+}
+
+// ---- split-K reduction -------------------------------------------------------------------------
+namespace {
+__global__ void splitk_reduce_kernel(const float* __restrict__ ws, int split, long M, long N, float* __restrict__ out,
+                                     long ldo, long obs, int accumulate) {
+  const int z = blockIdx.y;
+  const long total = M * N;
+  const float* w = ws + (long)z * split * total;
+  float* o = out + z * obs;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    float s = 0.f;
+    for (int k = 0; k < split; ++k) s += w[k * total + i];
+    const long m = i / N, n = i - m * N;
+    float* dst = o + m * ldo + n;
+    *dst = accumulate ? *dst + s : s;
+  }
+}
+}  // namespace
+
+extern "C" int vit_splitk_reduce(const float* ws, int64_t batch, int64_t split, int64_t M, int64_t N, float* out,
+                                 int64_t ldo, int64_t out_batch_stride, int32_t accumulate, vit_stream_t stream) {
+  VIT_CHECK_ARG(ws && out && batch >= 1 && split >= 1 && ldo >= N, "vit_splitk_reduce: bad args");
+  if (M * N == 0) return VIT_OK;
+  long blocks = (M * N + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)blocks, (unsigned)batch), dim3(256), 0, (hipStream_t)stream, ws,
+                     (int)split, (long)M, (long)N, out, (long)ldo, (long)out_batch_stride, (int)accumulate);
+  VIT_LAUNCH_CHECK("vit_splitk_reduce");
+}

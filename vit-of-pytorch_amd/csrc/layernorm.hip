@@ -1,0 +1,217 @@
+// LayerNorm forward/backward (nn.LayerNorm(D), eps 1e-5, reference src/model.py:108,114,146).
+// One wavefront per row, the row held in registers as float4 chunks (HBM-bound kernels: each
+// row is read once and written once; 16-B loads per lane). Statistics in fp32.
+#include "common.h"
+
+namespace {
+
+// NV = float4 chunks per lane (D <= NV * 256).
+template <int NV>
+__global__ void __launch_bounds__(256) ln_fwd_kernel(const float* __restrict__ x, long ldx, const float* __restrict__ gamma,
+                                                     const float* __restrict__ beta, void* __restrict__ y, long ldy,
+                                                     int y_f32, float* __restrict__ mean, float* __restrict__ rstd,
+                                                     int rows, int D, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const float* xr = x + (long)row * ldx;
+  float4 v[NV];
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const int c = (k * 64 + lane) * 4;
+    if (c < D) {
+      v[k] = *reinterpret_cast<const float4*>(xr + c);
+      s += v[k].x + v[k].y + v[k].z + v[k].w;
+    } else {
+      v[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
+  const float mu = wave_sum(s) / D;
+  float ss = 0.f;
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const int c = (k * 64 + lane) * 4;
+    if (c < D) {
+      const float a = v[k].x - mu, b = v[k].y - mu, cc = v[k].z - mu, d = v[k].w - mu;
+      ss += a * a + b * b + cc * cc + d * d;
+    }
+  }
+  const float var = wave_sum(ss) / D;
+  const float rs = rsqrtf(var + eps);
+  if (lane == 0) {
+    mean[row] = mu;
+    rstd[row] = rs;
+  }
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const int c = (k * 64 + lane) * 4;
+    if (c < D) {
+      const float4 gm = *reinterpret_cast<const float4*>(gamma + c);
+      const float4 bt = *reinterpret_cast<const float4*>(beta + c);
+      const float o0 = (v[k].x - mu) * rs * gm.x + bt.x;
+      const float o1 = (v[k].y - mu) * rs * gm.y + bt.y;
+      const float o2 = (v[k].z - mu) * rs * gm.z + bt.z;
+      const float o3 = (v[k].w - mu) * rs * gm.w + bt.w;
+      if (y_f32) {
+        *reinterpret_cast<float4*>((float*)y + (long)row * ldy + c) = make_float4(o0, o1, o2, o3);
+      } else {
+        uint2 u;
+        u.x = pack2bf(o0, o1);
+        u.y = pack2bf(o2, o3);
+        *reinterpret_cast<uint2*>((bf16_t*)y + (long)row * ldy + c) = u;
+      }
+    }
+  }
+}
+
+constexpr int LN_BWD_MAX_BLOCKS = 1024;
+
+template <int NV>
+__global__ void __launch_bounds__(256) ln_bwd_kernel(const void* __restrict__ dy, long lddy, int dy_f32,
+                                                     const float* __restrict__ x, long ldx, const float* __restrict__ mean,
+                                                     const float* __restrict__ rstd, const float* __restrict__ gamma,
+                                                     const float* __restrict__ dres, long lddres, float* __restrict__ dx,
+                                                     long lddx, bf16_t* __restrict__ dxb, long lddxb,
+                                                     float* __restrict__ partial, int rows, int D) {
+  __shared__ float red[4][2][NV * 256];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float4 pg[NV], pb[NV];
+  float4 gm[NV];
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    pg[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+    pb[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+    const int c = (k * 64 + lane) * 4;
+    gm[k] = c < D ? *reinterpret_cast<const float4*>(gamma + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  for (int row = blockIdx.x * 4 + wave; row < rows; row += gridDim.x * 4) {
+    const float mu = mean[row], rs = rstd[row];
+    float4 xh[NV], g[NV];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int c = (k * 64 + lane) * 4;
+      if (c < D) {
+        float4 d4;
+        if (dy_f32) {
+          d4 = *reinterpret_cast<const float4*>((const float*)dy + (long)row * lddy + c);
+        } else {
+          const uint2 u = *reinterpret_cast<const uint2*>((const bf16_t*)dy + (long)row * lddy + c);
+          d4 = make_float4(bf2f(u.x & 0xffff), bf2f(u.x >> 16), bf2f(u.y & 0xffff), bf2f(u.y >> 16));
+        }
+        const float4 x4 = *reinterpret_cast<const float4*>(x + (long)row * ldx + c);
+        xh[k] = make_float4((x4.x - mu) * rs, (x4.y - mu) * rs, (x4.z - mu) * rs, (x4.w - mu) * rs);
+        g[k] = make_float4(d4.x * gm[k].x, d4.y * gm[k].y, d4.z * gm[k].z, d4.w * gm[k].w);
+        s1 += g[k].x + g[k].y + g[k].z + g[k].w;
+        s2 += g[k].x * xh[k].x + g[k].y * xh[k].y + g[k].z * xh[k].z + g[k].w * xh[k].w;
+        pg[k].x += d4.x * xh[k].x; pg[k].y += d4.y * xh[k].y; pg[k].z += d4.z * xh[k].z; pg[k].w += d4.w * xh[k].w;
+        pb[k].x += d4.x; pb[k].y += d4.y; pb[k].z += d4.z; pb[k].w += d4.w;
+      } else {
+        xh[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+        g[k] = xh[k];
+      }
+    }
+    const float m1 = wave_sum(s1) / D, m2 = wave_sum(s2) / D;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int c = (k * 64 + lane) * 4;
+      if (c < D) {
+        float4 o;
+        o.x = rs * (g[k].x - m1 - xh[k].x * m2);
+        o.y = rs * (g[k].y - m1 - xh[k].y * m2);
+        o.z = rs * (g[k].z - m1 - xh[k].z * m2);
+        o.w = rs * (g[k].w - m1 - xh[k].w * m2);
+        if (dres) {
+          const float4 r4 = *reinterpret_cast<const float4*>(dres + (long)row * lddres + c);
+          o.x += r4.x; o.y += r4.y; o.z += r4.z; o.w += r4.w;
+        }
+        *reinterpret_cast<float4*>(dx + (long)row * lddx + c) = o;
+        if (dxb) {
+          uint2 u;
+          u.x = pack2bf(o.x, o.y);
+          u.y = pack2bf(o.z, o.w);
+          *reinterpret_cast<uint2*>(dxb + (long)row * lddxb + c) = u;
+        }
+      }
+    }
+  }
+  // block partials of dgamma (sum dy*xhat) and dbeta (sum dy)
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const int c = (k * 64 + lane) * 4;
+    *reinterpret_cast<float4*>(&red[wave][0][c]) = pg[k];
+    *reinterpret_cast<float4*>(&red[wave][1][c]) = pb[k];
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < D; c += 256) {
+    float a = 0.f, b = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      a += red[w][0][c];
+      b += red[w][1][c];
+    }
+    partial[(long)blockIdx.x * 2 * D + c] = a;
+    partial[(long)blockIdx.x * 2 * D + D + c] = b;
+  }
+}
+
+int nv_for(int64_t D) { return (int)((D + 255) / 256); }
+
+}  // namespace
+
+extern "C" int vit_layernorm_fwd(const float* x, int64_t ldx, const float* gamma, const float* beta, void* y,
+                                 int64_t ldy, int32_t y_f32, float* mean, float* rstd, int64_t rows, int64_t D,
+                                 float eps, vit_stream_t stream) {
+  VIT_CHECK_ARG(x && gamma && beta && y && mean && rstd, "vit_layernorm_fwd: null pointer");
+  VIT_CHECK_ARG(D > 0 && D % 4 == 0 && D <= 2048, "vit_layernorm_fwd: D=%lld unsupported", (long long)D);
+  VIT_CHECK_ARG(ldx % 4 == 0 && ldy % 4 == 0, "vit_layernorm_fwd: strides must be multiples of 4");
+  if (rows <= 0) return VIT_OK;
+  dim3 grid((unsigned)((rows + 3) / 4)), block(256);
+  hipStream_t s = (hipStream_t)stream;
+  switch (nv_for(D)) {
+#define C(n) \
+  case n: hipLaunchKernelGGL(ln_fwd_kernel<n>, grid, block, 0, s, x, (long)ldx, gamma, beta, y, (long)ldy, (int)y_f32, mean, rstd, (int)rows, (int)D, eps); break;
+    C(1) C(2) C(3) C(4) C(5) C(6) C(7) C(8)
+#undef C
+  }
+  VIT_LAUNCH_CHECK("vit_layernorm_fwd");
+}
+
+static int64_t ln_bwd_blocks(int64_t rows) {
+  int64_t b = (rows + 3) / 4;
+  if (b > LN_BWD_MAX_BLOCKS) b = LN_BWD_MAX_BLOCKS;
+  return b < 1 ? 1 : b;
+}
+
+// rows of 2*D floats the `partial` workspace must hold (block partials + their column reduction)
+extern "C" int64_t vit_layernorm_bwd_partial_rows(int64_t rows) {
+  const int64_t nb = ln_bwd_blocks(rows);
+  return nb + vit_colsum_partial_rows(nb);
+}
+
+extern "C" int vit_layernorm_bwd(const void* dy, int64_t lddy, int32_t dy_f32, const float* x, int64_t ldx,
+                                 const float* mean, const float* rstd, const float* gamma, const float* dres,
+                                 int64_t lddres, float* dx, int64_t lddx, void* dx_bf16, int64_t lddxb, float* partial,
+                                 float* dgamma_dbeta, int32_t accumulate_params, int64_t rows, int64_t D,
+                                 vit_stream_t stream) {
+  VIT_CHECK_ARG(dy && x && mean && rstd && gamma && dx && partial, "vit_layernorm_bwd: null pointer");
+  VIT_CHECK_ARG(D > 0 && D % 4 == 0 && D <= 2048, "vit_layernorm_bwd: D=%lld unsupported", (long long)D);
+  if (rows <= 0) return VIT_OK;
+  const int64_t nblk = ln_bwd_blocks(rows);
+  hipStream_t s = (hipStream_t)stream;
+  switch (nv_for(D)) {
+#define C(n)                                                                                                        \
+  case n:                                                                                                           \
+    hipLaunchKernelGGL(ln_bwd_kernel<n>, dim3((unsigned)nblk), dim3(256), 0, s, dy, (long)lddy, (int)dy_f32, x,     \
+                       (long)ldx, mean, rstd, gamma, dres, (long)lddres, dx, (long)lddx, (bf16_t*)dx_bf16,           \
+                       (long)lddxb, partial, (int)rows, (int)D);                                                    \
+    break;
+    C(1) C(2) C(3) C(4) C(5) C(6) C(7) C(8)
+#undef C
+  }
+  int st = vit::check_hip(hipGetLastError(), "vit_layernorm_bwd");
+  if (st || !dgamma_dbeta) return st;
+  // reduce the block partials into [dgamma | dbeta]
+  return vit_colsum(partial, 0, nblk, 2 * D, 2 * D, partial + nblk * 2 * D, dgamma_dbeta, accumulate_params, stream);
+}

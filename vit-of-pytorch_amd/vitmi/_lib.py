@@ -1,0 +1,94 @@
+"""ctypes binding of libvit_hip.so (the C ABI declared in include/vit_hip.h).
+
+The library is built in-tree by `make -C vit-of-pytorch_amd` (or __graft_entry__.build()).
+There is no fallback: if the library is missing, importing the GPU ops raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libvit_hip.so")
+
+c_i64 = ctypes.c_int64
+c_i32 = ctypes.c_int32
+c_f32 = ctypes.c_float
+c_vp = ctypes.c_void_p
+
+# enum vit_layout / vit_epilogue (include/vit_hip.h)
+K_CONTIG, MN_CONTIG = 0, 1
+EPI_F32, EPI_BF16, EPI_BIAS_BF16, EPI_BIAS_GELU, EPI_BIAS_RESID_F32, EPI_GELU_BWD, EPI_PATCH, EPI_SPLITK = range(8)
+
+
+class GemmArgs(ctypes.Structure):
+    _fields_ = [
+        ("M", c_i64), ("N", c_i64), ("K", c_i64),
+        ("A", c_vp), ("lda", c_i64), ("a_batch_stride", c_i64),
+        ("a_layout", c_i32), ("b_layout", c_i32),
+        ("B", c_vp), ("ldb", c_i64), ("b_batch_stride", c_i64),
+        ("C", c_vp), ("ldc", c_i64), ("c_batch_stride", c_i64),
+        ("C2", c_vp), ("ldc2", c_i64),
+        ("bias", c_vp), ("bias_batch_stride", c_i64),
+        ("aux", c_vp), ("ldaux", c_i64), ("aux2", c_vp),
+        ("batch", c_i64), ("split_k", c_i64), ("tokens", c_i64),
+        ("epilogue", c_i32), ("tile", c_i32),
+    ]
+
+
+# name -> (restype, argtypes)
+_SIGS = {
+    "vit_last_error": (ctypes.c_char_p, []),
+    "vit_abi_version": (c_i32, []),
+    "vit_gemm_bf16": (c_i32, [ctypes.POINTER(GemmArgs), c_vp]),
+    "vit_splitk_reduce": (c_i32, [c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_i64, c_i64, c_i32, c_vp]),
+    "vit_layernorm_fwd": (c_i32, [c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_i32, c_vp, c_vp, c_i64, c_i64, c_f32, c_vp]),
+    "vit_layernorm_bwd_partial_rows": (c_i64, [c_i64]),
+    "vit_layernorm_bwd": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_i64,
+                                  c_vp, c_i64, c_vp, c_vp, c_i32, c_i64, c_i64, c_vp]),
+    "vit_attention_fwd": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_f32, c_vp]),
+    "vit_attention_bwd": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_f32, c_vp]),
+    "vit_im2col": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp]),
+    "vit_embed_grad": (c_i32, [c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp]),
+    "vit_colsum_partial_rows": (c_i64, [c_i64]),
+    "vit_colsum": (c_i32, [c_vp, c_i32, c_i64, c_i64, c_i64, c_vp, c_vp, c_i32, c_vp]),
+    "vit_gemm_f32": (c_i32, [c_i64, c_i64, c_i64, c_vp, c_i64, c_i32, c_vp, c_i64, c_i32, c_vp, c_i64, c_vp, c_i32,
+                             c_vp]),
+    "vit_cross_entropy": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_vp, c_f32, c_vp, c_vp]),
+    "vit_sgd_step": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_i64, c_f32, c_f32, c_f32, c_i32, c_vp]),
+    "vit_cast_f32_bf16": (c_i32, [c_vp, c_vp, c_i64, c_vp]),
+    "vit_cast_pad_rows": (c_i32, [c_vp, c_i64, c_i64, c_vp, c_i64, c_vp]),
+    "vit_axpby": (c_i32, [c_vp, c_vp, c_i64, c_f32, c_f32, c_vp]),
+    "vit_pack_cols": (c_i32, [c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp, c_i64, c_i32, c_vp]),
+}
+
+EXPORTED = tuple(_SIGS)
+
+_lib = None
+
+
+class VitHipError(RuntimeError):
+    pass
+
+
+def load(path: str | None = None):
+    """Load the library once and attach prototypes. Raises if it is missing (no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise VitHipError(f"libvit_hip.so not built ({p}); run `make -C vit-of-pytorch_amd` or __graft_entry__.build()")
+    lib = ctypes.CDLL(p)
+    for name, (res, args) in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(status: int, what: str):
+    if status != 0:
+        msg = _lib.vit_last_error().decode(errors="replace") if _lib is not None else "?"
+        raise VitHipError(f"{what} failed (status {status}): {msg}")

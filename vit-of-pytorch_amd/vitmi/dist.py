@@ -1,0 +1,70 @@
+"""Data parallelism: one process per GPU, gradient all-reduce over RCCL (xGMI), overlapped with backward.
+
+Replaces the reference's single-process torch.nn.DataParallel (src/train.py:128-129), whose
+per-step parameter broadcast + reduce-to-GPU0 star is the wrong shape for point-to-point xGMI.
+Every rank keeps a full persistent replica; the engine's flat gradient buffer is laid out in
+backward-completion order, so each encoder layer's gradients form one contiguous bucket that is
+all-reduced on a side stream as soon as the engine's backward releases it (grad_ready_hook),
+while the backward of the layers below keeps running on the compute stream.
+
+Gradient scaling: each rank's cross entropy is scaled by 1/(b * world), the buckets are summed,
+which equals the global-batch mean gradient of the reference's DataParallel CE (computed on the
+gathered batch). Replicas stay bit-identical because every rank applies the same SGD update to the
+same all-reduced gradient.
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+
+class GradAllReducer:
+    def __init__(self, engine, group=None, min_bucket_elems=1 << 20):
+        self.engine = engine
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.cuda = engine.dev.type == "cuda"
+        self.stream = torch.cuda.Stream(device=engine.dev) if self.cuda else None
+        self.min_bucket = min_bucket_elems
+        self._pending = None  # (buf, start) of a bucket being coalesced with the next one
+        self._works = []
+
+    def attach(self):
+        self.engine.grad_ready_hook = self.hook
+        return self
+
+    def detach(self):
+        self.engine.grad_ready_hook = None
+
+    def _launch(self, buf, start, end):
+        t = buf[start:end]
+        if self.cuda:
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(self.engine.dev))
+            self.stream.wait_event(ev)
+            with torch.cuda.stream(self.stream):
+                dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
+        else:
+            self._works.append(dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group, async_op=True))
+
+    def hook(self, buf, name, start, end):
+        if self.world == 1:
+            return
+        if self._pending is not None:
+            start = self._pending
+            self._pending = None
+        if end - start < self.min_bucket and name != "embed":
+            self._pending = start  # coalesce small buckets (head) with the next layer's
+            return
+        self._launch(buf, start, end)
+
+    def finish(self):
+        """Make the compute stream wait for every outstanding all-reduce."""
+        if self.world == 1:
+            return
+        if self.cuda:
+            torch.cuda.current_stream(self.engine.dev).wait_stream(self.stream)
+        else:
+            for w in self._works:
+                w.wait()
+            self._works = []

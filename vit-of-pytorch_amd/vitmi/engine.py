@@ -1,0 +1,400 @@
+"""ViT training-step engine: runs forward and backward of the whole network on libvit_hip.so.
+
+This is the host-side orchestration of the hot path (reference src/model.py:196-211 forward,
+autograd backward at src/train.py:23). Design:
+
+* Parameters live in ONE flat fp32 buffer (`flat`) whose order is the order in which the
+  backward finishes their gradients: classifier, final LayerNorm, encoder layers L-1 .. 0,
+  embedding. The nn.Parameters of vitmi.model are views into it, the gradient buffer has the
+  same layout, so data-parallel all-reduce buckets are contiguous slices released layer by layer.
+* A bf16 mirror of `flat` (same offsets) feeds the MFMA GEMMs; q/k/v weights are additionally
+  packed to one [D][3D] operand per layer so the QKV projection is a single GEMM.
+* Activations are kept per layer (bf16 GEMM operands, fp32 residual stream and LN stats); rows
+  are padded to a multiple of 64 with zeros so the weight-gradient GEMMs (K = tokens) need no
+  tail handling.
+"""
+from __future__ import annotations
+
+import math
+from collections import OrderedDict
+from dataclasses import dataclass
+
+import torch
+
+from . import ops
+from ._lib import (EPI_BF16, EPI_BIAS_BF16, EPI_BIAS_GELU, EPI_BIAS_RESID_F32, EPI_GELU_BWD, EPI_PATCH, EPI_SPLITK,
+                   K_CONTIG, MN_CONTIG)
+
+ALIGN = 64  # elements; every parameter starts 256-B aligned in the flat buffers
+
+
+def _rup(x, m):
+    return (x + m - 1) // m * m
+
+
+@dataclass(frozen=True)
+class ArchConfig:
+    image_size: int = 224
+    patch_size: int = 16
+    emb_dim: int = 768
+    mlp_dim: int = 3072
+    num_heads: int = 12
+    num_layers: int = 12
+    num_classes: int = 1000
+
+    @property
+    def grid(self):
+        return self.image_size // self.patch_size
+
+    @property
+    def tokens(self):
+        return self.grid * self.grid + 1
+
+    @property
+    def head_dim(self):
+        return self.emb_dim // self.num_heads
+
+    @property
+    def patch_k(self):
+        return 3 * self.patch_size * self.patch_size
+
+
+def layer_param_specs(cfg: ArchConfig, i: int):
+    """(name, shape) of encoder layer i in reference state_dict order (src/model.py:104-130)."""
+    D, M, H = cfg.emb_dim, cfg.mlp_dim, cfg.num_heads
+    hd = D // H
+    p = f"transformer.encoder_layers.{i}."
+    out = [(p + "norm1.weight", (D,)), (p + "norm1.bias", (D,))]
+    for w in ("query", "key", "value"):
+        out += [(p + f"attn.{w}.weight", (D, H, hd)), (p + f"attn.{w}.bias", (H, hd))]
+    out += [(p + "attn.out.weight", (H, hd, D)), (p + "attn.out.bias", (D,))]
+    out += [(p + "norm2.weight", (D,)), (p + "norm2.bias", (D,))]
+    out += [(p + "mlp.fc1.weight", (M, D)), (p + "mlp.fc1.bias", (M,))]
+    out += [(p + "mlp.fc2.weight", (D, M)), (p + "mlp.fc2.bias", (D,))]
+    return out
+
+
+def flat_param_specs(cfg: ArchConfig):
+    """All parameters in flat-buffer order (reverse of backward completion)."""
+    D, P, C = cfg.emb_dim, cfg.patch_size, cfg.num_classes
+    specs = [("classifier.weight", (C, D)), ("classifier.bias", (C,)),
+             ("transformer.norm.weight", (D,)), ("transformer.norm.bias", (D,))]
+    for i in reversed(range(cfg.num_layers)):
+        specs += layer_param_specs(cfg, i)
+    specs += [("embedding.weight", (D, 3, P, P)), ("embedding.bias", (D,)),
+              ("transformer.pos_embedding.pos_embedding", (1, cfg.tokens, D)), ("cls_token", (1, 1, D))]
+    return specs
+
+
+class FlatLayout:
+    def __init__(self, cfg: ArchConfig):
+        self.cfg = cfg
+        self.offsets = OrderedDict()
+        self.shapes = OrderedDict()
+        off = 0
+        self.layer_ranges = {}
+        for name, shape in flat_param_specs(cfg):
+            n = math.prod(shape)
+            self.offsets[name] = off
+            self.shapes[name] = shape
+            off = _rup(off + n, ALIGN)
+        self.numel = off
+        # contiguous [start, end) of every gradient bucket in backward-completion order
+        L = cfg.num_layers
+        self.buckets = []
+        self.buckets.append(("head", 0, self.offsets[self._lname(L - 1, "norm1.weight")]))
+        for i in reversed(range(L)):
+            start = self.offsets[self._lname(i, "norm1.weight")]
+            end = self.offsets[self._lname(i - 1, "norm1.weight")] if i > 0 else self.offsets["embedding.weight"]
+            self.buckets.append((f"layer{i}", start, end))
+        self.buckets.append(("embed", self.offsets["embedding.weight"], self.numel))
+
+    @staticmethod
+    def _lname(i, s):
+        return f"transformer.encoder_layers.{i}.{s}"
+
+    def view(self, buf, name):
+        o = self.offsets[name]
+        shape = self.shapes[name]
+        return buf[o:o + math.prod(shape)].view(shape)
+
+
+class _Acts:
+    """Per-batch-size activation workspace (allocated once, rows padded to 64)."""
+
+    def __init__(self, cfg: ArchConfig, b: int, dev):
+        D, M, H, L, N = cfg.emb_dim, cfg.mlp_dim, cfg.num_heads, cfg.num_layers, cfg.tokens
+        T = b * N
+        Tp = _rup(T, 64)
+        self.b, self.T, self.Tp = b, T, Tp
+        z = lambda *s, dt=torch.bfloat16: torch.zeros(*s, device=dev, dtype=dt)
+        f = torch.float32
+        self.kpad = _rup(cfg.patch_k, 64)
+        self.patches = z(Tp, self.kpad)
+        self.h = [z(Tp, D, dt=f) for _ in range(L + 1)]        # layer inputs (fp32 residual stream)
+        self.hm = [z(Tp, D, dt=f) for _ in range(L)]           # after attention
+        self.ln1 = [z(Tp, D) for _ in range(L)]
+        self.ln2 = [z(Tp, D) for _ in range(L)]
+        self.mu1 = [z(T, dt=f) for _ in range(L)]
+        self.rs1 = [z(T, dt=f) for _ in range(L)]
+        self.mu2 = [z(T, dt=f) for _ in range(L)]
+        self.rs2 = [z(T, dt=f) for _ in range(L)]
+        self.qkv = [z(Tp, 3 * D) for _ in range(L)]
+        self.o = [z(Tp, D) for _ in range(L)]
+        self.lse = [z(b, H, N, dt=f) for _ in range(L)]
+        self.u = [z(Tp, M) for _ in range(L)]
+        self.g = [z(Tp, M) for _ in range(L)]
+        self.lncls = z(b, D, dt=f)
+        self.muf = z(b, dt=f)
+        self.rsf = z(b, dt=f)
+        self.logits = z(b, cfg.num_classes, dt=f)
+        # backward scratch
+        self.dh = z(Tp, D, dt=f)
+        self.dhb = z(Tp, D)
+        self.dg = z(Tp, M)
+        self.dyln = z(Tp, D)
+        self.dO = z(Tp, D)
+        self.dqkv = z(Tp, 3 * D)
+        self.dlncls = z(b, D, dt=f)
+        self.dlogits = z(b, cfg.num_classes, dt=f)
+        self.row_stats = z(b, 3, dt=f)
+        self.lnpart = z(ops.layernorm_bwd_partial_rows(T), 2 * D, dt=f)
+        self.colpart = z(ops.colsum_partial_rows(T), max(3 * D, M, cfg.num_classes), dt=f)
+
+
+class ViTEngine:
+    """Owns flat parameter/gradient buffers, the bf16 mirror and per-batch activations."""
+
+    def __init__(self, cfg: ArchConfig, device="cuda", flat: torch.Tensor | None = None):
+        if cfg.emb_dim % cfg.num_heads:
+            raise ValueError("emb_dim must be divisible by num_heads")
+        if cfg.head_dim not in (32, 64):
+            raise NotImplementedError(f"head_dim {cfg.head_dim} not supported by the HIP attention kernel yet")
+        if cfg.emb_dim % 64 or cfg.mlp_dim % 64:
+            raise NotImplementedError("emb_dim and mlp_dim must be multiples of 64")
+        if cfg.tokens > 320:
+            raise NotImplementedError(f"{cfg.tokens} tokens > 320 not supported by the attention kernel")
+        self.cfg = cfg
+        self.dev = torch.device(device)
+        self.layout = FlatLayout(cfg)
+        n = self.layout.numel
+        self.flat = flat if flat is not None else torch.zeros(n, device=self.dev)
+        self.grad = torch.zeros(n, device=self.dev)
+        self.mirror = torch.zeros(n, device=self.dev, dtype=torch.bfloat16)
+        D, L = cfg.emb_dim, cfg.num_layers
+        self.wqkv = torch.zeros(L, D, 3 * D, device=self.dev, dtype=torch.bfloat16)
+        self.bqkv = torch.zeros(L, 3 * D, device=self.dev)
+        kp = _rup(cfg.patch_k, 64)
+        self.wconv = torch.zeros(D, kp, device=self.dev, dtype=torch.bfloat16) if kp != cfg.patch_k else None
+        self._acts = {}
+        self._mirror_sig = None
+        self._ws = None
+        self.step_id = 0
+        self.grad_ready_hook = None  # callable(grad_buf, bucket_name, start, end) during backward
+        self.probe = None  # list: (start, end) HIP events around every fc1 forward GEMM launch
+
+    # ---- parameters --------------------------------------------------------------------------
+    def pv(self, name, buf=None):
+        return self.layout.view(self.flat if buf is None else buf, name)
+
+    def off(self, name):
+        return self.layout.offsets[name]
+
+    def lname(self, i, s):
+        return f"transformer.encoder_layers.{i}.{s}"
+
+    def load_params(self, params):
+        for k, v in params.items():
+            self.pv(k).copy_(v.to(self.dev, torch.float32).reshape(self.layout.shapes[k]))
+        self.invalidate_mirror()
+
+    def state(self):
+        return OrderedDict((k, self.pv(k)) for k in self.layout.offsets)
+
+    def invalidate_mirror(self):
+        self._mirror_sig = None
+
+    def refresh_mirror(self, full=True):
+        """Re-derive the bf16 GEMM operands from the fp32 master weights."""
+        cfg = self.cfg
+        D = cfg.emb_dim
+        if full:
+            ops.cast_bf16(self.flat, self.mirror, self.layout.numel)
+        for i in range(cfg.num_layers):
+            qo = self.off(self.lname(i, "attn.query.weight"))
+            zs = self.off(self.lname(i, "attn.key.weight")) - qo
+            ops.pack_cols(self.flat[qo:], zs, D, D, D, 3, self.wqkv[i], 3 * D)
+            bo = self.off(self.lname(i, "attn.query.bias"))
+            ops.pack_cols(self.flat[bo:], zs, D, 1, D, 3, self.bqkv[i], 3 * D)
+        if self.wconv is not None:
+            w = self.off("embedding.weight")
+            ops.cast_pad_rows(self.flat[w:], D, cfg.patch_k, self.wconv, self.wconv.shape[1])
+
+    def mark_mirror_fresh(self, sig):
+        self._mirror_sig = sig
+
+    # ---- workspaces --------------------------------------------------------------------------
+    def acts(self, b):
+        a = self._acts.get(b)
+        if a is None:
+            if len(self._acts) >= 2:
+                self._acts.pop(next(iter(self._acts)))
+            a = _Acts(self.cfg, b, self.dev)
+            self._acts[b] = a
+        return a
+
+    def _splitk(self, M, N, K, z=1):
+        tiles = ((M + 127) // 128) * ((N + 127) // 128) * z
+        nkt = K // 64
+        s = max(1, min(round(1024 / tiles), nkt // 8, 32))
+        return s
+
+    def _workspace(self, numel):
+        if self._ws is None or self._ws.numel() < numel:
+            self._ws = torch.empty(numel, device=self.dev)
+        return self._ws
+
+    def _wgrad(self, A, lda, B, ldb, M, N, K, out, ldo, batch=1, b_bs=0, out_bs=0):
+        """out[z] (f32, [M][N], ld ldo) = sum_t A[t][m] B[t][n]  (both operands K-major)."""
+        s = self._splitk(M, N, K, batch)
+        ws = self._workspace(batch * s * M * N)
+        ops.gemm(A, B, ws, M, N, K, a_layout=MN_CONTIG, b_layout=MN_CONTIG, lda=lda, ldb=ldb, ldc=N,
+                 epilogue=EPI_SPLITK, batch=batch, b_bs=b_bs, split_k=s)
+        ops.splitk_reduce(ws, batch, s, M, N, out, ldo, out_bs)
+
+    def _bias_grad(self, a, inp, cols, ld, out):
+        ops.colsum(inp, a.T, cols, ld, a.colpart, out)
+
+    # ---- forward -------------------------------------------------------------------------------
+    def forward(self, x: torch.Tensor):
+        """x: [b, 3, img, img] fp32 on the device. Returns logits [b, C] (fp32, engine-owned)."""
+        cfg = self.cfg
+        if x.dim() != 4 or x.shape[1] != 3 or x.shape[2] != cfg.image_size or x.shape[3] != cfg.image_size:
+            raise ValueError(f"expected input [b, 3, {cfg.image_size}, {cfg.image_size}], got {tuple(x.shape)}")
+        x = x.to(self.dev, torch.float32).contiguous()
+        b = x.shape[0]
+        a = self.acts(b)
+        D, M, H, N, L = cfg.emb_dim, cfg.mlp_dim, cfg.num_heads, cfg.tokens, cfg.num_layers
+        hd = D // H
+        T = a.T
+        mv = self.mirror
+        f = self.flat
+        # patch embedding: im2col + GEMM with conv-bias / cls / pos-emb epilogue
+        ops.im2col(x, a.patches, b, cfg.image_size, cfg.patch_size, a.kpad)
+        wconv = self.wconv if self.wconv is not None else mv[self.off("embedding.weight"):]
+        ops.gemm(a.patches, wconv, a.h[0], T, D, a.kpad, a_layout=K_CONTIG, b_layout=K_CONTIG, lda=a.kpad,
+                 ldb=a.kpad, ldc=D, epilogue=EPI_PATCH, bias=f[self.off("embedding.bias"):],
+                 aux=f[self.off("transformer.pos_embedding.pos_embedding"):], ldaux=D,
+                 aux2=f[self.off("cls_token"):], tokens=N)
+        scale = 1.0 / math.sqrt(hd)
+        for i in range(L):
+            ln = lambda s: self.off(self.lname(i, s))
+            ops.layernorm_fwd(a.h[i], D, f[ln("norm1.weight"):], f[ln("norm1.bias"):], a.ln1[i], D, a.mu1[i],
+                              a.rs1[i], T, D)
+            ops.gemm(a.ln1[i], self.wqkv[i], a.qkv[i], T, 3 * D, D, a_layout=K_CONTIG, b_layout=MN_CONTIG, lda=D,
+                     ldb=3 * D, ldc=3 * D, epilogue=EPI_BIAS_BF16, bias=self.bqkv[i])
+            ops.attention_fwd(a.qkv[i], a.o[i], a.lse[i], b, N, H, hd, scale)
+            ops.gemm(a.o[i], mv[ln("attn.out.weight"):], a.hm[i], T, D, D, a_layout=K_CONTIG, b_layout=MN_CONTIG,
+                     lda=D, ldb=D, ldc=D, epilogue=EPI_BIAS_RESID_F32, bias=f[ln("attn.out.bias"):], aux=a.h[i],
+                     ldaux=D)
+            ops.layernorm_fwd(a.hm[i], D, f[ln("norm2.weight"):], f[ln("norm2.bias"):], a.ln2[i], D, a.mu2[i],
+                              a.rs2[i], T, D)
+            if self.probe is not None:
+                ev0 = torch.cuda.Event(enable_timing=True)
+                ev0.record()
+            ops.gemm(a.ln2[i], mv[ln("mlp.fc1.weight"):], a.u[i], T, M, D, a_layout=K_CONTIG, b_layout=K_CONTIG,
+                     lda=D, ldb=D, ldc=M, epilogue=EPI_BIAS_GELU, bias=f[ln("mlp.fc1.bias"):], C2=a.g[i], ldc2=M)
+            if self.probe is not None:
+                ev1 = torch.cuda.Event(enable_timing=True)
+                ev1.record()
+                self.probe.append((ev0, ev1))
+            ops.gemm(a.g[i], mv[ln("mlp.fc2.weight"):], a.h[i + 1], T, D, M, a_layout=K_CONTIG, b_layout=K_CONTIG,
+                     lda=M, ldb=M, ldc=D, epilogue=EPI_BIAS_RESID_F32, bias=f[ln("mlp.fc2.bias"):], aux=a.hm[i],
+                     ldaux=D)
+        # final LayerNorm on the cls rows only (only row 0 reaches the classifier, src/model.py:210)
+        ops.layernorm_fwd(a.h[L], N * D, f[self.off("transformer.norm.weight"):], f[self.off("transformer.norm.bias"):],
+                          a.lncls, D, a.muf, a.rsf, b, D)
+        C = cfg.num_classes
+        ops.gemm_f32(b, C, D, a.lncls, D, False, f[self.off("classifier.weight"):], D, True, a.logits, C,
+                     bias=f[self.off("classifier.bias"):])
+        self.step_id += 1
+        self._last_b = b
+        return a.logits
+
+    # ---- loss ------------------------------------------------------------------------------------
+    def cross_entropy(self, labels: torch.Tensor, grad_scale: float | None = None):
+        """Fused CE on the last logits: fills dlogits (scaled by grad_scale, default 1/b) and
+        per-row {loss, top1, top5}. Returns (dlogits, row_stats)."""
+        a = self.acts(self._last_b)
+        gs = 1.0 / a.b if grad_scale is None else grad_scale
+        ops.cross_entropy(a.logits, labels.to(self.dev, torch.int64).contiguous(), a.dlogits, gs, a.row_stats)
+        return a.dlogits, a.row_stats
+
+    # ---- backward --------------------------------------------------------------------------------
+    def backward(self, dlogits: torch.Tensor, grad: torch.Tensor | None = None):
+        """Backward of the last forward given dL/dlogits [b, C]; writes every parameter gradient
+        into `grad` (default self.grad, flat layout)."""
+        cfg = self.cfg
+        b = self._last_b
+        a = self.acts(b)
+        g = self.grad if grad is None else grad
+        D, M, H, N, L, C = cfg.emb_dim, cfg.mlp_dim, cfg.num_heads, cfg.tokens, cfg.num_layers, cfg.num_classes
+        hd = D // H
+        T = a.T
+        f = self.flat
+        mv = self.mirror
+        gv = lambda name: g[self.off(name):]
+        dl = dlogits.to(self.dev, torch.float32).contiguous()
+        hook = self.grad_ready_hook
+        # classifier head (f32): dWc = dl^T lncls, dbc = colsum(dl), dlncls = dl Wc
+        ops.gemm_f32(C, D, b, dl, C, True, a.lncls, D, False, gv("classifier.weight"), D)
+        ops.colsum(dl, b, C, C, a.colpart, gv("classifier.bias"))
+        ops.gemm_f32(b, D, C, dl, C, False, f[self.off("classifier.weight"):], D, False, a.dlncls, D)
+        # final LN backward on cls rows -> residual grad (zero elsewhere)
+        a.dh.zero_()
+        a.dhb.zero_()
+        ops.layernorm_bwd(a.dlncls, D, a.h[L], N * D, a.muf, a.rsf, f[self.off("transformer.norm.weight"):], a.dh,
+                          N * D, a.lnpart, b, D, dx_bf16=a.dhb, lddxb=N * D,
+                          dgamma_dbeta=gv("transformer.norm.weight"))
+        if hook:
+            hook(g, *self.layout.buckets[0])
+        scale = 1.0 / math.sqrt(hd)
+        for i in reversed(range(L)):
+            ln = lambda s: self.off(self.lname(i, s))
+            # ---- MLP: h_{i+1} = hm + fc2(gelu(fc1(ln2(hm)))) ----
+            self._wgrad(a.dhb, D, a.g[i], M, D, M, a.Tp, gv(self.lname(i, "mlp.fc2.weight")), M)
+            self._bias_grad(a, a.dh, D, D, gv(self.lname(i, "mlp.fc2.bias")))
+            ops.gemm(a.dhb, mv[ln("mlp.fc2.weight"):], a.dg, T, M, D, a_layout=K_CONTIG, b_layout=MN_CONTIG, lda=D,
+                     ldb=M, ldc=M, epilogue=EPI_GELU_BWD, aux=a.u[i], ldaux=M)
+            self._wgrad(a.dg, M, a.ln2[i], D, M, D, a.Tp, gv(self.lname(i, "mlp.fc1.weight")), D)
+            self._bias_grad(a, a.dg, M, M, gv(self.lname(i, "mlp.fc1.bias")))
+            ops.gemm(a.dg, mv[ln("mlp.fc1.weight"):], a.dyln, T, D, M, a_layout=K_CONTIG, b_layout=MN_CONTIG, lda=M,
+                     ldb=D, ldc=D, epilogue=EPI_BF16)
+            ops.layernorm_bwd(a.dyln, D, a.hm[i], D, a.mu2[i], a.rs2[i], f[ln("norm2.weight"):], a.dh, D, a.lnpart, T,
+                              D, dres=a.dh, lddres=D, dx_bf16=a.dhb, lddxb=D,
+                              dgamma_dbeta=gv(self.lname(i, "norm2.weight")))
+            # ---- attention: hm = h + out(attn(ln1(h))) ----
+            self._wgrad(a.o[i], D, a.dhb, D, D, D, a.Tp, gv(self.lname(i, "attn.out.weight")), D)
+            self._bias_grad(a, a.dh, D, D, gv(self.lname(i, "attn.out.bias")))
+            ops.gemm(a.dhb, mv[ln("attn.out.weight"):], a.dO, T, D, D, a_layout=K_CONTIG, b_layout=K_CONTIG, lda=D,
+                     ldb=D, ldc=D, epilogue=EPI_BF16)
+            ops.attention_bwd(a.qkv[i], a.o[i], a.dO, a.lse[i], a.dqkv, b, N, H, hd, scale)
+            qo = ln("attn.query.weight")
+            zs = ln("attn.key.weight") - qo
+            self._wgrad(a.ln1[i], D, a.dqkv, 3 * D, D, D, a.Tp, g[qo:], D, batch=3, b_bs=D, out_bs=zs)
+            for z in range(3):
+                self._bias_grad(a, a.dqkv[:, z * D:], D, 3 * D, g[ln("attn.query.bias") + z * zs:])
+            ops.gemm(a.dqkv, self.wqkv[i], a.dyln, T, D, 3 * D, a_layout=K_CONTIG, b_layout=K_CONTIG, lda=3 * D,
+                     ldb=3 * D, ldc=D, epilogue=EPI_BF16)
+            ops.layernorm_bwd(a.dyln, D, a.h[i], D, a.mu1[i], a.rs1[i], f[ln("norm1.weight"):], a.dh, D, a.lnpart, T,
+                              D, dres=a.dh, lddres=D, dx_bf16=a.dhb, lddxb=D,
+                              dgamma_dbeta=gv(self.lname(i, "norm1.weight")))
+            if hook:
+                hook(g, *self.layout.buckets[L - i])
+        # ---- embedding: conv weight grad (wgrad over patches), bias / pos / cls ----
+        self._wgrad(a.dhb, D, a.patches, a.kpad, D, cfg.patch_k, a.Tp, gv("embedding.weight"), cfg.patch_k)
+        ops.embed_grad(a.dh, b, N, D, gv("transformer.pos_embedding.pos_embedding"), gv("cls_token"),
+                       gv("embedding.bias"))
+        if hook:
+            hook(g, *self.layout.buckets[-1])
+        return g

@@ -1,0 +1,148 @@
+"""Torch-tensor wrappers over the C ABI (include/vit_hip.h).
+
+Every function launches hand-written gfx950 kernels from libvit_hip.so on the current torch
+stream. Inputs must already live on the GPU with the documented dtype/layout; nothing here
+falls back to a PyTorch implementation.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _lib
+from ._lib import GemmArgs, check
+
+BF16 = torch.bfloat16
+F32 = torch.float32
+
+
+def lib():
+    return _lib.load()
+
+
+def _stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _p(t):
+    return ctypes.c_void_p(0 if t is None else t.data_ptr())
+
+
+def _chk(t, dtype, name):
+    if t is None:
+        return
+    if not t.is_cuda:
+        raise ValueError(f"{name} must be a GPU tensor")
+    if t.dtype != dtype:
+        raise TypeError(f"{name} must be {dtype}, got {t.dtype}")
+
+
+# ---------------------------------------------------------------------------------------------
+def gemm(A, B, C, M, N, K, *, a_layout, b_layout, lda, ldb, ldc, epilogue, bias=None, aux=None, ldaux=0,
+         C2=None, ldc2=0, aux2=None, batch=1, a_bs=0, b_bs=0, c_bs=0, bias_bs=0, split_k=1, tokens=0):
+    """bf16 MFMA GEMM, C[m,n] = sum_k A(m,k) B(k,n) + fused epilogue (see vit_gemm_args)."""
+    _chk(A, BF16, "A")
+    _chk(B, BF16, "B")
+    a = GemmArgs()
+    a.M, a.N, a.K = M, N, K
+    a.A, a.lda, a.a_batch_stride, a.a_layout = A.data_ptr(), lda, a_bs, a_layout
+    a.B, a.ldb, a.b_batch_stride, a.b_layout = B.data_ptr(), ldb, b_bs, b_layout
+    a.C, a.ldc, a.c_batch_stride = C.data_ptr(), ldc, c_bs
+    a.C2, a.ldc2 = (C2.data_ptr() if C2 is not None else None), ldc2
+    a.bias, a.bias_batch_stride = (bias.data_ptr() if bias is not None else None), bias_bs
+    a.aux, a.ldaux = (aux.data_ptr() if aux is not None else None), ldaux
+    a.aux2 = aux2.data_ptr() if aux2 is not None else None
+    a.batch, a.split_k, a.tokens = batch, split_k, tokens
+    a.epilogue, a.tile = epilogue, 0
+    check(lib().vit_gemm_bf16(ctypes.byref(a), _stream()), "vit_gemm_bf16")
+
+
+def splitk_reduce(ws, batch, split, M, N, out, ldo, out_bs=0, accumulate=False):
+    _chk(ws, F32, "ws")
+    _chk(out, F32, "out")
+    check(lib().vit_splitk_reduce(_p(ws), batch, split, M, N, _p(out), ldo, out_bs, int(accumulate), _stream()),
+          "vit_splitk_reduce")
+
+
+def layernorm_fwd(x, ldx, gamma, beta, y, ldy, mean, rstd, rows, D, eps=1e-5):
+    _chk(x, F32, "x")
+    check(lib().vit_layernorm_fwd(_p(x), ldx, _p(gamma), _p(beta), _p(y), ldy, int(y.dtype == F32), _p(mean),
+                                  _p(rstd), rows, D, eps, _stream()), "vit_layernorm_fwd")
+
+
+def layernorm_bwd_partial_rows(rows):
+    return int(lib().vit_layernorm_bwd_partial_rows(rows))
+
+
+def layernorm_bwd(dy, lddy, x, ldx, mean, rstd, gamma, dx, lddx, partial, rows, D, *, dres=None, lddres=0,
+                  dx_bf16=None, lddxb=0, dgamma_dbeta=None, accumulate=False):
+    check(lib().vit_layernorm_bwd(_p(dy), lddy, int(dy.dtype == F32), _p(x), ldx, _p(mean), _p(rstd), _p(gamma),
+                                  _p(dres), lddres, _p(dx), lddx, _p(dx_bf16), lddxb, _p(partial), _p(dgamma_dbeta),
+                                  int(accumulate), rows, D, _stream()), "vit_layernorm_bwd")
+
+
+def attention_fwd(qkv, o, lse, B, N, H, hd, scale):
+    _chk(qkv, BF16, "qkv")
+    _chk(o, BF16, "o")
+    _chk(lse, F32, "lse")
+    check(lib().vit_attention_fwd(_p(qkv), _p(o), _p(lse), B, N, H, hd, scale, _stream()), "vit_attention_fwd")
+
+
+def attention_bwd(qkv, o, dout, lse, dqkv, B, N, H, hd, scale):
+    check(lib().vit_attention_bwd(_p(qkv), _p(o), _p(dout), _p(lse), _p(dqkv), B, N, H, hd, scale, _stream()),
+          "vit_attention_bwd")
+
+
+def im2col(x, out, B, img, P, Kpad):
+    _chk(x, F32, "x")
+    _chk(out, BF16, "out")
+    check(lib().vit_im2col(_p(x), _p(out), B, img, P, Kpad, _stream()), "vit_im2col")
+
+
+def embed_grad(dh0, B, N, D, dpos, dcls, dconv_bias):
+    check(lib().vit_embed_grad(_p(dh0), B, N, D, _p(dpos), _p(dcls), _p(dconv_bias), _stream()), "vit_embed_grad")
+
+
+def colsum_partial_rows(rows):
+    return int(lib().vit_colsum_partial_rows(rows))
+
+
+def colsum(inp, rows, cols, ld, partial, out, accumulate=False):
+    check(lib().vit_colsum(_p(inp), int(inp.dtype == BF16), rows, cols, ld, _p(partial), _p(out), int(accumulate),
+                           _stream()), "vit_colsum")
+
+
+def gemm_f32(M, N, K, A, lda, a_trans, B, ldb, b_trans, C, ldc, bias=None, accumulate=False):
+    check(lib().vit_gemm_f32(M, N, K, _p(A), lda, int(a_trans), _p(B), ldb, int(b_trans), _p(C), ldc, _p(bias),
+                             int(accumulate), _stream()), "vit_gemm_f32")
+
+
+def cross_entropy(logits, labels, dlogits, grad_scale, row_stats):
+    _chk(logits, F32, "logits")
+    _chk(labels, torch.int64, "labels")
+    B, C = logits.shape
+    check(lib().vit_cross_entropy(_p(logits), _p(labels), B, C, _p(dlogits), grad_scale, _p(row_stats), _stream()),
+          "vit_cross_entropy")
+
+
+def sgd_step(p, g, buf, p_bf16, n, lr, momentum, wd, first):
+    check(lib().vit_sgd_step(_p(p), _p(g), _p(buf), _p(p_bf16), n, lr, momentum, wd, int(first), _stream()),
+          "vit_sgd_step")
+
+
+def cast_bf16(inp, out, n):
+    check(lib().vit_cast_f32_bf16(_p(inp), _p(out), n, _stream()), "vit_cast_f32_bf16")
+
+
+def cast_pad_rows(inp, rows, cols, out, ldo):
+    check(lib().vit_cast_pad_rows(_p(inp), rows, cols, _p(out), ldo, _stream()), "vit_cast_pad_rows")
+
+
+def axpby(x, y, n, a, b):
+    check(lib().vit_axpby(_p(x), _p(y), n, a, b, _stream()), "vit_axpby")
+
+
+def pack_cols(inp, zstride, ldi, rows, cols, Z, out, ldo):
+    check(lib().vit_pack_cols(_p(inp), zstride, ldi, rows, cols, Z, _p(out), ldo, int(out.dtype == BF16), _stream()),
+          "vit_pack_cols")
