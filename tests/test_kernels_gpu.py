@@ -212,6 +212,14 @@ def test_colsum_ce_gemm_f32_sgd():
     xb = x.bfloat16()
     ops.colsum(xb, 5000, 300, 300, part, out)
     assert rel(out, xb.float().sum(0)) < 1e-5
+    for rows, cols in ((50432, 768), (333, 3072), (7, 64)):   # vector path (cols % 8 == 0)
+        xv = torch.randn(rows, cols + 16, device=DEV)
+        pv = torch.empty(ops.colsum_partial_rows(rows), cols, device=DEV)
+        ov = torch.full((cols,), 1.0, device=DEV)
+        ops.colsum(xv, rows, cols, cols + 16, pv, ov, accumulate=True)
+        assert rel(ov, 1.0 + xv[:, :cols].sum(0)) < 1e-5
+        ops.colsum(xv.bfloat16(), rows, cols, cols + 16, pv, ov)
+        assert rel(ov, xv[:, :cols].bfloat16().float().sum(0)) < 1e-5
 
     logits = torch.randn(64, 1000, device=DEV) * 3
     y = torch.randint(0, 1000, (64,), device=DEV)

@@ -48,13 +48,54 @@ __global__ void cls_bias_grad_kernel(const float* __restrict__ dpos, int N, int 
 }
 
 // ---- column sums --------------------------------------------------------------------------------
-constexpr int COLSUM_ROWS_PER_CHUNK = 64;
-constexpr int COLSUM_MAX_CHUNKS = 512;
+// Vector path: a thread owns 8 consecutive columns (one 16-B bf16 / 32-B f32 load per row), a
+// 256-thread block = 32 column groups x 8 row lanes; each block reduces a chunk of rows into one
+// partial row, a second pass of the same kernel reduces the partial rows.
+constexpr int COLSUM_MAX_CHUNKS = 256;
+constexpr int COLSUM_MIN_ROWS_PER_CHUNK = 64;
 
+template <bool BF16>
+__global__ void __launch_bounds__(256) colsum8_kernel(const void* __restrict__ in, long rows, int cols, long ld,
+                                                      int chunks, float* __restrict__ out, int accumulate) {
+  __shared__ float red[8][32][9];
+  const int cgl = threadIdx.x & 31, rl = threadIdx.x >> 5;
+  const int cg = blockIdx.x * 32 + cgl;
+  const int ch = blockIdx.y;
+  const long per = (rows + chunks - 1) / chunks;
+  const long r0 = ch * per, r1 = r0 + per < rows ? r0 + per : rows;
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (cg * 8 < cols) {
+    for (long r = r0 + rl; r < r1; r += 8) {
+      if constexpr (BF16) {
+        const uint4 u = *reinterpret_cast<const uint4*>((const bf16_t*)in + r * ld + cg * 8);
+        acc[0] += bf2f(u.x & 0xffff); acc[1] += bf2f(u.x >> 16); acc[2] += bf2f(u.y & 0xffff); acc[3] += bf2f(u.y >> 16);
+        acc[4] += bf2f(u.z & 0xffff); acc[5] += bf2f(u.z >> 16); acc[6] += bf2f(u.w & 0xffff); acc[7] += bf2f(u.w >> 16);
+      } else {
+        const float4 a = *reinterpret_cast<const float4*>((const float*)in + r * ld + cg * 8);
+        const float4 b = *reinterpret_cast<const float4*>((const float*)in + r * ld + cg * 8 + 4);
+        acc[0] += a.x; acc[1] += a.y; acc[2] += a.z; acc[3] += a.w;
+        acc[4] += b.x; acc[5] += b.y; acc[6] += b.z; acc[7] += b.w;
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) red[rl][cgl][k] = acc[k];
+  __syncthreads();
+  const int ocg = threadIdx.x >> 3, k = threadIdx.x & 7;
+  const int col = (blockIdx.x * 32 + ocg) * 8 + k;
+  if (col < cols) {
+    float s = 0.f;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) s += red[q][ocg][k];
+    float* dst = out + (long)ch * cols + col;
+    *dst = accumulate ? *dst + s : s;
+  }
+}
+
+// Scalar fallback (odd widths / alignment).
 __device__ __forceinline__ float ld_elem(const void* p, long i, int is_bf16) {
   return is_bf16 ? bf2f(((const bf16_t*)p)[i]) : ((const float*)p)[i];
 }
-
 __global__ void colsum_partial_kernel(const void* __restrict__ in, int in_bf16, long rows, int cols, long ld,
                                       int chunks, float* __restrict__ partial) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
@@ -228,7 +269,7 @@ extern "C" int vit_embed_grad(const float* dh0, int64_t B, int64_t N, int64_t D,
 }
 
 extern "C" int64_t vit_colsum_partial_rows(int64_t rows) {
-  int64_t c = (rows + COLSUM_ROWS_PER_CHUNK - 1) / COLSUM_ROWS_PER_CHUNK;
+  int64_t c = rows / COLSUM_MIN_ROWS_PER_CHUNK;
   if (c > COLSUM_MAX_CHUNKS) c = COLSUM_MAX_CHUNKS;
   return c < 1 ? 1 : c;
 }
@@ -238,6 +279,22 @@ extern "C" int vit_colsum(const void* in, int32_t in_bf16, int64_t rows, int64_t
   VIT_CHECK_ARG(in && partial && out && cols > 0 && ld >= cols, "vit_colsum: bad args");
   hipStream_t s = (hipStream_t)stream;
   const int chunks = (int)vit_colsum_partial_rows(rows);
+  const bool vec = cols % 8 == 0 && ld % 8 == 0 && ((uintptr_t)in % 32) == 0 && ((uintptr_t)partial % 16) == 0 &&
+                   ((uintptr_t)out % 4) == 0;
+  if (vec) {
+    const unsigned gx = (unsigned)((cols / 8 + 31) / 32);
+    float* dst1 = chunks == 1 ? out : partial;
+    if (in_bf16)
+      hipLaunchKernelGGL(colsum8_kernel<true>, dim3(gx, chunks), dim3(256), 0, s, in, (long)rows, (int)cols, (long)ld,
+                         chunks, dst1, chunks == 1 ? (int)accumulate : 0);
+    else
+      hipLaunchKernelGGL(colsum8_kernel<false>, dim3(gx, chunks), dim3(256), 0, s, in, (long)rows, (int)cols,
+                         (long)ld, chunks, dst1, chunks == 1 ? (int)accumulate : 0);
+    if (chunks > 1)
+      hipLaunchKernelGGL(colsum8_kernel<false>, dim3(gx, 1), dim3(256), 0, s, (const void*)partial, (long)chunks,
+                         (int)cols, (long)cols, 1, out, (int)accumulate);
+    VIT_LAUNCH_CHECK("vit_colsum");
+  }
   const unsigned gx = (unsigned)((cols + 255) / 256);
   hipLaunchKernelGGL(colsum_partial_kernel, dim3(gx, chunks), dim3(256), 0, s, in, (int)in_bf16, (long)rows, (int)cols,
                      (long)ld, chunks, partial);

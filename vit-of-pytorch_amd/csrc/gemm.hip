@@ -41,6 +41,7 @@ struct GemmDev {
   const float* aux2;
   int split_k;
   int tokens;
+  int vec;  // every pointer / leading dim allows 8-column (16/32-B) vector access
 };
 
 __device__ __forceinline__ int swz_k(int row) { return (row >> 1) & 7; }          // 16-B chunk xor
@@ -143,6 +144,81 @@ __device__ __forceinline__ void epi_store(const GemmDev& p, int z, int split_idx
   }
 }
 
+__device__ __forceinline__ void ld8f(const float* p, float* v) {
+  const float4 a = *reinterpret_cast<const float4*>(p);
+  const float4 b = *reinterpret_cast<const float4*>(p + 4);
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+__device__ __forceinline__ void st8f(float* p, const float* v) {
+  *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+  *reinterpret_cast<float4*>(p + 4) = make_float4(v[4], v[5], v[6], v[7]);
+}
+__device__ __forceinline__ void st8bf(bf16_t* p, const float* v) {
+  uint4 u;
+  u.x = pack2bf(v[0], v[1]); u.y = pack2bf(v[2], v[3]); u.z = pack2bf(v[4], v[5]); u.w = pack2bf(v[6], v[7]);
+  *reinterpret_cast<uint4*>(p) = u;
+}
+__device__ __forceinline__ void ld8bf(const bf16_t* p, float* v) {
+  const uint4 u = *reinterpret_cast<const uint4*>(p);
+  v[0] = bf2f(u.x & 0xffff); v[1] = bf2f(u.x >> 16); v[2] = bf2f(u.y & 0xffff); v[3] = bf2f(u.y >> 16);
+  v[4] = bf2f(u.z & 0xffff); v[5] = bf2f(u.z >> 16); v[6] = bf2f(u.w & 0xffff); v[7] = bf2f(u.w >> 16);
+}
+
+// 8 consecutive columns n..n+7 of row m (all in range, aligned: p.vec).
+template <int EPI>
+__device__ __forceinline__ void epi_store8(const GemmDev& p, int z, int split_idx, int m, int n, float* v) {
+  float b[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if constexpr (EPI == VIT_EPI_BIAS_BF16 || EPI == VIT_EPI_BIAS_GELU || EPI == VIT_EPI_BIAS_RESID_F32) {
+    if (p.bias) ld8f(p.bias + z * p.bias_bs + n, b);
+  }
+  if constexpr (EPI == VIT_EPI_F32) {
+    st8f((float*)p.C + z * p.c_bs + (long)m * p.ldc + n, v);
+  } else if constexpr (EPI == VIT_EPI_BF16) {
+    st8bf((bf16_t*)p.C + z * p.c_bs + (long)m * p.ldc + n, v);
+  } else if constexpr (EPI == VIT_EPI_BIAS_BF16) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] += b[k];
+    st8bf((bf16_t*)p.C + z * p.c_bs + (long)m * p.ldc + n, v);
+  } else if constexpr (EPI == VIT_EPI_BIAS_GELU) {
+    float gl[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      v[k] += b[k];
+      gl[k] = gelu_f(v[k]);
+    }
+    st8bf((bf16_t*)p.C + z * p.c_bs + (long)m * p.ldc + n, v);
+    st8bf((bf16_t*)p.C2 + z * p.c_bs + (long)m * p.ldc2 + n, gl);
+  } else if constexpr (EPI == VIT_EPI_BIAS_RESID_F32) {
+    float r[8];
+    ld8f((const float*)p.aux + (long)m * p.ldaux + n, r);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] += b[k] + r[k];
+    st8f((float*)p.C + z * p.c_bs + (long)m * p.ldc + n, v);
+  } else if constexpr (EPI == VIT_EPI_GELU_BWD) {
+    float u[8];
+    ld8bf((const bf16_t*)p.aux + (long)m * p.ldaux + n, u);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] *= gelu_grad_f(u[k]);
+    st8bf((bf16_t*)p.C + z * p.c_bs + (long)m * p.ldc + n, v);
+  } else if constexpr (EPI == VIT_EPI_PATCH) {
+    const int t = m % p.tokens;
+    float ps[8];
+    ld8f((const float*)p.aux + (long)t * p.ldaux + n, ps);
+    if (t == 0) {
+      ld8f(p.aux2 + n, b);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] = b[k] + ps[k];
+    } else {
+      ld8f(p.bias + n, b);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] += b[k] + ps[k];
+    }
+    st8f((float*)p.C + (long)m * p.ldc + n, v);
+  } else if constexpr (EPI == VIT_EPI_SPLITK) {
+    st8f((float*)p.C + ((long)z * p.split_k + split_idx) * (long)p.M * p.N + (long)m * p.N + n, v);
+  }
+}
+
 template <int BM, int BN, int WM, int WN, bool AK, bool BKC, int EPI>
 __global__ void __launch_bounds__(WM* WN * 64) gemm_bf16_kernel(const GemmDev p) {
   constexpr int NWAVE = WM * WN;
@@ -150,7 +226,9 @@ __global__ void __launch_bounds__(WM* WN * 64) gemm_bf16_kernel(const GemmDev p)
   constexpr int FM = TM / 16, FN = TN / 16;
   constexpr int A_BYTES = BM * 128, B_BYTES = BN * 128;
   constexpr int STAGE = A_BYTES + B_BYTES;
-  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+  constexpr int LDC = BN + 4;  // fp32 staging row stride (floats): +4 keeps the acc writes conflict-free
+  constexpr int SMEM = (2 * STAGE > BM * LDC * 4) ? 2 * STAGE : BM * LDC * 4;
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -220,15 +298,34 @@ __global__ void __launch_bounds__(WM* WN * 64) gemm_bf16_kernel(const GemmDev p)
     }
   }
 
-  // ---- epilogue: C[m0+wm0+16i+4g+r][n0+wn0+16j+(lane&15)] ----
+  // ---- epilogue: stage the fp32 tile in LDS, then each thread finishes 8-column row chunks ----
+  // (coalesced 16-B / 32-B stores and vector loads of bias / residual / GELU input)
   const int g = lane >> 4, c = lane & 15;
+  __syncthreads();  // every wave is done reading the operand stages
+  float* cs = reinterpret_cast<float*>(smem);
 #pragma unroll
   for (int i = 0; i < FM; ++i)
 #pragma unroll
     for (int j = 0; j < FN; ++j)
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
-        epi_store<EPI>(p, z, split_idx, m0 + wm0 + i * 16 + 4 * g + r, n0 + wn0 + j * 16 + c, acc[i][j][r]);
+      for (int r = 0; r < 4; ++r) cs[(wm0 + i * 16 + 4 * g + r) * LDC + wn0 + j * 16 + c] = acc[i][j][r];
+  __syncthreads();
+  constexpr int CPR = BN / 8;
+  constexpr int NT = NWAVE * 64;
+#pragma unroll 2
+  for (int e = threadIdx.x; e < BM * CPR; e += NT) {
+    const int row = e / CPR, ch = e % CPR;
+    const int m = m0 + row, n = n0 + ch * 8;
+    if (m >= p.M || n >= p.N) continue;
+    float v[8];
+    ld8f(cs + row * LDC + ch * 8, v);
+    if (p.vec && n + 8 <= p.N) {
+      epi_store8<EPI>(p, z, split_idx, m, n, v);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) epi_store<EPI>(p, z, split_idx, m, n + k, v[k]);
+    }
+  }
 }
 
 template <int BM, int BN, int WM, int WN, bool AK, bool BKC, int EPI>
@@ -291,6 +388,17 @@ extern "C" int vit_gemm_bf16(const vit_gemm_args* a, vit_stream_t stream) {
   d.bias = a->bias; d.bias_bs = a->bias_batch_stride;
   d.aux = a->aux; d.ldaux = a->ldaux; d.aux2 = a->aux2;
   d.split_k = (int)a->split_k; d.tokens = (int)a->tokens;
+  {
+    // 8-column vector epilogue: every row start of every touched array must be 32-B aligned
+    auto al = [](const void* q) { return ((uintptr_t)q % 32) == 0; };
+    bool v = al(a->C) && a->ldc % 8 == 0 && a->c_batch_stride % 8 == 0;
+    if (a->C2) v = v && al(a->C2) && a->ldc2 % 8 == 0;
+    if (a->bias) v = v && al(a->bias) && a->bias_batch_stride % 8 == 0;
+    if (a->aux) v = v && al(a->aux) && a->ldaux % 8 == 0;
+    if (a->aux2) v = v && al(a->aux2);
+    if (a->epilogue == VIT_EPI_SPLITK) v = al(a->C) && a->N % 8 == 0;
+    d.vec = v ? 1 : 0;
+  }
   hipStream_t s = (hipStream_t)stream;
   const int batch = (int)a->batch, split = (int)a->split_k;
   hipError_t e;
