@@ -59,6 +59,35 @@ def test_gemm_exact_integers(al, bl, M, N, K):
 
 
 @pytest.mark.parametrize("al,bl", LAYOUTS)
+@pytest.mark.parametrize("tile,M,N,K", [(1, 600, 520, 128), (2, 600, 300, 192), (0, 300, 200, 128), (1, 2100, 1600, 64),
+                                        (2, 2100, 768, 128)])
+def test_gemm_tiles_exact(al, bl, tile, M, N, K):
+    A, B, Am, Bm, lda, ldb = _mats(M, N, K, al, bl, ints=True)
+    C = torch.full((M, N), float("nan"), device=DEV)
+    ops.gemm(Am, Bm, C, M, N, K, a_layout=al, b_layout=bl, lda=lda, ldb=ldb, ldc=N, epilogue=EPI_F32, tile=tile)
+    assert torch.equal(C, A.float() @ B.float())
+
+
+@pytest.mark.parametrize("tile", [1, 2])
+def test_gemm_tiles_epilogue_splitk(tile):
+    M, N, K = 700, 520, 512
+    A, B, Am, Bm, lda, ldb = _mats(M, N, K, K_CONTIG, MN_CONTIG)
+    ref = A.float() @ B.float()
+    bias = torch.randn(N, device=DEV)
+    C = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    C2 = torch.empty_like(C)
+    ops.gemm(Am, Bm, C, M, N, K, a_layout=K_CONTIG, b_layout=MN_CONTIG, lda=lda, ldb=ldb, ldc=N,
+             epilogue=EPI_BIAS_GELU, bias=bias, C2=C2, ldc2=N, tile=tile)
+    assert rel(C.float(), ref + bias) < 5e-3
+    assert rel(C2.float(), torch.nn.functional.gelu(ref + bias)) < 5e-3
+    S = 3
+    ws = torch.empty(S, M, N, device=DEV)
+    ops.gemm(Am, Bm, ws, M, N, K, a_layout=K_CONTIG, b_layout=MN_CONTIG, lda=lda, ldb=ldb, ldc=N,
+             epilogue=EPI_SPLITK, split_k=S, tile=tile)
+    assert rel(ws.sum(0), ref) < 1e-5
+
+
+@pytest.mark.parametrize("al,bl", LAYOUTS)
 def test_gemm_random_f32(al, bl):
     M, N, K = 1000, 768, 768
     A, B, Am, Bm, lda, ldb = _mats(M, N, K, al, bl)

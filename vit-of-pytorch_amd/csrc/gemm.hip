@@ -44,14 +44,21 @@ struct GemmDev {
   int vec;  // every pointer / leading dim allows 8-column (16/32-B) vector access
 };
 
-__device__ __forceinline__ int swz_k(int row) { return (row >> 1) & 7; }          // 16-B chunk xor
-__device__ __forceinline__ int swz_mn(int row) { return (row & 3) | (((row >> 3) & 1) << 2); }  // 32-B granule xor
+// K-contiguous image [rows][BK]: XOR of the 16-B chunk index, conflict-free for the 16x16x32
+// fragment read (16 rows x 16 B per ds_read_b128 lane group).
+template <int BK>
+__device__ __forceinline__ int swz_k(int row) {
+  if constexpr (BK == 64) return (row >> 1) & 7;
+  return (-(row >> 2)) & 3;  // BK == 32: 64-B rows
+}
+// M/N-contiguous image [BK][rows]: XOR of the 32-B granule, conflict-free for ds_read_b64_tr_b16.
+__device__ __forceinline__ int swz_mn(int row) { return (row & 3) | (((row >> 3) & 1) << 2); }
 
-// Stage one operand tile (ROWS rows of the M/N dim x 64 k) into LDS at byte offset `lds_off`.
-template <int ROWS, bool KC, int NWAVE>
-__device__ __forceinline__ void stage_tile(char* smem, int lds_off, __amdgpu_buffer_rsrc_t rs, long ld,
-                                           int kt, int wave, int lane) {
-  constexpr int BYTES = ROWS * 128;
+// Issue the LDS-DMA of one operand k-tile (ROWS rows of the M/N dim x BK k) to byte offset lds_off.
+template <int ROWS, int BK, bool KC, int NWAVE>
+__device__ __forceinline__ void stage_tile(char* smem, int lds_off, __amdgpu_buffer_rsrc_t rs, long ld, int kt,
+                                           int wave, int lane) {
+  constexpr int BYTES = ROWS * BK * 2;
   constexpr int INSTR = BYTES / 1024 / NWAVE;
   static_assert(INSTR * 1024 * NWAVE == BYTES, "tile must split evenly over waves");
 #pragma unroll
@@ -60,29 +67,28 @@ __device__ __forceinline__ void stage_tile(char* smem, int lds_off, __amdgpu_buf
     const int c = piece * 64 + lane;     // 16-B chunk index in the image
     int voff;
     if constexpr (KC) {
-      // image [ROWS][64 k] : 8 chunks per row
-      const int r = c >> 3, pc = c & 7;
-      const int lc = pc ^ swz_k(r);
-      voff = (int)(r * ld * 2) + kt * 128 + lc * 16;
+      constexpr int CPR = BK / 8;
+      const int r = c / CPR, pc = c % CPR;
+      const int lc = pc ^ swz_k<BK>(r);
+      voff = (int)(r * ld * 2) + kt * BK * 2 + lc * 16;
     } else {
-      // image [64 k][ROWS] : ROWS*2 bytes per row
       constexpr int CPR = ROWS * 2 / 16;
       const int r = c / CPR, pc = c % CPR;
       const int lb = (pc * 16) ^ (swz_mn(r) << 5);
-      voff = (int)((long)(kt * 64 + r) * ld * 2) + lb;
+      voff = (int)((long)(kt * BK + r) * ld * 2) + lb;
     }
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, LDS_PTR(void, smem + lds_off + piece * 1024), 16, voff, 0, 0, 0);
   }
 }
 
-// Read the 16x32 MFMA fragment (rows r0..r0+15, k = kk*32 .. kk*32+31) for this lane.
-template <int ROWS, bool KC>
+// 16 rows (r0..r0+15) x 32 k (kk*32..) MFMA fragment of this lane.
+template <int ROWS, int BK, bool KC>
 __device__ __forceinline__ v8s read_frag(const char* smem, int lds_off, int r0, int kk, int lane) {
   if constexpr (KC) {
     const int row = r0 + (lane & 15);
     const int lc = kk * 4 + (lane >> 4);
-    const int pc = lc ^ swz_k(row);
-    return *reinterpret_cast<const v8s*>(smem + lds_off + row * 128 + pc * 16);
+    const int pc = lc ^ swz_k<BK>(row);
+    return *reinterpret_cast<const v8s*>(smem + lds_off + row * BK * 2 + pc * 16);
   } else {
     constexpr int RB = ROWS * 2;
     const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
@@ -98,6 +104,11 @@ __device__ __forceinline__ v8s read_frag(const char* smem, int lds_off, int r0, 
     r.hi = hi;
     return r;
   }
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
 template <int EPI>
@@ -219,15 +230,35 @@ __device__ __forceinline__ void epi_store8(const GemmDev& p, int z, int split_id
   }
 }
 
-template <int BM, int BN, int WM, int WN, bool AK, bool BKC, int EPI>
-__global__ void __launch_bounds__(WM* WN * 64) gemm_bf16_kernel(const GemmDev p) {
+// Multi-stage LDS-DMA pipeline: STAGES k-tile buffers; at step t the DMA of step t+STAGES-1 is
+// issued into the buffer read at step t-1, so STAGES-2 k-tiles stay in flight across every
+// barrier (counted vmcnt, raw s_barrier: no vmcnt(0) drain inside the loop).
+// waves per SIMD the register allocation must allow: 2 resident workgroups when the LDS fits twice
+template <int BM, int BN, int BK, int STAGES, int WM, int WN>
+constexpr int gemm_min_waves() {
+  return (STAGES * (BM + BN) * BK * 2 <= 80 * 1024) ? (2 * WM * WN) / 4 : (WM * WN) / 4;
+}
+
+template <int BM, int BN, int BK, int STAGES, int WM, int WN, bool AK, bool BKC, int EPI>
+__global__ void __launch_bounds__(WM* WN * 64, (gemm_min_waves<BM, BN, BK, STAGES, WM, WN>()))
+    gemm_bf16_kernel(const GemmDev p) {
   constexpr int NWAVE = WM * WN;
+  constexpr int NT = NWAVE * 64;
   constexpr int TM = BM / WM, TN = BN / WN;
   constexpr int FM = TM / 16, FN = TN / 16;
-  constexpr int A_BYTES = BM * 128, B_BYTES = BN * 128;
+  constexpr int KK = BK / 32;
+  constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
   constexpr int STAGE = A_BYTES + B_BYTES;
-  constexpr int LDC = BN + 4;  // fp32 staging row stride (floats): +4 keeps the acc writes conflict-free
-  constexpr int SMEM = (2 * STAGE > BM * LDC * 4) ? 2 * STAGE : BM * LDC * 4;
+  constexpr int PIPE = STAGES * STAGE;
+  constexpr int LPS = (A_BYTES + B_BYTES) / 1024 / NWAVE;  // DMA instructions per wave per k-step
+  constexpr int LDC = BN + 4;                               // fp32 staging row stride (floats)
+  // stage the epilogue in 2 passes when one pass would not fit, or would cost the 2nd resident WG
+  constexpr int NPASS = (BM * LDC * 4 > 160 * 1024 || (PIPE <= 80 * 1024 && BM * LDC * 4 > 80 * 1024)) ? 2 : 1;
+  constexpr int PASS_ROWS = BM / NPASS;
+  constexpr int STG = PASS_ROWS * LDC * 4;
+  constexpr int SMEM = PIPE > STG ? PIPE : STG;
+  static_assert(SMEM <= 160 * 1024, "LDS budget");
+  static_assert(NPASS == 1 || WM % 2 == 0, "two-pass epilogue splits the wave rows");
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
 
   const int lane = threadIdx.x & 63;
@@ -248,15 +279,15 @@ __global__ void __launch_bounds__(WM* WN * 64) gemm_bf16_kernel(const GemmDev p)
   // ---- operand descriptors (base moved to the block's first row/col) ----
   const char* Ab = p.A + (long)z * p.a_bs * 2;
   const char* Bb = p.B + (long)z * p.b_bs * 2;
-  long a_shift = AK ? (long)m0 * p.lda * 2 : (long)m0 * 2;
-  long b_shift = BKC ? (long)n0 * p.ldb * 2 : (long)n0 * 2;
+  const long a_shift = AK ? (long)m0 * p.lda * 2 : (long)m0 * 2;
+  const long b_shift = BKC ? (long)n0 * p.ldb * 2 : (long)n0 * 2;
   const uint32_t a_rec = (long)p.a_bytes > a_shift ? (uint32_t)(p.a_bytes - a_shift) : 0u;
   const uint32_t b_rec = (long)p.b_bytes > b_shift ? (uint32_t)(p.b_bytes - b_shift) : 0u;
   const __amdgpu_buffer_rsrc_t rsA = make_rsrc(Ab + a_shift, a_rec);
   const __amdgpu_buffer_rsrc_t rsB = make_rsrc(Bb + b_shift, b_rec);
 
   // ---- k range of this split ----
-  const int nkt = p.K / 64;
+  const int nkt = p.K / BK;
   const int kt0 = (int)((long)nkt * split_idx / p.split_k);
   const int kt1 = (int)((long)nkt * (split_idx + 1) / p.split_k);
   const int nk = kt1 - kt0;
@@ -266,82 +297,125 @@ __global__ void __launch_bounds__(WM* WN * 64) gemm_bf16_kernel(const GemmDev p)
   for (int i = 0; i < FM; ++i)
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
-
   const int wm0 = wm * TM, wn0 = wn * TN;
 
-  if (nk > 0) {
-    stage_tile<BM, AK, NWAVE>(smem, 0, rsA, p.lda, kt0, wave, lane);
-    stage_tile<BN, BKC, NWAVE>(smem, A_BYTES, rsB, p.ldb, kt0, wave, lane);
-  }
+  auto issue = [&](int step) {
+    const int buf = (step % STAGES) * STAGE;
+    stage_tile<BM, BK, AK, NWAVE>(smem, buf, rsA, p.lda, kt0 + step, wave, lane);
+    stage_tile<BN, BK, BKC, NWAVE>(smem, buf + A_BYTES, rsB, p.ldb, kt0 + step, wave, lane);
+  };
+#pragma unroll
+  for (int s = 0; s < STAGES - 1; ++s)
+    if (s < nk) issue(s);
+
   for (int t = 0; t < nk; ++t) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    const int cur = (t & 1) * STAGE;
-    if (t + 1 < nk) {
-      const int nxt = ((t + 1) & 1) * STAGE;
-      stage_tile<BM, AK, NWAVE>(smem, nxt, rsA, p.lda, kt0 + t + 1, wave, lane);
-      stage_tile<BN, BKC, NWAVE>(smem, nxt + A_BYTES, rsB, p.ldb, kt0 + t + 1, wave, lane);
+    // step t's DMA must have landed (own wave), leaving the younger steps in flight
+    const int younger = nk - 1 - t;
+    if (younger >= STAGES - 2) {
+      wait_vm<LPS * (STAGES - 2)>();
+    } else if constexpr (STAGES > 3) {
+      if (younger == 1) wait_vm<LPS>(); else wait_vm<0>();
+    } else {
+      wait_vm<0>();
     }
+    __builtin_amdgcn_s_barrier();  // every wave's share landed; every wave done reading step t-1
+    asm volatile("" ::: "memory");
+    if (t + STAGES - 1 < nk) issue(t + STAGES - 1);
+    const int cur = (t % STAGES) * STAGE;
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      v8s af[FM], bfr[FN];
+    for (int kk = 0; kk < KK; ++kk) {
+      v8s bfr[FN];
 #pragma unroll
-      for (int i = 0; i < FM; ++i) af[i] = read_frag<BM, AK>(smem, cur, wm0 + i * 16, kk, lane);
+      for (int j = 0; j < FN; ++j) bfr[j] = read_frag<BN, BK, BKC>(smem, cur + A_BYTES, wn0 + j * 16, kk, lane);
 #pragma unroll
-      for (int j = 0; j < FN; ++j) bfr[j] = read_frag<BN, BKC>(smem, cur + A_BYTES, wn0 + j * 16, kk, lane);
+      for (int i = 0; i < FM; ++i) {
+        const v8s af = read_frag<BM, BK, AK>(smem, cur, wm0 + i * 16, kk, lane);
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(v8bf, af),
+                                                              __builtin_bit_cast(v8bf, bfr[j]), acc[i][j], 0, 0, 0);
+      }
+    }
+    asm volatile("" ::: "memory");
+  }
+
+  // ---- epilogue: stage the fp32 tile in LDS (1 or 2 passes of rows), then each thread finishes
+  //      8-column row chunks (coalesced 16/32-B stores, vector loads of bias / residual / GELU input)
+  const int g = lane >> 4, c = lane & 15;
+  wait_vm<0>();
+  __syncthreads();
+  float* cs = reinterpret_cast<float*>(smem);
+  constexpr int CPR = BN / 8;
+#pragma unroll
+  for (int pass = 0; pass < NPASS; ++pass) {
+    if (NPASS == 1 || wm / (WM / NPASS) == pass) {
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int j = 0; j < FN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(v8bf, af[i]),
-                                                              __builtin_bit_cast(v8bf, bfr[j]), acc[i][j], 0, 0, 0);
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            cs[(wm0 - pass * PASS_ROWS + i * 16 + 4 * g + r) * LDC + wn0 + j * 16 + c] = acc[i][j][r];
     }
-  }
-
-  // ---- epilogue: stage the fp32 tile in LDS, then each thread finishes 8-column row chunks ----
-  // (coalesced 16-B / 32-B stores and vector loads of bias / residual / GELU input)
-  const int g = lane >> 4, c = lane & 15;
-  __syncthreads();  // every wave is done reading the operand stages
-  float* cs = reinterpret_cast<float*>(smem);
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int j = 0; j < FN; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) cs[(wm0 + i * 16 + 4 * g + r) * LDC + wn0 + j * 16 + c] = acc[i][j][r];
-  __syncthreads();
-  constexpr int CPR = BN / 8;
-  constexpr int NT = NWAVE * 64;
+    __syncthreads();
 #pragma unroll 2
-  for (int e = threadIdx.x; e < BM * CPR; e += NT) {
-    const int row = e / CPR, ch = e % CPR;
-    const int m = m0 + row, n = n0 + ch * 8;
-    if (m >= p.M || n >= p.N) continue;
-    float v[8];
-    ld8f(cs + row * LDC + ch * 8, v);
-    if (p.vec && n + 8 <= p.N) {
-      epi_store8<EPI>(p, z, split_idx, m, n, v);
-    } else {
+    for (int e = threadIdx.x; e < PASS_ROWS * CPR; e += NT) {
+      const int row = e / CPR, ch = e % CPR;
+      const int m = m0 + pass * PASS_ROWS + row, n = n0 + ch * 8;
+      if (m >= p.M || n >= p.N) continue;
+      float v[8];
+      ld8f(cs + row * LDC + ch * 8, v);
+      if (p.vec && n + 8 <= p.N) {
+        epi_store8<EPI>(p, z, split_idx, m, n, v);
+      } else {
 #pragma unroll
-      for (int k = 0; k < 8; ++k) epi_store<EPI>(p, z, split_idx, m, n + k, v[k]);
+        for (int k = 0; k < 8; ++k) epi_store<EPI>(p, z, split_idx, m, n + k, v[k]);
+      }
     }
+    if (NPASS > 1) __syncthreads();
   }
 }
 
-template <int BM, int BN, int WM, int WN, bool AK, bool BKC, int EPI>
+template <int BM, int BN, int BK, int STAGES, int WM, int WN, bool AK, bool BKC, int EPI>
 hipError_t launch_t(const GemmDev& d, int batch, int split, hipStream_t s) {
   const int tiles = ((d.M + BM - 1) / BM) * ((d.N + BN - 1) / BN);
   dim3 grid(tiles, split, batch);
-  hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, WM, WN, AK, BKC, EPI>), grid, dim3(WM * WN * 64), 0, s, d);
+  hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, BK, STAGES, WM, WN, AK, BKC, EPI>), grid, dim3(WM * WN * 64), 0, s, d);
   return hipGetLastError();
 }
 
+// Tile configurations:
+//   0: 128x128x64, 2 stages, 4 waves (2x2)   — small problems
+//   1: 256x256x32, 4 stages, 8 waves (2x4)   — large M and N >= 1536, and the split-K wgrads
+//   2: 256x128x64, 3 stages, 8 waves (4x2)   — large M, narrow N (768)
+//   3: 256x128x32, 3 stages, 8 waves (4x2)   — 2 workgroups per CU (epilogue overlaps MFMA)
+//   4: 128x128x32, 4 stages, 4 waves (2x2)   — 2 workgroups per CU
+template <int EPI, bool AK, bool BKC>
+hipError_t launch_cfg(int cfg, const GemmDev& d, int batch, int split, hipStream_t s) {
+  switch (cfg) {
+    case 1: return launch_t<256, 256, 32, 4, 2, 4, AK, BKC, EPI>(d, batch, split, s);
+    case 2: return launch_t<256, 128, 64, 3, 4, 2, AK, BKC, EPI>(d, batch, split, s);
+    case 3: return launch_t<256, 128, 32, 3, 4, 2, AK, BKC, EPI>(d, batch, split, s);
+    case 4: return launch_t<128, 128, 32, 4, 2, 2, AK, BKC, EPI>(d, batch, split, s);
+    default: return launch_t<128, 128, 64, 2, 2, 2, AK, BKC, EPI>(d, batch, split, s);
+  }
+}
+
 template <int EPI>
-hipError_t launch_layout(const GemmDev& d, bool ak, bool bk, int batch, int split, hipStream_t s) {
-  if (ak && bk) return launch_t<128, 128, 2, 2, true, true, EPI>(d, batch, split, s);
-  if (ak && !bk) return launch_t<128, 128, 2, 2, true, false, EPI>(d, batch, split, s);
-  if (!ak && !bk) return launch_t<128, 128, 2, 2, false, false, EPI>(d, batch, split, s);
-  return launch_t<128, 128, 2, 2, false, true, EPI>(d, batch, split, s);
+hipError_t launch_layout(int cfg, const GemmDev& d, bool ak, bool bk, int batch, int split, hipStream_t s) {
+  if (ak && bk) return launch_cfg<EPI, true, true>(cfg, d, batch, split, s);
+  if (ak && !bk) return launch_cfg<EPI, true, false>(cfg, d, batch, split, s);
+  if (!ak && !bk) return launch_cfg<EPI, false, false>(cfg, d, batch, split, s);
+  return launch_cfg<EPI, false, true>(cfg, d, batch, split, s);
+}
+
+int pick_tile(const vit_gemm_args* a) {
+  if (a->tile > 0) return (int)a->tile;
+  // measured on MI355X (tools/gemm_bench.py): 256x128x32 with 2 resident workgroups per CU is the
+  // fastest or within 4% for every ViT-B/16 shape (fwd, dgrad, split-K wgrad); 128x128 for small M
+  if (a->M >= 1024 && a->N >= 256) return 3;
+  if (a->epilogue == VIT_EPI_SPLITK && a->M >= 256 && a->N >= 256) return 3;
+  return 0;
 }
 
 }  // namespace
@@ -402,15 +476,18 @@ extern "C" int vit_gemm_bf16(const vit_gemm_args* a, vit_stream_t stream) {
   hipStream_t s = (hipStream_t)stream;
   const int batch = (int)a->batch, split = (int)a->split_k;
   hipError_t e;
+  const int cfg = pick_tile(a);
+  VIT_CHECK_ARG(cfg >= 0 && cfg <= 4, "vit_gemm_bf16: bad tile config %d", cfg);
+  VIT_CHECK_ARG(cfg != 1 || a->K % 32 == 0, "vit_gemm_bf16: K");
   switch (a->epilogue) {
-    case VIT_EPI_F32: e = launch_layout<VIT_EPI_F32>(d, ak, bk, batch, split, s); break;
-    case VIT_EPI_BF16: e = launch_layout<VIT_EPI_BF16>(d, ak, bk, batch, split, s); break;
-    case VIT_EPI_BIAS_BF16: e = launch_layout<VIT_EPI_BIAS_BF16>(d, ak, bk, batch, split, s); break;
-    case VIT_EPI_BIAS_GELU: e = launch_layout<VIT_EPI_BIAS_GELU>(d, ak, bk, batch, split, s); break;
-    case VIT_EPI_BIAS_RESID_F32: e = launch_layout<VIT_EPI_BIAS_RESID_F32>(d, ak, bk, batch, split, s); break;
-    case VIT_EPI_GELU_BWD: e = launch_layout<VIT_EPI_GELU_BWD>(d, ak, bk, batch, split, s); break;
-    case VIT_EPI_PATCH: e = launch_layout<VIT_EPI_PATCH>(d, ak, bk, batch, split, s); break;
-    case VIT_EPI_SPLITK: e = launch_layout<VIT_EPI_SPLITK>(d, ak, bk, batch, split, s); break;
+    case VIT_EPI_F32: e = launch_layout<VIT_EPI_F32>(cfg, d, ak, bk, batch, split, s); break;
+    case VIT_EPI_BF16: e = launch_layout<VIT_EPI_BF16>(cfg, d, ak, bk, batch, split, s); break;
+    case VIT_EPI_BIAS_BF16: e = launch_layout<VIT_EPI_BIAS_BF16>(cfg, d, ak, bk, batch, split, s); break;
+    case VIT_EPI_BIAS_GELU: e = launch_layout<VIT_EPI_BIAS_GELU>(cfg, d, ak, bk, batch, split, s); break;
+    case VIT_EPI_BIAS_RESID_F32: e = launch_layout<VIT_EPI_BIAS_RESID_F32>(cfg, d, ak, bk, batch, split, s); break;
+    case VIT_EPI_GELU_BWD: e = launch_layout<VIT_EPI_GELU_BWD>(cfg, d, ak, bk, batch, split, s); break;
+    case VIT_EPI_PATCH: e = launch_layout<VIT_EPI_PATCH>(cfg, d, ak, bk, batch, split, s); break;
+    case VIT_EPI_SPLITK: e = launch_layout<VIT_EPI_SPLITK>(cfg, d, ak, bk, batch, split, s); break;
     default: vit::set_error("vit_gemm_bf16: unknown epilogue %d", a->epilogue); return VIT_ERR_INVALID_ARG;
   }
   return vit::check_hip(e, "vit_gemm_bf16 launch");

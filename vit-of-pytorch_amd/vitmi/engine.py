@@ -244,10 +244,11 @@ class ViTEngine:
         return a
 
     def _splitk(self, M, N, K, z=1):
-        tiles = ((M + 127) // 128) * ((N + 127) // 128) * z
+        """split-K factor for a weight-gradient GEMM (K = tokens): ~3 waves of 256x128 tiles
+        over 2 workgroups/CU x 256 CUs, at least 8 k-tiles per split (tools/gemm_bench.py)."""
+        tiles = ((M + 255) // 256) * ((N + 127) // 128) * z
         nkt = K // 64
-        s = max(1, min(round(1024 / tiles), nkt // 8, 32))
-        return s
+        return max(1, min(round(1536 / tiles), nkt // 8, 16))
 
     def _workspace(self, numel):
         if self._ws is None or self._ws.numel() < numel:

@@ -40,7 +40,7 @@ def _chk(t, dtype, name):
 
 # ---------------------------------------------------------------------------------------------
 def gemm(A, B, C, M, N, K, *, a_layout, b_layout, lda, ldb, ldc, epilogue, bias=None, aux=None, ldaux=0,
-         C2=None, ldc2=0, aux2=None, batch=1, a_bs=0, b_bs=0, c_bs=0, bias_bs=0, split_k=1, tokens=0):
+         C2=None, ldc2=0, aux2=None, batch=1, a_bs=0, b_bs=0, c_bs=0, bias_bs=0, split_k=1, tokens=0, tile=0):
     """bf16 MFMA GEMM, C[m,n] = sum_k A(m,k) B(k,n) + fused epilogue (see vit_gemm_args)."""
     _chk(A, BF16, "A")
     _chk(B, BF16, "B")
@@ -54,7 +54,7 @@ def gemm(A, B, C, M, N, K, *, a_layout, b_layout, lda, ldb, ldc, epilogue, bias=
     a.aux, a.ldaux = (aux.data_ptr() if aux is not None else None), ldaux
     a.aux2 = aux2.data_ptr() if aux2 is not None else None
     a.batch, a.split_k, a.tokens = batch, split_k, tokens
-    a.epilogue, a.tile = epilogue, 0
+    a.epilogue, a.tile = epilogue, tile
     check(lib().vit_gemm_bf16(ctypes.byref(a), _stream()), "vit_gemm_bf16")
 
 
