@@ -90,7 +90,7 @@ def main():
     dev = torch.device("cuda", local)
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        dist.init_process_group(os.environ.get("VITMI_DIST_BACKEND", "nccl"), device_id=dev)
 
     from vitmi import ops
     from vitmi.dist import GradAllReducer
@@ -112,7 +112,7 @@ def main():
     x = torch.randn(b, 3, args.image_size, args.image_size, device=dev, generator=g)
     y = torch.randint(0, args.num_classes, (b,), device=dev, generator=g)
     mom_buf = torch.zeros_like(eng.flat)
-    reducer = GradAllReducer(eng).attach() if world > 1 else None
+    reducer = GradAllReducer(eng, average=False).attach() if world > 1 else None  # CE pre-scaled by 1/(b*world)
     total_steps = args.warmup + args.steps
     # OneCycleLR schedule scalars as configured by reference src/train.py:159-163 (lr .03, 500 warmup/15000)
     from torch.optim.lr_scheduler import OneCycleLR

@@ -1,0 +1,81 @@
+"""Data-parallel gradient exchange (vitmi.dist.GradAllReducer) on a 2-rank gloo group (CPU)."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+class _FakeLayout:
+    def __init__(self, sizes):
+        self.buckets = []
+        off = 0
+        names = ["head"] + [f"layer{i}" for i in reversed(range(len(sizes) - 2))] + ["embed"]
+        for n, s in zip(names, sizes):
+            self.buckets.append((n, off, off + s))
+            off += s
+        self.numel = off
+
+
+class _FakeEngine:
+    """Stands in for vitmi.engine.ViTEngine: a flat CPU grad buffer + bucket layout + hook slot."""
+
+    def __init__(self, sizes):
+        self.layout = _FakeLayout(sizes)
+        self.grad = torch.zeros(self.layout.numel)
+        self.dev = torch.device("cpu")
+        self.grad_ready_hook = None
+
+    def backward(self, rank):
+        # fill each bucket as the real backward would, releasing it through the hook in order
+        for name, s, e in self.layout.buckets:
+            self.grad[s:e] = torch.arange(s, e, dtype=torch.float32) * (rank + 1)
+            if self.grad_ready_hook:
+                self.grad_ready_hook(self.grad, name, s, e)
+
+
+def _worker(rank, world, port, sizes, average, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from vitmi.dist import GradAllReducer
+    eng = _FakeEngine(sizes)
+    red = GradAllReducer(eng, min_bucket_elems=50, average=average).attach()
+    for _ in range(2):  # two steps: buckets re-used
+        eng.backward(rank)
+        red.finish()
+    q.put((rank, eng.grad.clone()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.parametrize("average", [True, False])
+def test_grad_allreduce_gloo_world2(average):
+    world = 2
+    sizes = [10, 100, 100, 100, 37]  # head (coalesced with layer2: below min_bucket), layers, embed
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, sizes, average, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    n = sum(sizes)
+    base = torch.arange(n, dtype=torch.float32)
+    expect = base * (1 + 2) / (world if average else 1)
+    for r in range(world):
+        assert torch.allclose(res[r], expect), r
+    assert torch.equal(res[0], res[1])  # replicas bit-identical

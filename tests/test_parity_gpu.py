@@ -25,7 +25,7 @@ B16 = ViTConfig()
 
 
 def rel(a, b):
-    a = torch.as_tensor(a).double().cpu()
+    a = torch.as_tensor(a).detach().double().cpu()
     b = torch.as_tensor(b).double().cpu()
     return float((a - b).norm() / b.norm().clamp_min(1e-30))
 

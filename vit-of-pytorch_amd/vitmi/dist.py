@@ -7,10 +7,12 @@ backward-completion order, so each encoder layer's gradients form one contiguous
 all-reduced on a side stream as soon as the engine's backward releases it (grad_ready_hook),
 while the backward of the layers below keeps running on the compute stream.
 
-Gradient scaling: each rank's cross entropy is scaled by 1/(b * world), the buckets are summed,
-which equals the global-batch mean gradient of the reference's DataParallel CE (computed on the
-gathered batch). Replicas stay bit-identical because every rank applies the same SGD update to the
-same all-reduced gradient.
+Gradient scaling: with average=True (default) the buckets are averaged over ranks (ReduceOp.AVG on
+RCCL; SUM followed by a 1/world scale on backends without AVG, e.g. gloo), so a per-rank mean
+cross entropy yields the global-batch mean gradient of the reference's DataParallel CE (computed on
+the gathered batch). With average=False the buckets are summed (the caller pre-scales the loss by
+1/(b*world), as bench.py does). Replicas stay bit-identical because every rank applies the same SGD
+update to the same all-reduced gradient.
 """
 from __future__ import annotations
 
@@ -19,10 +21,14 @@ import torch.distributed as dist
 
 
 class GradAllReducer:
-    def __init__(self, engine, group=None, min_bucket_elems=1 << 20):
+    def __init__(self, engine, group=None, min_bucket_elems=1 << 20, average=True):
         self.engine = engine
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.average = average
+        backend = dist.get_backend(group) if dist.is_initialized() else None
+        self.native_avg = average and backend == "nccl"
+        self._to_scale = []
         self.cuda = engine.dev.type == "cuda"
         self.stream = torch.cuda.Stream(device=engine.dev) if self.cuda else None
         self.min_bucket = min_bucket_elems
@@ -38,14 +44,17 @@ class GradAllReducer:
 
     def _launch(self, buf, start, end):
         t = buf[start:end]
+        op = dist.ReduceOp.AVG if self.native_avg else dist.ReduceOp.SUM
+        if self.average and not self.native_avg:
+            self._to_scale.append(t)
         if self.cuda:
             ev = torch.cuda.Event()
             ev.record(torch.cuda.current_stream(self.engine.dev))
             self.stream.wait_event(ev)
             with torch.cuda.stream(self.stream):
-                dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
+                dist.all_reduce(t, op=op, group=self.group)
         else:
-            self._works.append(dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group, async_op=True))
+            self._works.append(dist.all_reduce(t, op=op, group=self.group, async_op=True))
 
     def hook(self, buf, name, start, end):
         if self.world == 1:
@@ -68,3 +77,6 @@ class GradAllReducer:
             for w in self._works:
                 w.wait()
             self._works = []
+        for t in self._to_scale:
+            t.mul_(1.0 / self.world)
+        self._to_scale = []

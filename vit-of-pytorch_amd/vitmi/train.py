@@ -1,0 +1,240 @@
+"""Training driver, mirroring reference src/train.py on the MI355X HIP engine.
+
+    python -m vitmi.train --model-arch b16 --batch-size 256 --synthetic --checkpoint-path "" --no-save
+    torchrun --nproc-per-node 8 -m vitmi.train ...   # data parallel, one process per GPU (RCCL)
+
+Entry points keep the reference signatures: train_epoch (src/train.py:12-37), valid_epoch (:40-66),
+save_model (:69-81), main (:84-194). Differences, all on the execution side:
+  * the model is vitmi.model.VisionTransformer (HIP engine), the optimizer vitmi.optim.SGD
+    (torch.optim.SGD semantics, fused HIP update), the scheduler torch's OneCycleLR as configured
+    by the reference (:159-163);
+  * multi-GPU is one process per GPU with gradient all-reduce over RCCL overlapped with the
+    backward (vitmi.dist), instead of single-process nn.DataParallel (:128-129);
+  * loss / accuracy are accumulated on the device and read back when printed, instead of three
+    .item() host syncs per step (:29-32); the reported means are the same.
+"""
+from __future__ import annotations
+
+import os
+import random
+import sys
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from .config import get_train_config
+from .dist import GradAllReducer
+from .model import CrossEntropyLoss, VisionTransformer
+from .optim import SGD
+
+
+def set_seed(seed=42):
+    """reference src/data_loaders.py:13-29"""
+    random.seed(seed)
+    np.random.seed(seed)
+    torch.manual_seed(seed)
+    torch.cuda.manual_seed_all(seed)
+    os.environ["PYTHONHASHSEED"] = str(seed)
+
+
+def accuracy(output, target, topk=(1,)):
+    """top-k precision in percent (reference src/utils.py:28-41)."""
+    maxk = max(topk)
+    batch_size = target.size(0)
+    _, pred = output.topk(maxk, 1, True, True)
+    pred = pred.t()
+    correct = pred.eq(target.view(1, -1).expand_as(pred))
+    return [correct[:k].reshape(-1).float().sum(0) / batch_size * 100.0 for k in topk]
+
+
+class MetricTracker:
+    """Running means of named scalars (reference src/utils.py:79-100), device-resident."""
+
+    def __init__(self, *keys, writer=None):
+        self.writer = writer
+        self.keys = keys
+        self.reset()
+
+    def reset(self):
+        self._total = {k: 0.0 for k in self.keys}
+        self._count = {k: 0 for k in self.keys}
+
+    def update(self, key, value, n=1):
+        self._total[key] = self._total[key] + value * n
+        self._count[key] += n
+
+    def avg(self, key):
+        t = self._total[key]
+        t = float(t) if torch.is_tensor(t) else t
+        return t / max(1, self._count[key])
+
+    def result(self):
+        return {k: self.avg(k) for k in self.keys}
+
+
+class SyntheticDataLoader:
+    """Synthetic N(0,1) images / uniform labels generated on the device (no host copies)."""
+
+    def __init__(self, batch_size, image_size, num_classes, steps, device, seed=0):
+        self.batch_size, self.image_size, self.num_classes, self.steps = batch_size, image_size, num_classes, steps
+        g = torch.Generator(device=device).manual_seed(seed)
+        self.x = torch.randn(batch_size, 3, image_size, image_size, device=device, generator=g)
+        self.y = torch.randint(0, num_classes, (batch_size,), device=device, generator=g)
+
+    def __len__(self):
+        return self.steps
+
+    def __iter__(self):
+        for _ in range(self.steps):
+            yield self.x, self.y
+
+
+def _world():
+    return dist.get_world_size() if dist.is_initialized() else 1
+
+
+def train_epoch(epoch, model, data_loader, criterion, optimizer, lr_scheduler, metrics, device=torch.device("cpu"),
+                reducer=None, log_every=100):
+    """reference src/train.py:12-37 (one optimizer step per batch)."""
+    metrics.reset()
+    for batch_idx, (batch_data, batch_target) in enumerate(data_loader):
+        batch_data = batch_data.to(device, non_blocking=True)
+        batch_target = batch_target.to(device, non_blocking=True)
+        optimizer.zero_grad()
+        batch_pred = model(batch_data)
+        loss = criterion(batch_pred, batch_target)
+        loss.backward()
+        if reducer is not None:
+            reducer.finish()
+        optimizer.step()
+        lr_scheduler.step()
+        acc1, acc5 = accuracy(batch_pred.detach(), batch_target, topk=(1, 5))
+        metrics.update("loss", loss.detach())
+        metrics.update("acc1", acc1)
+        metrics.update("acc5", acc5)
+        if batch_idx % log_every == 0 and (not dist.is_initialized() or dist.get_rank() == 0):
+            print("Train Epoch: {:03d} Batch: {:05d}/{:05d} Loss: {:.4f} Acc@1: {:.2f}, Acc@5: {:.2f}"
+                  .format(epoch, batch_idx, len(data_loader), float(loss.detach()), float(acc1), float(acc5)), flush=True)
+    return metrics.result()
+
+
+def valid_epoch(epoch, model, data_loader, criterion, metrics, device=torch.device("cpu")):
+    """reference src/train.py:40-66 (forward-only)."""
+    metrics.reset()
+    losses, acc1s, acc5s = [], [], []
+    with torch.no_grad():
+        for batch_data, batch_target in data_loader:
+            batch_data = batch_data.to(device)
+            batch_target = batch_target.to(device)
+            batch_pred = model(batch_data)
+            loss = criterion(batch_pred, batch_target)
+            acc1, acc5 = accuracy(batch_pred, batch_target, topk=(1, 5))
+            losses.append(loss)
+            acc1s.append(acc1)
+            acc5s.append(acc5)
+    metrics.update("loss", float(torch.stack(losses).mean()))
+    metrics.update("acc1", float(torch.stack(acc1s).mean()))
+    metrics.update("acc5", float(torch.stack(acc5s).mean()))
+    return metrics.result()
+
+
+def save_model(save_dir, epoch, model, optimizer, lr_scheduler, device_ids=(), best=False):
+    """Checkpoint format of reference src/train.py:69-81."""
+    state = {
+        "epoch": epoch,
+        "state_dict": model.state_dict(),
+        "optimizer": optimizer.state_dict(),
+        "lr_scheduler": lr_scheduler.state_dict(),
+    }
+    torch.save(state, str(save_dir + "current.pth"))
+    if best:
+        torch.save(state, str(save_dir + "best.pth"))
+
+
+def load_checkpoint(path):
+    """Weights of a reference .pth checkpoint (src/checkpoint.py:7-17, pth branch)."""
+    if not path.endswith("pth"):
+        raise NotImplementedError("only .pth checkpoints are supported (JAX .npz import is a later round)")
+    return torch.load(path, map_location="cpu", weights_only=True)["state_dict"]
+
+
+def build_model(config, device):
+    return VisionTransformer(image_size=(config.image_size, config.image_size),
+                             patch_size=(config.patch_size, config.patch_size), emb_dim=config.emb_dim,
+                             mlp_dim=config.mlp_dim, num_heads=config.num_heads, num_layers=config.num_layers,
+                             num_classes=config.num_classes, attn_dropout_rate=config.attn_dropout_rate,
+                             dropout_rate=config.dropout_rate)
+
+
+def main(argv=None):
+    config = get_train_config(argv)
+    set_seed(config.seed)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if not torch.cuda.is_available():
+        raise SystemExit("vitmi.train needs a ROCm GPU (MI355X)")
+    torch.cuda.set_device(local)
+    device = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group(os.environ.get("VITMI_DIST_BACKEND", "nccl"), device_id=device)
+
+    model = build_model(config, device)
+    if config.checkpoint_path:
+        state_dict = load_checkpoint(config.checkpoint_path)
+        if config.num_classes != state_dict["classifier.weight"].size(0):
+            del state_dict["classifier.weight"]
+            del state_dict["classifier.bias"]
+            print("re-initialize fc layer")
+            model.load_state_dict(state_dict, strict=False)
+        else:
+            model.load_state_dict(state_dict)
+        print("Load pretrained weights from {}".format(config.checkpoint_path))
+    model = model.to(device)
+    engine = model.engine()
+    reducer = None
+    if world > 1:
+        dist.broadcast(engine.flat, 0)  # identical replicas
+        reducer = GradAllReducer(engine).attach()
+
+    if not config.synthetic:
+        raise SystemExit("torchvision datasets are not available in this environment; use --synthetic "
+                         "(the input pipeline is outside the MI355X hot path, SURVEY.md §2 row 5)")
+    train_loader = SyntheticDataLoader(config.batch_size, config.image_size, config.num_classes,
+                                       config.steps_per_epoch, device, seed=config.seed + rank)
+    valid_loader = SyntheticDataLoader(config.batch_size, config.image_size, config.num_classes,
+                                       max(1, config.steps_per_epoch // 10), device, seed=10_000 + config.seed + rank)
+
+    criterion = CrossEntropyLoss()
+    optimizer = SGD(params=model.parameters(), lr=config.lr, weight_decay=config.wd, momentum=0.9, model=model)
+    lr_scheduler = torch.optim.lr_scheduler.OneCycleLR(optimizer=optimizer, max_lr=config.lr,
+                                                       pct_start=config.warmup_steps / config.train_steps,
+                                                       total_steps=config.train_steps)
+    metric_names = ["loss", "acc1", "acc5"]
+    train_metrics = MetricTracker(*metric_names)
+    valid_metrics = MetricTracker(*metric_names)
+    best_acc = 0.0
+    epochs = max(1, config.train_steps // len(train_loader))
+    for epoch in range(1, epochs + 1):
+        log = {"epoch": epoch}
+        model.train()
+        log.update(train_epoch(epoch, model, train_loader, criterion, optimizer, lr_scheduler, train_metrics, device,
+                               reducer=reducer))
+        model.eval()
+        result = valid_epoch(epoch, model, valid_loader, criterion, valid_metrics, device)
+        log.update(**{"val_" + k: v for k, v in result.items()})
+        best = log["val_acc1"] > best_acc
+        if best:
+            best_acc = log["val_acc1"]
+        if rank == 0 and not config.no_save:
+            save_model(config.checkpoint_dir, epoch, model, optimizer, lr_scheduler, best=best)
+        if rank == 0:
+            for key, value in log.items():
+                print("    {:15s}: {}".format(str(key), value), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main(sys.argv[1:])
