@@ -89,11 +89,16 @@ typedef struct vit_gemm_args {
   int64_t batch;   /* >= 1 */
   int64_t split_k; /* >= 1; > 1 only with VIT_EPI_SPLITK */
   int64_t tokens;  /* VIT_EPI_PATCH: tokens per image */
+  float* col_partial; /* optional (batch 1, split_k 1): col_partial[tile_m * N + n] = sum over the
+                         tile's rows of the epilogue's output (bias-gradient partials); reduce the
+                         ceil(M / tile_rows) rows with vit_colsum. tile_rows: vit_gemm_tile_rows() */
   int32_t epilogue;
   int32_t tile;    /* 0 = auto */
 } vit_gemm_args;
 
 int vit_gemm_bf16(const vit_gemm_args* args, vit_stream_t stream);
+/* rows of C covered by one workgroup tile for these arguments (sizing of col_partial) */
+int64_t vit_gemm_tile_rows(const vit_gemm_args* args);
 
 /* out[z*out_batch_stride + m*ldo + n] (+)= sum_s ws[((z*split + s)*M + m)*N + n]  (f32) */
 int vit_splitk_reduce(const float* ws, int64_t batch, int64_t split, int64_t M, int64_t N,
@@ -104,9 +109,10 @@ int vit_splitk_reduce(const float* ws, int64_t batch, int64_t split, int64_t M, 
  * LayerNorm over the last dim (eps, biased variance, affine).  nn.LayerNorm src/model.py:108,114,146
  * fwd: y = (x - mean) * rstd * gamma + beta; saves mean/rstd (f32). y is bf16 or f32 (y_f32).
  * bwd: dx = rstd*(g - mean(g) - xhat*mean(g*xhat)), g = dy*gamma; dx_out = dres + dx (dres may
- *      be NULL); optional bf16 copy of dx_out. Writes per-block partial [nblk][2*D] sums of
- *      (dy*xhat, dy) into `partial` (>= vit_layernorm_bwd_partial_rows(rows) rows) and, when
- *      dgamma_dbeta != NULL, reduces them into dgamma_dbeta[0:D] (dgamma), [D:2D] (dbeta).
+ *      be NULL); optional bf16 copy of dx_out. Per-block partial sums [nblk][3*D] of
+ *      (dy*xhat, dy, dx_out) go to `partial` (>= vit_layernorm_bwd_partial_rows(rows) rows of 3*D);
+ *      when non-NULL, dgamma_dbeta[0:D] = dgamma, [D:2D] = dbeta, and dx_colsum[0:D] = column sums of
+ *      dx_out (= the bias gradient of the linear layer feeding this residual stream).
  * ---------------------------------------------------------------------------------------- */
 int vit_layernorm_fwd(const float* x, int64_t ldx, const float* gamma, const float* beta,
                       void* y, int64_t ldy, int32_t y_f32, float* mean, float* rstd,
@@ -116,20 +122,24 @@ int vit_layernorm_bwd(const void* dy, int64_t lddy, int32_t dy_f32, const float*
                       const float* mean, const float* rstd, const float* gamma,
                       const float* dres, int64_t lddres, float* dx, int64_t lddx,
                       void* dx_bf16, int64_t lddxb, float* partial, float* dgamma_dbeta,
-                      int32_t accumulate_params, int64_t rows, int64_t D, vit_stream_t stream);
+                      float* dx_colsum, int32_t accumulate_params, int64_t rows, int64_t D,
+                      vit_stream_t stream);
 
 /* ------------------------------------------------------------------------------------------
  * Fused multi-head self-attention, one (image, head) per workgroup, all keys in LDS.
  * qkv: bf16 [B*N, 3, H, hd] (q | k | v);  o: bf16 [B*N, H, hd];  lse: f32 [B, H, N]
  * S = (q k^T) * scale (scale = 1/sqrt(hd)), P = softmax(S), O = P v.
  * Replaces SelfAttention.forward src/model.py:90-97 (matmul, /scale, softmax, matmul, permutes)
- * bwd: dqkv (bf16 [B*N, 3, H, hd]) from dO, recomputing P from lse.
- * Limits: N <= 320, hd in {32, 64, 80(padded to 96)}.
+ * bwd: dqkv (bf16 [B*N, 3, H, hd]) from dO, recomputing P from lse; when bias_partial != NULL
+ *      it also receives per-image column sums of dq | dk | dv (f32 [B][3*H*hd], the q/k/v bias
+ *      gradient partials; reduce over B with vit_colsum).
+ * Limits: N <= 320, hd in {32, 64}.
  * ---------------------------------------------------------------------------------------- */
 int vit_attention_fwd(const void* qkv, void* o, float* lse, int64_t B, int64_t N, int64_t H,
                       int64_t hd, float scale, vit_stream_t stream);
 int vit_attention_bwd(const void* qkv, const void* o, const void* dout, const float* lse, void* dqkv,
-                      int64_t B, int64_t N, int64_t H, int64_t hd, float scale, vit_stream_t stream);
+                      float* bias_partial, int64_t B, int64_t N, int64_t H, int64_t hd, float scale,
+                      vit_stream_t stream);
 
 /* ------------------------------------------------------------------------------------------
  * Patch embedding im2col (Conv2d k=s=P as a GEMM, src/model.py:179,197-200):

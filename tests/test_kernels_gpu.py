@@ -68,6 +68,23 @@ def test_gemm_tiles_exact(al, bl, tile, M, N, K):
     assert torch.equal(C, A.float() @ B.float())
 
 
+@pytest.mark.parametrize("tile", [0, 3])
+def test_gemm_col_partial(tile):
+    M, N, K = 1000, 384, 256
+    A, B, Am, Bm, lda, ldb = _mats(M, N, K, K_CONTIG, MN_CONTIG)
+    U = torch.randn(M, N, device=DEV).bfloat16()
+    C = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    kw = dict(a_layout=K_CONTIG, b_layout=MN_CONTIG, lda=lda, ldb=ldb, ldc=N, epilogue=EPI_GELU_BWD, aux=U, ldaux=N,
+              tile=tile)
+    rows = ops.gemm_tile_rows(Am, Bm, C, M, N, K, **kw)
+    part = torch.full(((M + rows - 1) // rows, N), float("nan"), device=DEV)
+    ops.gemm(Am, Bm, C, M, N, K, col_partial=part, **kw)
+    u = U.float().requires_grad_(True)
+    gref, = torch.autograd.grad(torch.nn.functional.gelu(u), u, A.float() @ B.float())
+    assert rel(part.sum(0), gref.sum(0)) < 1e-3
+    assert rel(C.float(), gref) < 5e-3
+
+
 @pytest.mark.parametrize("tile", [1, 2])
 def test_gemm_tiles_epilogue_splitk(tile):
     M, N, K = 700, 520, 512
@@ -167,10 +184,12 @@ def test_layernorm(D):
     gx, gg, gb = torch.autograd.grad(ref, (x, g, b), dy.float())
     dx = torch.empty(rows, D, device=DEV)
     dxb = torch.empty(rows, D, device=DEV, dtype=torch.bfloat16)
-    part = torch.empty(ops.layernorm_bwd_partial_rows(rows), 2 * D, device=DEV)
+    part = torch.empty(ops.layernorm_bwd_partial_rows(rows), 3 * D, device=DEV)
     dgb = torch.empty(2 * D, device=DEV)
+    dsum = torch.empty(D, device=DEV)
     ops.layernorm_bwd(dy, D, x.detach(), D, mean, rstd, g.detach(), dx, D, part, rows, D, dres=dres, lddres=D,
-                      dx_bf16=dxb, lddxb=D, dgamma_dbeta=dgb)
+                      dx_bf16=dxb, lddxb=D, dgamma_dbeta=dgb, dx_colsum=dsum)
+    assert rel(dsum, (gx + dres).sum(0)) < 1e-4
     assert rel(dx, gx + dres) < 1e-4
     assert rel(dxb.float(), gx + dres) < 5e-3
     assert rel(dgb[:D], gg) < 1e-4
@@ -199,10 +218,15 @@ def test_attention(B, N, H, hd):
     assert rel(lse, lref.detach()) < 1e-4
     dout = torch.randn(B * N, D, device=DEV).bfloat16()
     dqkv = torch.full((B * N, 3 * D), float("nan"), device=DEV, dtype=torch.bfloat16)
-    ops.attention_bwd(qkv.detach(), o, dout, lse, dqkv, B, N, H, hd, 1.0 / math.sqrt(hd))
+    bpart = torch.full((B, 3 * D), float("nan"), device=DEV)
+    ops.attention_bwd(qkv.detach(), o, dout, lse, dqkv, B, N, H, hd, 1.0 / math.sqrt(hd), bias_partial=bpart)
     gref, = torch.autograd.grad(oref, qf, dout.float())
     gq, gk, gv = gref.view(B * N, 3, D).unbind(1)
     mq, mk, mv = dqkv.float().view(B * N, 3, D).unbind(1)
+    # per-image column sums (bias-gradient partials), dq | dk | dv; dk sums are ~0 (shift invariance)
+    bref = gref.view(B, N, 3 * D).sum(1)
+    assert rel(bpart[:, :D], bref[:, :D]) < 2e-2 and rel(bpart[:, 2 * D:], bref[:, 2 * D:]) < 2e-2
+    assert float((bpart[:, D:2 * D] - bref[:, D:2 * D]).abs().max()) < 1e-2 * float(bref.abs().max())
     assert rel(mq, gq) < 2e-2
     assert rel(mk, gk) < 2e-2
     assert rel(mv, gv) < 2e-2

@@ -161,3 +161,20 @@ def test_engine_fused_step_matches_oracle_sgd():
         if k.endswith("attn.key.bias") or float(upd_ref.norm()) < 1e-6:
             continue
         assert rel(upd, upd_ref) < 3e-2, (k, rel(upd, upd_ref))
+
+
+def test_b16_full_gradients_match_oracle():
+    """ViT-B/16 @224 tamed, bs 2: every gradient tensor (not just its norm) vs the oracle's (fp32 CPU)."""
+    params = tame_params(init_params(B16, seed=42))
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn(2, 3, 224, 224, generator=g)
+    y = torch.randint(0, 1000, (2,), generator=g)
+    ref_logits, ref_loss, ref_grads = loss_and_grads(params, x, y, B16)
+    m = make_model(B16, params)
+    from vitmi.model import CrossEntropyLoss
+    logits = m(x.cuda())
+    loss = CrossEntropyLoss()(logits, y.cuda())
+    loss.backward()
+    assert rel(logits, ref_logits) < 1e-2
+    assert abs(float(loss.detach()) - float(ref_loss)) <= 1e-3 * abs(float(ref_loss))
+    check_grads(m, ref_grads)

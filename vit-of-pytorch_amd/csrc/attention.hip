@@ -162,12 +162,26 @@ __global__ void __launch_bounds__(NW * 64) attn_fwd_kernel(const bf16_t* __restr
   }
 }
 
+// sum of the 16 lanes that share (lane >> 4): reduction over the MFMA column (key / query) index
+__device__ __forceinline__ float sum16(float v) {
+  v += __shfl_xor(v, 1, 64);
+  v += __shfl_xor(v, 2, 64);
+  v += __shfl_xor(v, 4, 64);
+  v += __shfl_xor(v, 8, 64);
+  return v;
+}
+
 // ------------------------------------------------------------------------------------------------
+// Backward. Phase 0 (query pairs): delta = rowsum(P * dP). Phase 1: each wave owns two 16-key tiles
+// (dK, dV); phase 2: two 16-query tiles (dQ). Q / dO / K / V fragments read from LDS are shared by
+// the two tiles. Optionally writes per-image column sums of
+// dQ, dK, dV (the q/k/v bias gradient partials) to bias_partial[b][3*D].
 template <int HD, int NKT, int NW>
 __global__ void __launch_bounds__(NW * 64) attn_bwd_kernel(const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ o,
                                                            const bf16_t* __restrict__ dout,
                                                            const float* __restrict__ lse, bf16_t* __restrict__ dqkv,
-                                                           int N, int H, int hd, float scale) {
+                                                           float* __restrict__ bias_partial, int N, int H, int hd,
+                                                           float scale) {
   constexpr int NP = NKT * 16;
   constexpr int IMG = NP * HD * 2;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -177,6 +191,7 @@ __global__ void __launch_bounds__(NW * 64) attn_bwd_kernel(const bf16_t* __restr
   char* Oi = smem + 3 * IMG;  // dO image
   float* lse_s = reinterpret_cast<float*>(smem + 4 * IMG);
   float* dlt_s = lse_s + NP;
+  float* bsum = dlt_s + NP;  // [NW][3][HD]
 
   const int bh = blockIdx.x, b = bh / H, h = bh % H;
   const int D = H * hd;
@@ -188,126 +203,248 @@ __global__ void __launch_bounds__(NW * 64) attn_bwd_kernel(const bf16_t* __restr
   load_image<HD>(Ki, base + D, rs, N, hd, NP);
   load_image<HD>(Vi, base + 2 * D, rs, N, hd, NP);
   load_image<HD>(Oi, dob, D, N, hd, NP);
-  for (int r = threadIdx.x; r < NP; r += blockDim.x) {
-    float d = 0.f, ls = INFINITY;
-    if (r < N) {
-      ls = lse[(long)bh * N + r] * LOG2E;
-      for (int k = 0; k < hd; k += 8) {
-        v8s a = *reinterpret_cast<const v8s*>(dob + (long)r * D + k);
-        v8s bb = *reinterpret_cast<const v8s*>(ob + (long)r * D + k);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) d += bf2f((bf16_t)a[j]) * bf2f((bf16_t)bb[j]);
-      }
-    }
-    lse_s[r] = ls;
-    dlt_s[r] = d;
-  }
+  (void)ob;
+  for (int r = threadIdx.x; r < NP; r += blockDim.x) lse_s[r] = r < N ? lse[(long)bh * N + r] * LOG2E : INFINITY;
   __syncthreads();
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int g = lane >> 4, i = lane & 15;
   const float c = scale * LOG2E;
-  const int nt_valid = (N + 15) / 16;       // 16-row tiles holding valid rows
-  const int ns_valid = (N + 31) / 32;       // 32-row steps holding valid rows
-  bf16_t* dq_base = dqkv + (long)b * N * rs + (long)h * hd;
+  const int npair = (N + 31) / 32;  // pairs of 16-row tiles holding valid rows
 
-  // ---- phase 1: dK, dV (key tiles owned by waves) ----
-  for (int kt = wave; kt < nt_valid; kt += NW) {
-    v8bf kf[HD / 32], vf[HD / 32];
+  // ---- phase 0: delta_q = sum_j P_qj dP_qj from the recomputed P and dP themselves ----
+  // (FlashAttention-2 uses rowsum(dO * O); with bf16 O that differs from sum_j P dP by O's rounding,
+  //  and dS = P (dP - delta) is a small difference of the two — near-uniform attention turned that
+  //  into 10-25% errors on the q/k weight gradients. The consistent delta costs two extra products.)
+  for (int qp = wave; qp < npair; qp += NW) {
+    v8bf qf[2][HD / 32], df[2][HD / 32];
+    float ls[2], dsum[2] = {0.f, 0.f};
 #pragma unroll
-    for (int kk = 0; kk < HD / 32; ++kk) {
-      kf[kk] = rd_row<HD>(Ki, kt * 16, kk, lane);
-      vf[kk] = rd_row<HD>(Vi, kt * 16, kk, lane);
-    }
-    v4f dv[HD / 16], dk[HD / 16];
+    for (int u = 0; u < 2; ++u) {
 #pragma unroll
-    for (int dt = 0; dt < HD / 16; ++dt) {
-      dv[dt] = v4f{0.f, 0.f, 0.f, 0.f};
-      dk[dt] = v4f{0.f, 0.f, 0.f, 0.f};
+      for (int kk = 0; kk < HD / 32; ++kk) {
+        qf[u][kk] = rd_row<HD>(Qi, (2 * qp + u) * 16, kk, lane);
+        df[u][kk] = rd_row<HD>(Oi, (2 * qp + u) * 16, kk, lane);
+      }
+      ls[u] = lse_s[(2 * qp + u) * 16 + i];
     }
-    const int key = kt * 16 + i;
-    const bool kvalid = key < N;
-    for (int qs = 0; qs < ns_valid; ++qs) {
-      v4f P[2], DS[2];
+    for (int kt = 0; kt < 2 * npair; ++kt) {
+      v8bf kr[HD / 32], vr[HD / 32];
+#pragma unroll
+      for (int kk = 0; kk < HD / 32; ++kk) {
+        kr[kk] = rd_row<HD>(Ki, kt * 16, kk, lane);
+        vr[kk] = rd_row<HD>(Vi, kt * 16, kk, lane);
+      }
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
-        const int qt = 2 * qs + u;
-        v4f s = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int kk = 0; kk < HD / 32; ++kk) {
-          s = mfma(rd_row<HD>(Qi, qt * 16, kk, lane), kf[kk], s);
-          dp = mfma(rd_row<HD>(Oi, qt * 16, kk, lane), vf[kk], dp);
-        }
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int q = qt * 16 + 4 * g + r;
-          const float p = kvalid ? exp2f(s[r] * c - lse_s[q]) : 0.f;
-          P[u][r] = p;
-          DS[u][r] = p * (dp[r] - dlt_s[q]);
-        }
-      }
-      const v8bf bP = pack8(P[0], P[1]);
-      const v8bf bD = pack8(DS[0], DS[1]);
-#pragma unroll
-      for (int dt = 0; dt < HD / 16; ++dt) {
-        dv[dt] = mfma(rd_tr<HD>(Oi, 2 * qs, 2 * qs + 1, dt * 16, lane), bP, dv[dt]);
-        dk[dt] = mfma(rd_tr<HD>(Qi, 2 * qs, 2 * qs + 1, dt * 16, lane), bD, dk[dt]);
-      }
-    }
-    if (kvalid) {
-#pragma unroll
-      for (int dt = 0; dt < HD / 16; ++dt) {
-        const int d = dt * 16 + 4 * g;
-        if (d < hd) {
-          store4(dq_base + (long)key * rs + D + d, dk[dt], scale);
-          store4(dq_base + (long)key * rs + 2 * D + d, dv[dt], 1.0f);
-        }
-      }
-    }
-  }
-
-  // ---- phase 2: dQ (query tiles owned by waves) ----
-  for (int qt = wave; qt < nt_valid; qt += NW) {
-    v8bf qf[HD / 32], df[HD / 32];
-#pragma unroll
-    for (int kk = 0; kk < HD / 32; ++kk) {
-      qf[kk] = rd_row<HD>(Qi, qt * 16, kk, lane);
-      df[kk] = rd_row<HD>(Oi, qt * 16, kk, lane);
-    }
-    const int q = qt * 16 + i;
-    const float ls = lse_s[q], dl = dlt_s[q];
-    v4f dq[HD / 16];
-#pragma unroll
-    for (int dt = 0; dt < HD / 16; ++dt) dq[dt] = v4f{0.f, 0.f, 0.f, 0.f};
-    for (int ks = 0; ks < ns_valid; ++ks) {
-      v4f DS[2];
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const int kt = 2 * ks + u;
         v4f st = {0.f, 0.f, 0.f, 0.f}, dpt = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int kk = 0; kk < HD / 32; ++kk) {
-          st = mfma(rd_row<HD>(Ki, kt * 16, kk, lane), qf[kk], st);
-          dpt = mfma(rd_row<HD>(Vi, kt * 16, kk, lane), df[kk], dpt);
+          st = mfma(kr[kk], qf[u][kk], st);
+          dpt = mfma(vr[kk], df[u][kk], dpt);
         }
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int key = kt * 16 + 4 * g + r;
-          const float p = key < N ? exp2f(st[r] * c - ls) : 0.f;
-          DS[u][r] = p * (dpt[r] - dl);
+          if (key < N) dsum[u] += exp2f(st[r] * c - ls[u]) * dpt[r];
         }
       }
-      const v8bf bD = pack8(DS[0], DS[1]);
-#pragma unroll
-      for (int dt = 0; dt < HD / 16; ++dt)
-        dq[dt] = mfma(rd_tr<HD>(Ki, 2 * ks, 2 * ks + 1, dt * 16, lane), bD, dq[dt]);
     }
-    if (q < N) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      float v = dsum[u];
+      v += __shfl_xor(v, 16, 64);
+      v += __shfl_xor(v, 32, 64);
+      const int q = (2 * qp + u) * 16 + i;
+      if (g == 0) dlt_s[q] = q < N ? v : 0.f;
+    }
+  }
+  __syncthreads();
+  bf16_t* dq_base = dqkv + (long)b * N * rs + (long)h * hd;
+  float bq[HD / 16][4], bk[HD / 16][4], bv[HD / 16][4];
+#pragma unroll
+  for (int dt = 0; dt < HD / 16; ++dt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bq[dt][r] = bk[dt][r] = bv[dt][r] = 0.f;
+
+  // ---- phase 1: dK, dV (key-tile pairs owned by waves) ----
+  for (int kp = wave; kp < npair; kp += NW) {
+    v8bf kf[2][HD / 32], vf[2][HD / 32];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int kk = 0; kk < HD / 32; ++kk) {
+        kf[t][kk] = rd_row<HD>(Ki, (2 * kp + t) * 16, kk, lane);
+        vf[t][kk] = rd_row<HD>(Vi, (2 * kp + t) * 16, kk, lane);
+      }
+    v4f dv[2][HD / 16], dk[2][HD / 16];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
 #pragma unroll
       for (int dt = 0; dt < HD / 16; ++dt) {
-        const int d = dt * 16 + 4 * g;
-        if (d < hd) store4(dq_base + (long)q * rs + d, dq[dt], scale);
+        dv[t][dt] = v4f{0.f, 0.f, 0.f, 0.f};
+        dk[t][dt] = v4f{0.f, 0.f, 0.f, 0.f};
       }
+    for (int qs = 0; qs < npair; ++qs) {
+      v4f P[2][2], DS[2][2];  // [key tile][query tile]
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int qt = 2 * qs + u;
+        v8bf qr[HD / 32], orow[HD / 32];
+#pragma unroll
+        for (int kk = 0; kk < HD / 32; ++kk) {
+          qr[kk] = rd_row<HD>(Qi, qt * 16, kk, lane);
+          orow[kk] = rd_row<HD>(Oi, qt * 16, kk, lane);
+        }
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          v4f sv = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int kk = 0; kk < HD / 32; ++kk) {
+            sv = mfma(qr[kk], kf[t][kk], sv);
+            dp = mfma(orow[kk], vf[t][kk], dp);
+          }
+          const bool kvalid = (2 * kp + t) * 16 + i < N;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int q = qt * 16 + 4 * g + r;
+            const float p = kvalid ? exp2f(sv[r] * c - lse_s[q]) : 0.f;
+            P[t][u][r] = p;
+            DS[t][u][r] = p * (dp[r] - dlt_s[q]);
+          }
+        }
+      }
+      const v8bf bP0 = pack8(P[0][0], P[0][1]), bP1 = pack8(P[1][0], P[1][1]);
+      const v8bf bD0 = pack8(DS[0][0], DS[0][1]), bD1 = pack8(DS[1][0], DS[1][1]);
+#pragma unroll
+      for (int dt = 0; dt < HD / 16; ++dt) {
+        const v8bf ot = rd_tr<HD>(Oi, 2 * qs, 2 * qs + 1, dt * 16, lane);
+        const v8bf qt = rd_tr<HD>(Qi, 2 * qs, 2 * qs + 1, dt * 16, lane);
+        dv[0][dt] = mfma(ot, bP0, dv[0][dt]);
+        dv[1][dt] = mfma(ot, bP1, dv[1][dt]);
+        dk[0][dt] = mfma(qt, bD0, dk[0][dt]);
+        dk[1][dt] = mfma(qt, bD1, dk[1][dt]);
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int key = (2 * kp + t) * 16 + i;
+      if (key < N) {
+#pragma unroll
+        for (int dt = 0; dt < HD / 16; ++dt) {
+          const int d = dt * 16 + 4 * g;
+          if (d < hd) {
+            store4(dq_base + (long)key * rs + D + d, dk[t][dt], scale);
+            store4(dq_base + (long)key * rs + 2 * D + d, dv[t][dt], 1.0f);
+          }
+        }
+      }
+      if (bias_partial) {
+#pragma unroll
+        for (int dt = 0; dt < HD / 16; ++dt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {  // invalid keys hold exact zeros (P = 0)
+            bk[dt][r] += sum16(dk[t][dt][r]);
+            bv[dt][r] += sum16(dv[t][dt][r]);
+          }
+      }
+    }
+  }
+
+  // ---- phase 2: dQ (query-tile pairs owned by waves) ----
+  for (int qp = wave; qp < npair; qp += NW) {
+    v8bf qf[2][HD / 32], df[2][HD / 32];
+    float ls[2], dl[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+#pragma unroll
+      for (int kk = 0; kk < HD / 32; ++kk) {
+        qf[u][kk] = rd_row<HD>(Qi, (2 * qp + u) * 16, kk, lane);
+        df[u][kk] = rd_row<HD>(Oi, (2 * qp + u) * 16, kk, lane);
+      }
+      ls[u] = lse_s[(2 * qp + u) * 16 + i];
+      dl[u] = dlt_s[(2 * qp + u) * 16 + i];
+    }
+    v4f dq[2][HD / 16];
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int dt = 0; dt < HD / 16; ++dt) dq[u][dt] = v4f{0.f, 0.f, 0.f, 0.f};
+    for (int ks = 0; ks < npair; ++ks) {
+      v4f DS[2][2];  // [query tile][key tile]
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const int kt = 2 * ks + t;
+        v8bf kr[HD / 32], vr[HD / 32];
+#pragma unroll
+        for (int kk = 0; kk < HD / 32; ++kk) {
+          kr[kk] = rd_row<HD>(Ki, kt * 16, kk, lane);
+          vr[kk] = rd_row<HD>(Vi, kt * 16, kk, lane);
+        }
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          v4f st = {0.f, 0.f, 0.f, 0.f}, dpt = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int kk = 0; kk < HD / 32; ++kk) {
+            st = mfma(kr[kk], qf[u][kk], st);
+            dpt = mfma(vr[kk], df[u][kk], dpt);
+          }
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int key = kt * 16 + 4 * g + r;
+            const float p = key < N ? exp2f(st[r] * c - ls[u]) : 0.f;
+            DS[u][t][r] = p * (dpt[r] - dl[u]);
+          }
+        }
+      }
+      const v8bf bD0 = pack8(DS[0][0], DS[0][1]), bD1 = pack8(DS[1][0], DS[1][1]);
+#pragma unroll
+      for (int dt = 0; dt < HD / 16; ++dt) {
+        const v8bf kt_ = rd_tr<HD>(Ki, 2 * ks, 2 * ks + 1, dt * 16, lane);
+        dq[0][dt] = mfma(kt_, bD0, dq[0][dt]);
+        dq[1][dt] = mfma(kt_, bD1, dq[1][dt]);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int q = (2 * qp + u) * 16 + i;
+      if (q < N) {
+#pragma unroll
+        for (int dt = 0; dt < HD / 16; ++dt) {
+          const int d = dt * 16 + 4 * g;
+          if (d < hd) store4(dq_base + (long)q * rs + d, dq[u][dt], scale);
+        }
+      }
+      if (bias_partial) {
+#pragma unroll
+        for (int dt = 0; dt < HD / 16; ++dt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) bq[dt][r] += sum16(dq[u][dt][r]);  // padded queries: dS = 0
+      }
+    }
+  }
+
+  if (bias_partial) {
+    // lanes i == 0 hold the wave's column sums for d = 16dt + 4g + r; fixed-order sum over waves
+    if (i == 0) {
+#pragma unroll
+      for (int dt = 0; dt < HD / 16; ++dt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int d = dt * 16 + 4 * g + r;
+          bsum[(wave * 3 + 0) * HD + d] = bq[dt][r] * scale;
+          bsum[(wave * 3 + 1) * HD + d] = bk[dt][r] * scale;
+          bsum[(wave * 3 + 2) * HD + d] = bv[dt][r];
+        }
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < 3 * HD; e += blockDim.x) {
+      const int z = e / HD, d = e % HD;
+      if (d >= hd) continue;
+      float acc = 0.f;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) acc += bsum[(w * 3 + z) * HD + d];
+      bias_partial[(long)b * 3 * D + z * D + h * hd + d] = acc;
     }
   }
 }
@@ -322,13 +459,13 @@ hipError_t launch_fwd(const bf16_t* qkv, bf16_t* o, float* lse, int B, int N, in
 }
 
 template <int HD, int NKT>
-hipError_t launch_bwd(const bf16_t* qkv, const bf16_t* o, const bf16_t* dout, const float* lse, bf16_t* dqkv, int B,
-                      int N, int H, int hd, float scale, hipStream_t s) {
+hipError_t launch_bwd(const bf16_t* qkv, const bf16_t* o, const bf16_t* dout, const float* lse, bf16_t* dqkv,
+                      float* bias_partial, int B, int N, int H, int hd, float scale, hipStream_t s) {
   constexpr int NW = 8;
-  const size_t lds = (size_t)4 * NKT * 16 * HD * 2 + 2 * NKT * 16 * 4;
+  const size_t lds = (size_t)4 * NKT * 16 * HD * 2 + 2 * NKT * 16 * 4 + (size_t)NW * 3 * HD * 4;
   auto kern = attn_bwd_kernel<HD, NKT, NW>;
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL(kern, dim3(B * H), dim3(NW * 64), lds, s, qkv, o, dout, lse, dqkv, N, H, hd, scale);
+  hipLaunchKernelGGL(kern, dim3(B * H), dim3(NW * 64), lds, s, qkv, o, dout, lse, dqkv, bias_partial, N, H, hd, scale);
   return hipGetLastError();
 }
 
@@ -347,10 +484,10 @@ hipError_t dispatch_fwd(int nkt, const bf16_t* qkv, bf16_t* o, float* lse, int B
 }
 template <int HD>
 hipError_t dispatch_bwd(int nkt, const bf16_t* qkv, const bf16_t* o, const bf16_t* dout, const float* lse,
-                        bf16_t* dqkv, int B, int N, int H, int hd, float scale, hipStream_t s) {
+                        bf16_t* dqkv, float* bias_partial, int B, int N, int H, int hd, float scale, hipStream_t s) {
   switch (nkt) {
 #define C(n) \
-  case n: return launch_bwd<HD, n>(qkv, o, dout, lse, dqkv, B, N, H, hd, scale, s);
+  case n: return launch_bwd<HD, n>(qkv, o, dout, lse, dqkv, bias_partial, B, N, H, hd, scale, s);
     VIT_NKT_CASES(C)
 #undef C
   }
@@ -381,15 +518,18 @@ extern "C" int vit_attention_fwd(const void* qkv, void* o, float* lse, int64_t B
 }
 
 extern "C" int vit_attention_bwd(const void* qkv, const void* o, const void* dout, const float* lse, void* dqkv,
-                                 int64_t B, int64_t N, int64_t H, int64_t hd, float scale, vit_stream_t stream) {
+                                 float* bias_partial, int64_t B, int64_t N, int64_t H, int64_t hd, float scale,
+                                 vit_stream_t stream) {
   int st = check_shape(B, N, H, hd);
   if (st) return st;
   VIT_CHECK_ARG(qkv && o && dout && lse && dqkv, "vit_attention_bwd: null pointer");
   const int nkt = (int)((N + 31) / 32) * 2;
   hipError_t e = hd == 64
                      ? dispatch_bwd<64>(nkt, (const bf16_t*)qkv, (const bf16_t*)o, (const bf16_t*)dout, lse,
-                                        (bf16_t*)dqkv, (int)B, (int)N, (int)H, (int)hd, scale, (hipStream_t)stream)
+                                        (bf16_t*)dqkv, bias_partial, (int)B, (int)N, (int)H, (int)hd, scale,
+                                        (hipStream_t)stream)
                      : dispatch_bwd<32>(nkt, (const bf16_t*)qkv, (const bf16_t*)o, (const bf16_t*)dout, lse,
-                                        (bf16_t*)dqkv, (int)B, (int)N, (int)H, (int)hd, scale, (hipStream_t)stream);
+                                        (bf16_t*)dqkv, bias_partial, (int)B, (int)N, (int)H, (int)hd, scale,
+                                        (hipStream_t)stream);
   return vit::check_hip(e, "vit_attention_bwd launch");
 }

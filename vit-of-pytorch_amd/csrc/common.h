@@ -37,11 +37,28 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
-// Exact-erf GELU (nn.GELU() default, reference src/model.py:33) and its derivative.
-__device__ __forceinline__ float gelu_f(float u) { return 0.5f * u * (1.0f + erff(u * 0.70710678118654752f)); }
+// Erf GELU (nn.GELU() default approximate='none', reference src/model.py:33) and its derivative.
+// erf(x) = 1 - poly(t) exp(-x^2), t = 1/(1 + p|x|) (Abramowitz & Stegun 7.1.26, |error| <= 1.5e-7,
+// i.e. fp32-erff class; GELU abs error <= 2.2e-7): one v_rcp and one v_exp instead of the ~40-op
+// libm erff, and the derivative reuses the same exp(-u^2/2) for the normal pdf.
+__device__ __forceinline__ float phi_and_pdf(float u, float* pdf) {
+  const float e = __expf(-0.5f * u * u);  // exp(-x^2), x = u/sqrt(2)
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f * 0.70710678118654752f, fabsf(u), 1.0f));
+  float p = fmaf(1.061405429f, t, -1.453152027f);
+  p = fmaf(p, t, 1.421413741f);
+  p = fmaf(p, t, -0.284496736f);
+  p = fmaf(p, t, 0.254829592f);
+  const float erfa = 1.0f - p * t * e;  // erf(|x|)
+  *pdf = 0.39894228040143268f * e;
+  return 0.5f + 0.5f * copysignf(erfa, u);
+}
+__device__ __forceinline__ float gelu_f(float u) {
+  float pdf;
+  return u * phi_and_pdf(u, &pdf);
+}
 __device__ __forceinline__ float gelu_grad_f(float u) {
-  const float cdf = 0.5f * (1.0f + erff(u * 0.70710678118654752f));
-  const float pdf = 0.39894228040143268f * __expf(-0.5f * u * u);
+  float pdf;
+  const float cdf = phi_and_pdf(u, &pdf);
   return cdf + u * pdf;
 }
 

@@ -42,6 +42,7 @@ struct GemmDev {
   int split_k;
   int tokens;
   int vec;  // every pointer / leading dim allows 8-column (16/32-B) vector access
+  float* col_partial;  // optional per-M-tile column sums of the output
 };
 
 // K-contiguous image [rows][BK]: XOR of the 16-B chunk index, conflict-free for the 16x16x32
@@ -346,6 +347,8 @@ __global__ void __launch_bounds__(WM* WN * 64, (gemm_min_waves<BM, BN, BK, STAGE
   __syncthreads();
   float* cs = reinterpret_cast<float*>(smem);
   constexpr int CPR = BN / 8;
+  static_assert(NT % CPR == 0, "a thread keeps one 8-column chunk across the epilogue loop");
+  float csum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int pass = 0; pass < NPASS; ++pass) {
     if (NPASS == 1 || wm / (WM / NPASS) == pass) {
@@ -366,13 +369,33 @@ __global__ void __launch_bounds__(WM* WN * 64, (gemm_min_waves<BM, BN, BK, STAGE
       float v[8];
       ld8f(cs + row * LDC + ch * 8, v);
       if (p.vec && n + 8 <= p.N) {
-        epi_store8<EPI>(p, z, split_idx, m, n, v);
+        epi_store8<EPI>(p, z, split_idx, m, n, v);  // v becomes the stored values
+        if (p.col_partial) {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) csum[k] += v[k];
+        }
       } else {
 #pragma unroll
         for (int k = 0; k < 8; ++k) epi_store<EPI>(p, z, split_idx, m, n + k, v[k]);
       }
     }
     if (NPASS > 1) __syncthreads();
+  }
+  if (p.col_partial) {
+    // per-tile column sums of the written values (e.g. the bias gradient of the next layer down)
+    __syncthreads();
+    float* red = cs;
+    constexpr int RL = NT / CPR;  // threads sharing one 8-column chunk
+    const int ch = threadIdx.x % CPR;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) red[(threadIdx.x / CPR) * BN + ch * 8 + k] = csum[k];
+    __syncthreads();
+    for (int c = threadIdx.x; c < BN; c += NT) {
+      float sum = 0.f;
+#pragma unroll 8
+      for (int r = 0; r < RL; ++r) sum += red[r * BN + c];
+      if (n0 + c < p.N) p.col_partial[(long)tm * p.N + n0 + c] = sum;
+    }
   }
 }
 
@@ -419,6 +442,14 @@ int pick_tile(const vit_gemm_args* a) {
 }
 
 }  // namespace
+
+extern "C" int64_t vit_gemm_tile_rows(const vit_gemm_args* a) {
+  if (!a) return 0;
+  switch (pick_tile(a)) {
+    case 1: case 2: case 3: return 256;
+    default: return 128;
+  }
+}
 
 extern "C" int vit_gemm_bf16(const vit_gemm_args* a, vit_stream_t stream) {
   VIT_CHECK_ARG(a != nullptr, "vit_gemm_bf16: null args");
@@ -472,6 +503,13 @@ extern "C" int vit_gemm_bf16(const vit_gemm_args* a, vit_stream_t stream) {
     if (a->aux2) v = v && al(a->aux2);
     if (a->epilogue == VIT_EPI_SPLITK) v = al(a->C) && a->N % 8 == 0;
     d.vec = v ? 1 : 0;
+  }
+  d.col_partial = a->col_partial;
+  if (a->col_partial) {
+    VIT_CHECK_ARG(a->batch == 1 && a->split_k == 1 && d.vec && a->N % 8 == 0 &&
+                      (a->epilogue == VIT_EPI_F32 || a->epilogue == VIT_EPI_BF16 || a->epilogue == VIT_EPI_GELU_BWD ||
+                       a->epilogue == VIT_EPI_BIAS_BF16 || a->epilogue == VIT_EPI_BIAS_RESID_F32),
+                  "vit_gemm_bf16: col_partial needs batch 1, split_k 1, aligned N%%8==0 operands and a plain epilogue");
   }
   hipStream_t s = (hipStream_t)stream;
   const int batch = (int)a->batch, split = (int)a->split_k;

@@ -74,14 +74,15 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const void* __restrict__ dy
                                                      const float* __restrict__ dres, long lddres, float* __restrict__ dx,
                                                      long lddx, bf16_t* __restrict__ dxb, long lddxb,
                                                      float* __restrict__ partial, int rows, int D) {
-  __shared__ float red[4][2][NV * 256];
+  __shared__ float red[4][NV * 256];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  float4 pg[NV], pb[NV];
+  float4 pg[NV], pb[NV], ps[NV];
   float4 gm[NV];
 #pragma unroll
   for (int k = 0; k < NV; ++k) {
     pg[k] = make_float4(0.f, 0.f, 0.f, 0.f);
     pb[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+    ps[k] = make_float4(0.f, 0.f, 0.f, 0.f);
     const int c = (k * 64 + lane) * 4;
     gm[k] = c < D ? *reinterpret_cast<const float4*>(gamma + c) : make_float4(0.f, 0.f, 0.f, 0.f);
   }
@@ -127,6 +128,7 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const void* __restrict__ dy
           o.x += r4.x; o.y += r4.y; o.z += r4.z; o.w += r4.w;
         }
         *reinterpret_cast<float4*>(dx + (long)row * lddx + c) = o;
+        ps[k].x += o.x; ps[k].y += o.y; ps[k].z += o.z; ps[k].w += o.w;
         if (dxb) {
           uint2 u;
           u.x = pack2bf(o.x, o.y);
@@ -136,23 +138,19 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const void* __restrict__ dy
       }
     }
   }
-  // block partials of dgamma (sum dy*xhat) and dbeta (sum dy)
+  // block partials [dgamma | dbeta | dsum]: sum dy*xhat, sum dy, sum of the written dx (the
+  // bias gradient of the linear layer that produced this residual stream)
 #pragma unroll
-  for (int k = 0; k < NV; ++k) {
-    const int c = (k * 64 + lane) * 4;
-    *reinterpret_cast<float4*>(&red[wave][0][c]) = pg[k];
-    *reinterpret_cast<float4*>(&red[wave][1][c]) = pb[k];
-  }
-  __syncthreads();
-  for (int c = threadIdx.x; c < D; c += 256) {
-    float a = 0.f, b = 0.f;
+  for (int q = 0; q < 3; ++q) {
 #pragma unroll
-    for (int w = 0; w < 4; ++w) {
-      a += red[w][0][c];
-      b += red[w][1][c];
+    for (int k = 0; k < NV; ++k) {
+      const int c = (k * 64 + lane) * 4;
+      *reinterpret_cast<float4*>(&red[wave][c]) = q == 0 ? pg[k] : (q == 1 ? pb[k] : ps[k]);
     }
-    partial[(long)blockIdx.x * 2 * D + c] = a;
-    partial[(long)blockIdx.x * 2 * D + D + c] = b;
+    __syncthreads();
+    for (int c = threadIdx.x; c < D; c += 256)
+      partial[(long)blockIdx.x * 3 * D + q * D + c] = red[0][c] + red[1][c] + red[2][c] + red[3][c];
+    __syncthreads();
   }
 }
 
@@ -184,7 +182,7 @@ static int64_t ln_bwd_blocks(int64_t rows) {
   return b < 1 ? 1 : b;
 }
 
-// rows of 2*D floats the `partial` workspace must hold (block partials + their column reduction)
+// rows of 3*D floats the `partial` workspace must hold (block partials + their column reduction)
 extern "C" int64_t vit_layernorm_bwd_partial_rows(int64_t rows) {
   const int64_t nb = ln_bwd_blocks(rows);
   return nb + vit_colsum_partial_rows(nb);
@@ -193,8 +191,8 @@ extern "C" int64_t vit_layernorm_bwd_partial_rows(int64_t rows) {
 extern "C" int vit_layernorm_bwd(const void* dy, int64_t lddy, int32_t dy_f32, const float* x, int64_t ldx,
                                  const float* mean, const float* rstd, const float* gamma, const float* dres,
                                  int64_t lddres, float* dx, int64_t lddx, void* dx_bf16, int64_t lddxb, float* partial,
-                                 float* dgamma_dbeta, int32_t accumulate_params, int64_t rows, int64_t D,
-                                 vit_stream_t stream) {
+                                 float* dgamma_dbeta, float* dx_colsum, int32_t accumulate_params, int64_t rows,
+                                 int64_t D, vit_stream_t stream) {
   VIT_CHECK_ARG(dy && x && mean && rstd && gamma && dx && partial, "vit_layernorm_bwd: null pointer");
   VIT_CHECK_ARG(D > 0 && D % 4 == 0 && D <= 2048, "vit_layernorm_bwd: D=%lld unsupported", (long long)D);
   if (rows <= 0) return VIT_OK;
@@ -211,7 +209,10 @@ extern "C" int vit_layernorm_bwd(const void* dy, int64_t lddy, int32_t dy_f32, c
 #undef C
   }
   int st = vit::check_hip(hipGetLastError(), "vit_layernorm_bwd");
-  if (st || !dgamma_dbeta) return st;
-  // reduce the block partials into [dgamma | dbeta]
-  return vit_colsum(partial, 0, nblk, 2 * D, 2 * D, partial + nblk * 2 * D, dgamma_dbeta, accumulate_params, stream);
+  if (st) return st;
+  float* ws = partial + nblk * 3 * D;
+  if (dgamma_dbeta) st = vit_colsum(partial, 0, nblk, 2 * D, 3 * D, ws, dgamma_dbeta, accumulate_params, stream);
+  if (st) return st;
+  if (dx_colsum) st = vit_colsum(partial + 2 * D, 0, nblk, D, 3 * D, ws, dx_colsum, accumulate_params, stream);
+  return st;
 }

@@ -31,7 +31,7 @@ class GemmArgs(ctypes.Structure):
         ("C2", c_vp), ("ldc2", c_i64),
         ("bias", c_vp), ("bias_batch_stride", c_i64),
         ("aux", c_vp), ("ldaux", c_i64), ("aux2", c_vp),
-        ("batch", c_i64), ("split_k", c_i64), ("tokens", c_i64),
+        ("batch", c_i64), ("split_k", c_i64), ("tokens", c_i64), ("col_partial", c_vp),
         ("epilogue", c_i32), ("tile", c_i32),
     ]
 
@@ -41,13 +41,14 @@ _SIGS = {
     "vit_last_error": (ctypes.c_char_p, []),
     "vit_abi_version": (c_i32, []),
     "vit_gemm_bf16": (c_i32, [ctypes.POINTER(GemmArgs), c_vp]),
+    "vit_gemm_tile_rows": (c_i64, [ctypes.POINTER(GemmArgs)]),
     "vit_splitk_reduce": (c_i32, [c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_i64, c_i64, c_i32, c_vp]),
     "vit_layernorm_fwd": (c_i32, [c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_i32, c_vp, c_vp, c_i64, c_i64, c_f32, c_vp]),
     "vit_layernorm_bwd_partial_rows": (c_i64, [c_i64]),
     "vit_layernorm_bwd": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_i64,
-                                  c_vp, c_i64, c_vp, c_vp, c_i32, c_i64, c_i64, c_vp]),
+                                  c_vp, c_i64, c_vp, c_vp, c_vp, c_i32, c_i64, c_i64, c_vp]),
     "vit_attention_fwd": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_f32, c_vp]),
-    "vit_attention_bwd": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_f32, c_vp]),
+    "vit_attention_bwd": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_f32, c_vp]),
     "vit_im2col": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp]),
     "vit_embed_grad": (c_i32, [c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp]),
     "vit_colsum_partial_rows": (c_i64, [c_i64]),

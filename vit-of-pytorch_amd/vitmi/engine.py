@@ -158,8 +158,10 @@ class _Acts:
         self.dlncls = z(b, D, dt=f)
         self.dlogits = z(b, cfg.num_classes, dt=f)
         self.row_stats = z(b, 3, dt=f)
-        self.lnpart = z(ops.layernorm_bwd_partial_rows(T), 2 * D, dt=f)
+        self.lnpart = z(ops.layernorm_bwd_partial_rows(T), 3 * D, dt=f)
         self.colpart = z(ops.colsum_partial_rows(T), max(3 * D, M, cfg.num_classes), dt=f)
+        self.gelu_part = z(-(-T // 128), M, dt=f)   # per-M-tile column sums of dU (fc1 bias grad)
+        self.qkv_bpart = z(b, 3 * D, dt=f)          # per-image column sums of dq|dk|dv (q/k/v bias grads)
 
 
 class ViTEngine:
@@ -263,9 +265,6 @@ class ViTEngine:
                  epilogue=EPI_SPLITK, batch=batch, b_bs=b_bs, split_k=s)
         ops.splitk_reduce(ws, batch, s, M, N, out, ldo, out_bs)
 
-    def _bias_grad(self, a, inp, cols, ld, out):
-        ops.colsum(inp, a.T, cols, ld, a.colpart, out)
-
     # ---- forward -------------------------------------------------------------------------------
     def forward(self, x: torch.Tensor):
         """x: [b, 3, img, img] fp32 on the device. Returns logits [b, C] (fp32, engine-owned)."""
@@ -354,42 +353,47 @@ class ViTEngine:
         # final LN backward on cls rows -> residual grad (zero elsewhere)
         a.dh.zero_()
         a.dhb.zero_()
+        # (its dx column sum is the last layer's fc2 bias gradient: only the cls rows are non-zero)
         ops.layernorm_bwd(a.dlncls, D, a.h[L], N * D, a.muf, a.rsf, f[self.off("transformer.norm.weight"):], a.dh,
                           N * D, a.lnpart, b, D, dx_bf16=a.dhb, lddxb=N * D,
-                          dgamma_dbeta=gv("transformer.norm.weight"))
+                          dgamma_dbeta=gv("transformer.norm.weight"),
+                          dx_colsum=gv(self.lname(L - 1, "mlp.fc2.bias")))
         if hook:
             hook(g, *self.layout.buckets[0])
         scale = 1.0 / math.sqrt(hd)
         for i in reversed(range(L)):
             ln = lambda s: self.off(self.lname(i, s))
             # ---- MLP: h_{i+1} = hm + fc2(gelu(fc1(ln2(hm)))) ----
+            # (fc2 bias grad = column sums of dh, already produced by the LayerNorm backward above)
             self._wgrad(a.dhb, D, a.g[i], M, D, M, a.Tp, gv(self.lname(i, "mlp.fc2.weight")), M)
-            self._bias_grad(a, a.dh, D, D, gv(self.lname(i, "mlp.fc2.bias")))
-            ops.gemm(a.dhb, mv[ln("mlp.fc2.weight"):], a.dg, T, M, D, a_layout=K_CONTIG, b_layout=MN_CONTIG, lda=D,
-                     ldb=M, ldc=M, epilogue=EPI_GELU_BWD, aux=a.u[i], ldaux=M)
+            kw = dict(a_layout=K_CONTIG, b_layout=MN_CONTIG, lda=D, ldb=M, ldc=M, epilogue=EPI_GELU_BWD, aux=a.u[i],
+                      ldaux=M, col_partial=a.gelu_part)
+            ops.gemm(a.dhb, mv[ln("mlp.fc2.weight"):], a.dg, T, M, D, **kw)
+            tiles_m = -(-T // ops.gemm_tile_rows(a.dhb, mv, a.dg, T, M, D, **kw))
+            ops.colsum(a.gelu_part, tiles_m, M, M, a.colpart, gv(self.lname(i, "mlp.fc1.bias")))
             self._wgrad(a.dg, M, a.ln2[i], D, M, D, a.Tp, gv(self.lname(i, "mlp.fc1.weight")), D)
-            self._bias_grad(a, a.dg, M, M, gv(self.lname(i, "mlp.fc1.bias")))
             ops.gemm(a.dg, mv[ln("mlp.fc1.weight"):], a.dyln, T, D, M, a_layout=K_CONTIG, b_layout=MN_CONTIG, lda=M,
                      ldb=D, ldc=D, epilogue=EPI_BF16)
             ops.layernorm_bwd(a.dyln, D, a.hm[i], D, a.mu2[i], a.rs2[i], f[ln("norm2.weight"):], a.dh, D, a.lnpart, T,
                               D, dres=a.dh, lddres=D, dx_bf16=a.dhb, lddxb=D,
-                              dgamma_dbeta=gv(self.lname(i, "norm2.weight")))
+                              dgamma_dbeta=gv(self.lname(i, "norm2.weight")),
+                              dx_colsum=gv(self.lname(i, "attn.out.bias")))
             # ---- attention: hm = h + out(attn(ln1(h))) ----
             self._wgrad(a.o[i], D, a.dhb, D, D, D, a.Tp, gv(self.lname(i, "attn.out.weight")), D)
-            self._bias_grad(a, a.dh, D, D, gv(self.lname(i, "attn.out.bias")))
             ops.gemm(a.dhb, mv[ln("attn.out.weight"):], a.dO, T, D, D, a_layout=K_CONTIG, b_layout=K_CONTIG, lda=D,
                      ldb=D, ldc=D, epilogue=EPI_BF16)
-            ops.attention_bwd(a.qkv[i], a.o[i], a.dO, a.lse[i], a.dqkv, b, N, H, hd, scale)
+            ops.attention_bwd(a.qkv[i], a.o[i], a.dO, a.lse[i], a.dqkv, b, N, H, hd, scale, bias_partial=a.qkv_bpart)
             qo = ln("attn.query.weight")
             zs = ln("attn.key.weight") - qo
-            self._wgrad(a.ln1[i], D, a.dqkv, 3 * D, D, D, a.Tp, g[qo:], D, batch=3, b_bs=D, out_bs=zs)
             for z in range(3):
-                self._bias_grad(a, a.dqkv[:, z * D:], D, 3 * D, g[ln("attn.query.bias") + z * zs:])
+                ops.colsum(a.qkv_bpart[:, z * D:], b, D, 3 * D, a.colpart, g[ln("attn.query.bias") + z * zs:])
+            self._wgrad(a.ln1[i], D, a.dqkv, 3 * D, D, D, a.Tp, g[qo:], D, batch=3, b_bs=D, out_bs=zs)
             ops.gemm(a.dqkv, self.wqkv[i], a.dyln, T, D, 3 * D, a_layout=K_CONTIG, b_layout=K_CONTIG, lda=3 * D,
                      ldb=3 * D, ldc=D, epilogue=EPI_BF16)
             ops.layernorm_bwd(a.dyln, D, a.h[i], D, a.mu1[i], a.rs1[i], f[ln("norm1.weight"):], a.dh, D, a.lnpart, T,
                               D, dres=a.dh, lddres=D, dx_bf16=a.dhb, lddxb=D,
-                              dgamma_dbeta=gv(self.lname(i, "norm1.weight")))
+                              dgamma_dbeta=gv(self.lname(i, "norm1.weight")),
+                              dx_colsum=gv(self.lname(i - 1, "mlp.fc2.bias")) if i > 0 else None)
             if hook:
                 hook(g, *self.layout.buckets[L - i])
         # ---- embedding: conv weight grad (wgrad over patches), bias / pos / cls ----

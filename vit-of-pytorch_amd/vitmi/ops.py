@@ -39,11 +39,9 @@ def _chk(t, dtype, name):
 
 
 # ---------------------------------------------------------------------------------------------
-def gemm(A, B, C, M, N, K, *, a_layout, b_layout, lda, ldb, ldc, epilogue, bias=None, aux=None, ldaux=0,
-         C2=None, ldc2=0, aux2=None, batch=1, a_bs=0, b_bs=0, c_bs=0, bias_bs=0, split_k=1, tokens=0, tile=0):
-    """bf16 MFMA GEMM, C[m,n] = sum_k A(m,k) B(k,n) + fused epilogue (see vit_gemm_args)."""
-    _chk(A, BF16, "A")
-    _chk(B, BF16, "B")
+def _gemm_args(A, B, C, M, N, K, *, a_layout, b_layout, lda, ldb, ldc, epilogue, bias=None, aux=None, ldaux=0,
+               C2=None, ldc2=0, aux2=None, batch=1, a_bs=0, b_bs=0, c_bs=0, bias_bs=0, split_k=1, tokens=0, tile=0,
+               col_partial=None):
     a = GemmArgs()
     a.M, a.N, a.K = M, N, K
     a.A, a.lda, a.a_batch_stride, a.a_layout = A.data_ptr(), lda, a_bs, a_layout
@@ -54,8 +52,21 @@ def gemm(A, B, C, M, N, K, *, a_layout, b_layout, lda, ldb, ldc, epilogue, bias=
     a.aux, a.ldaux = (aux.data_ptr() if aux is not None else None), ldaux
     a.aux2 = aux2.data_ptr() if aux2 is not None else None
     a.batch, a.split_k, a.tokens = batch, split_k, tokens
+    a.col_partial = col_partial.data_ptr() if col_partial is not None else None
     a.epilogue, a.tile = epilogue, tile
+    return a
+
+
+def gemm(A, B, C, M, N, K, **kw):
+    """bf16 MFMA GEMM, C[m,n] = sum_k A(m,k) B(k,n) + fused epilogue (see vit_gemm_args)."""
+    _chk(A, BF16, "A")
+    _chk(B, BF16, "B")
+    a = _gemm_args(A, B, C, M, N, K, **kw)
     check(lib().vit_gemm_bf16(ctypes.byref(a), _stream()), "vit_gemm_bf16")
+
+
+def gemm_tile_rows(A, B, C, M, N, K, **kw):
+    return int(lib().vit_gemm_tile_rows(ctypes.byref(_gemm_args(A, B, C, M, N, K, **kw))))
 
 
 def splitk_reduce(ws, batch, split, M, N, out, ldo, out_bs=0, accumulate=False):
@@ -76,10 +87,10 @@ def layernorm_bwd_partial_rows(rows):
 
 
 def layernorm_bwd(dy, lddy, x, ldx, mean, rstd, gamma, dx, lddx, partial, rows, D, *, dres=None, lddres=0,
-                  dx_bf16=None, lddxb=0, dgamma_dbeta=None, accumulate=False):
+                  dx_bf16=None, lddxb=0, dgamma_dbeta=None, dx_colsum=None, accumulate=False):
     check(lib().vit_layernorm_bwd(_p(dy), lddy, int(dy.dtype == F32), _p(x), ldx, _p(mean), _p(rstd), _p(gamma),
                                   _p(dres), lddres, _p(dx), lddx, _p(dx_bf16), lddxb, _p(partial), _p(dgamma_dbeta),
-                                  int(accumulate), rows, D, _stream()), "vit_layernorm_bwd")
+                                  _p(dx_colsum), int(accumulate), rows, D, _stream()), "vit_layernorm_bwd")
 
 
 def attention_fwd(qkv, o, lse, B, N, H, hd, scale):
@@ -89,9 +100,9 @@ def attention_fwd(qkv, o, lse, B, N, H, hd, scale):
     check(lib().vit_attention_fwd(_p(qkv), _p(o), _p(lse), B, N, H, hd, scale, _stream()), "vit_attention_fwd")
 
 
-def attention_bwd(qkv, o, dout, lse, dqkv, B, N, H, hd, scale):
-    check(lib().vit_attention_bwd(_p(qkv), _p(o), _p(dout), _p(lse), _p(dqkv), B, N, H, hd, scale, _stream()),
-          "vit_attention_bwd")
+def attention_bwd(qkv, o, dout, lse, dqkv, B, N, H, hd, scale, bias_partial=None):
+    check(lib().vit_attention_bwd(_p(qkv), _p(o), _p(dout), _p(lse), _p(dqkv), _p(bias_partial), B, N, H, hd, scale,
+                                  _stream()), "vit_attention_bwd")
 
 
 def im2col(x, out, B, img, P, Kpad):
