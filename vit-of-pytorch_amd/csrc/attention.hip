@@ -15,6 +15,7 @@
 // LDS images: [rows][HD] bf16 with a 16-B-chunk XOR swizzle that is conflict-free for both the
 // row read (ds_read_b128) and the transposed read (ds_read_b64_tr_b16) at HD = 64.
 #include "common.h"
+#include <stdlib.h>
 
 namespace {
 
@@ -171,25 +172,41 @@ __device__ __forceinline__ float sum16(float v) {
   return v;
 }
 
+// Global row fragment (16 rows x 32 k, MFMA operand layout) straight to registers: lane (g, i) gets
+// row r0 + i, columns kk*32 + 8g .. +7; rows >= N and columns >= hd read as zero.
+template <int HD>
+__device__ __forceinline__ v8bf gl_row(const bf16_t* __restrict__ src, long row_stride, int r0, int kk, int N, int hd,
+                                       int lane) {
+  const int row = r0 + (lane & 15), col = kk * 32 + 8 * (lane >> 4);
+  v8s v = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (row < N && col < hd) v = *reinterpret_cast<const v8s*>(src + (long)row * row_stride + col);
+  return __builtin_bit_cast(v8bf, v);
+}
+
 // ------------------------------------------------------------------------------------------------
-// Backward. Phase 0 (query pairs): delta = rowsum(P * dP). Phase 1: each wave owns two 16-key tiles
-// (dK, dV); phase 2: two 16-query tiles (dQ). Q / dO / K / V fragments read from LDS are shared by
-// the two tiles. Optionally writes per-image column sums of
-// dQ, dK, dV (the q/k/v bias gradient partials) to bias_partial[b][3*D].
+// Backward, two LDS images at a time (56 KB at N = 197, hd = 64: two workgroups per CU, so one
+// workgroup's image loads overlap the other's MFMA work).
+//   stage 1 (K, V images): each wave owns pairs of 16-query tiles, Q / dO rows in registers;
+//     pass A: delta_q = sum_j P_qj dP_qj from the recomputed P and dP themselves (FlashAttention-2's
+//     rowsum(dO * O) differs from it by bf16 O's rounding, and dS = P (dP - delta) is a small
+//     difference: that turned into 10-25% errors on the q/k weight gradients under near-uniform
+//     attention); pass B: dS and dQ = dS K.
+//   stage 2 (Q, dO images): each wave owns pairs of 16-key tiles, K / V rows in registers; dV =
+//     P^T dO, dK = dS^T Q, with delta from stage 1.
+// Deterministic (no atomics). Optionally writes per-image column sums of dQ | dK | dV (q/k/v bias
+// gradient partials) to bias_partial[b][3*D].
 template <int HD, int NKT, int NW>
-__global__ void __launch_bounds__(NW * 64) attn_bwd_kernel(const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ o,
-                                                           const bf16_t* __restrict__ dout,
-                                                           const float* __restrict__ lse, bf16_t* __restrict__ dqkv,
-                                                           float* __restrict__ bias_partial, int N, int H, int hd,
-                                                           float scale) {
+__global__ void __launch_bounds__(NW * 64, 2) attn_bwd_kernel(const bf16_t* __restrict__ qkv,
+                                                              const bf16_t* __restrict__ dout,
+                                                              const float* __restrict__ lse, bf16_t* __restrict__ dqkv,
+                                                              float* __restrict__ bias_partial, int N, int H, int hd,
+                                                              float scale) {
   constexpr int NP = NKT * 16;
   constexpr int IMG = NP * HD * 2;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* Qi = smem;
-  char* Ki = smem + IMG;
-  char* Vi = smem + 2 * IMG;
-  char* Oi = smem + 3 * IMG;  // dO image
-  float* lse_s = reinterpret_cast<float*>(smem + 4 * IMG);
+  char* ImA = smem;        // K, then Q
+  char* ImB = smem + IMG;  // V, then dO
+  float* lse_s = reinterpret_cast<float*>(smem + 2 * IMG);
   float* dlt_s = lse_s + NP;
   float* bsum = dlt_s + NP;  // [NW][3][HD]
 
@@ -198,12 +215,10 @@ __global__ void __launch_bounds__(NW * 64) attn_bwd_kernel(const bf16_t* __restr
   const long rs = 3L * D;
   const bf16_t* base = qkv + (long)b * N * rs + (long)h * hd;
   const bf16_t* dob = dout + (long)b * N * D + (long)h * hd;
-  const bf16_t* ob = o + (long)b * N * D + (long)h * hd;
-  load_image<HD>(Qi, base, rs, N, hd, NP);
-  load_image<HD>(Ki, base + D, rs, N, hd, NP);
-  load_image<HD>(Vi, base + 2 * D, rs, N, hd, NP);
-  load_image<HD>(Oi, dob, D, N, hd, NP);
-  (void)ob;
+  bf16_t* dq_base = dqkv + (long)b * N * rs + (long)h * hd;
+
+  load_image<HD>(ImA, base + D, rs, N, hd, NP);
+  load_image<HD>(ImB, base + 2 * D, rs, N, hd, NP);
   for (int r = threadIdx.x; r < NP; r += blockDim.x) lse_s[r] = r < N ? lse[(long)bh * N + r] * LOG2E : INFINITY;
   __syncthreads();
 
@@ -211,29 +226,32 @@ __global__ void __launch_bounds__(NW * 64) attn_bwd_kernel(const bf16_t* __restr
   const int g = lane >> 4, i = lane & 15;
   const float c = scale * LOG2E;
   const int npair = (N + 31) / 32;  // pairs of 16-row tiles holding valid rows
+  float bq[HD / 16][4], bk[HD / 16][4], bv[HD / 16][4];
+#pragma unroll
+  for (int dt = 0; dt < HD / 16; ++dt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bq[dt][r] = bk[dt][r] = bv[dt][r] = 0.f;
 
-  // ---- phase 0: delta_q = sum_j P_qj dP_qj from the recomputed P and dP themselves ----
-  // (FlashAttention-2 uses rowsum(dO * O); with bf16 O that differs from sum_j P dP by O's rounding,
-  //  and dS = P (dP - delta) is a small difference of the two — near-uniform attention turned that
-  //  into 10-25% errors on the q/k weight gradients. The consistent delta costs two extra products.)
+  // ---- stage 1: delta and dQ, query-tile pairs ----
   for (int qp = wave; qp < npair; qp += NW) {
     v8bf qf[2][HD / 32], df[2][HD / 32];
-    float ls[2], dsum[2] = {0.f, 0.f};
+    float ls[2], dl[2] = {0.f, 0.f};
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
 #pragma unroll
       for (int kk = 0; kk < HD / 32; ++kk) {
-        qf[u][kk] = rd_row<HD>(Qi, (2 * qp + u) * 16, kk, lane);
-        df[u][kk] = rd_row<HD>(Oi, (2 * qp + u) * 16, kk, lane);
+        qf[u][kk] = gl_row<HD>(base, rs, (2 * qp + u) * 16, kk, N, hd, lane);
+        df[u][kk] = gl_row<HD>(dob, D, (2 * qp + u) * 16, kk, N, hd, lane);
       }
       ls[u] = lse_s[(2 * qp + u) * 16 + i];
     }
+    // pass A: delta
     for (int kt = 0; kt < 2 * npair; ++kt) {
       v8bf kr[HD / 32], vr[HD / 32];
 #pragma unroll
       for (int kk = 0; kk < HD / 32; ++kk) {
-        kr[kk] = rd_row<HD>(Ki, kt * 16, kk, lane);
-        vr[kk] = rd_row<HD>(Vi, kt * 16, kk, lane);
+        kr[kk] = rd_row<HD>(ImA, kt * 16, kk, lane);
+        vr[kk] = rd_row<HD>(ImB, kt * 16, kk, lane);
       }
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
@@ -246,36 +264,91 @@ __global__ void __launch_bounds__(NW * 64) attn_bwd_kernel(const bf16_t* __restr
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int key = kt * 16 + 4 * g + r;
-          if (key < N) dsum[u] += exp2f(st[r] * c - ls[u]) * dpt[r];
+          if (key < N) dl[u] += exp2f(st[r] * c - ls[u]) * dpt[r];
         }
       }
     }
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
-      float v = dsum[u];
-      v += __shfl_xor(v, 16, 64);
-      v += __shfl_xor(v, 32, 64);
+      dl[u] += __shfl_xor(dl[u], 16, 64);
+      dl[u] += __shfl_xor(dl[u], 32, 64);
       const int q = (2 * qp + u) * 16 + i;
-      if (g == 0) dlt_s[q] = q < N ? v : 0.f;
+      if (q >= N) dl[u] = 0.f;
+      if (g == 0) dlt_s[q] = dl[u];
+    }
+    // pass B: dQ
+    v4f dq[2][HD / 16];
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int dt = 0; dt < HD / 16; ++dt) dq[u][dt] = v4f{0.f, 0.f, 0.f, 0.f};
+    for (int ks = 0; ks < npair; ++ks) {
+      v4f DS[2][2];  // [query tile][key tile]
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const int kt = 2 * ks + t;
+        v8bf kr[HD / 32], vr[HD / 32];
+#pragma unroll
+        for (int kk = 0; kk < HD / 32; ++kk) {
+          kr[kk] = rd_row<HD>(ImA, kt * 16, kk, lane);
+          vr[kk] = rd_row<HD>(ImB, kt * 16, kk, lane);
+        }
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          v4f st = {0.f, 0.f, 0.f, 0.f}, dpt = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int kk = 0; kk < HD / 32; ++kk) {
+            st = mfma(kr[kk], qf[u][kk], st);
+            dpt = mfma(vr[kk], df[u][kk], dpt);
+          }
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int key = kt * 16 + 4 * g + r;
+            const float p = key < N ? exp2f(st[r] * c - ls[u]) : 0.f;
+            DS[u][t][r] = p * (dpt[r] - dl[u]);
+          }
+        }
+      }
+      const v8bf bD0 = pack8(DS[0][0], DS[0][1]), bD1 = pack8(DS[1][0], DS[1][1]);
+#pragma unroll
+      for (int dt = 0; dt < HD / 16; ++dt) {
+        const v8bf kt_ = rd_tr<HD>(ImA, 2 * ks, 2 * ks + 1, dt * 16, lane);
+        dq[0][dt] = mfma(kt_, bD0, dq[0][dt]);
+        dq[1][dt] = mfma(kt_, bD1, dq[1][dt]);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int q = (2 * qp + u) * 16 + i;
+      if (q < N) {
+#pragma unroll
+        for (int dt = 0; dt < HD / 16; ++dt) {
+          const int d = dt * 16 + 4 * g;
+          if (d < hd) store4(dq_base + (long)q * rs + d, dq[u][dt], scale);
+        }
+      }
+      if (bias_partial) {
+#pragma unroll
+        for (int dt = 0; dt < HD / 16; ++dt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) bq[dt][r] += sum16(dq[u][dt][r]);  // padded queries: dS = 0
+      }
     }
   }
-  __syncthreads();
-  bf16_t* dq_base = dqkv + (long)b * N * rs + (long)h * hd;
-  float bq[HD / 16][4], bk[HD / 16][4], bv[HD / 16][4];
-#pragma unroll
-  for (int dt = 0; dt < HD / 16; ++dt)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) bq[dt][r] = bk[dt][r] = bv[dt][r] = 0.f;
+  __syncthreads();  // K / V images no longer read; delta complete
 
-  // ---- phase 1: dK, dV (key-tile pairs owned by waves) ----
+  // ---- stage 2: dK and dV, key-tile pairs ----
+  load_image<HD>(ImA, base, rs, N, hd, NP);   // Q
+  load_image<HD>(ImB, dob, D, N, hd, NP);     // dO
+  __syncthreads();
   for (int kp = wave; kp < npair; kp += NW) {
     v8bf kf[2][HD / 32], vf[2][HD / 32];
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
       for (int kk = 0; kk < HD / 32; ++kk) {
-        kf[t][kk] = rd_row<HD>(Ki, (2 * kp + t) * 16, kk, lane);
-        vf[t][kk] = rd_row<HD>(Vi, (2 * kp + t) * 16, kk, lane);
+        kf[t][kk] = gl_row<HD>(base + D, rs, (2 * kp + t) * 16, kk, N, hd, lane);
+        vf[t][kk] = gl_row<HD>(base + 2 * D, rs, (2 * kp + t) * 16, kk, N, hd, lane);
       }
     v4f dv[2][HD / 16], dk[2][HD / 16];
 #pragma unroll
@@ -293,8 +366,8 @@ __global__ void __launch_bounds__(NW * 64) attn_bwd_kernel(const bf16_t* __restr
         v8bf qr[HD / 32], orow[HD / 32];
 #pragma unroll
         for (int kk = 0; kk < HD / 32; ++kk) {
-          qr[kk] = rd_row<HD>(Qi, qt * 16, kk, lane);
-          orow[kk] = rd_row<HD>(Oi, qt * 16, kk, lane);
+          qr[kk] = rd_row<HD>(ImA, qt * 16, kk, lane);
+          orow[kk] = rd_row<HD>(ImB, qt * 16, kk, lane);
         }
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
@@ -318,8 +391,8 @@ __global__ void __launch_bounds__(NW * 64) attn_bwd_kernel(const bf16_t* __restr
       const v8bf bD0 = pack8(DS[0][0], DS[0][1]), bD1 = pack8(DS[1][0], DS[1][1]);
 #pragma unroll
       for (int dt = 0; dt < HD / 16; ++dt) {
-        const v8bf ot = rd_tr<HD>(Oi, 2 * qs, 2 * qs + 1, dt * 16, lane);
-        const v8bf qt = rd_tr<HD>(Qi, 2 * qs, 2 * qs + 1, dt * 16, lane);
+        const v8bf ot = rd_tr<HD>(ImB, 2 * qs, 2 * qs + 1, dt * 16, lane);
+        const v8bf qt = rd_tr<HD>(ImA, 2 * qs, 2 * qs + 1, dt * 16, lane);
         dv[0][dt] = mfma(ot, bP0, dv[0][dt]);
         dv[1][dt] = mfma(ot, bP1, dv[1][dt]);
         dk[0][dt] = mfma(qt, bD0, dk[0][dt]);
@@ -347,79 +420,6 @@ __global__ void __launch_bounds__(NW * 64) attn_bwd_kernel(const bf16_t* __restr
             bk[dt][r] += sum16(dk[t][dt][r]);
             bv[dt][r] += sum16(dv[t][dt][r]);
           }
-      }
-    }
-  }
-
-  // ---- phase 2: dQ (query-tile pairs owned by waves) ----
-  for (int qp = wave; qp < npair; qp += NW) {
-    v8bf qf[2][HD / 32], df[2][HD / 32];
-    float ls[2], dl[2];
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-#pragma unroll
-      for (int kk = 0; kk < HD / 32; ++kk) {
-        qf[u][kk] = rd_row<HD>(Qi, (2 * qp + u) * 16, kk, lane);
-        df[u][kk] = rd_row<HD>(Oi, (2 * qp + u) * 16, kk, lane);
-      }
-      ls[u] = lse_s[(2 * qp + u) * 16 + i];
-      dl[u] = dlt_s[(2 * qp + u) * 16 + i];
-    }
-    v4f dq[2][HD / 16];
-#pragma unroll
-    for (int u = 0; u < 2; ++u)
-#pragma unroll
-      for (int dt = 0; dt < HD / 16; ++dt) dq[u][dt] = v4f{0.f, 0.f, 0.f, 0.f};
-    for (int ks = 0; ks < npair; ++ks) {
-      v4f DS[2][2];  // [query tile][key tile]
-#pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        const int kt = 2 * ks + t;
-        v8bf kr[HD / 32], vr[HD / 32];
-#pragma unroll
-        for (int kk = 0; kk < HD / 32; ++kk) {
-          kr[kk] = rd_row<HD>(Ki, kt * 16, kk, lane);
-          vr[kk] = rd_row<HD>(Vi, kt * 16, kk, lane);
-        }
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          v4f st = {0.f, 0.f, 0.f, 0.f}, dpt = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-          for (int kk = 0; kk < HD / 32; ++kk) {
-            st = mfma(kr[kk], qf[u][kk], st);
-            dpt = mfma(vr[kk], df[u][kk], dpt);
-          }
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int key = kt * 16 + 4 * g + r;
-            const float p = key < N ? exp2f(st[r] * c - ls[u]) : 0.f;
-            DS[u][t][r] = p * (dpt[r] - dl[u]);
-          }
-        }
-      }
-      const v8bf bD0 = pack8(DS[0][0], DS[0][1]), bD1 = pack8(DS[1][0], DS[1][1]);
-#pragma unroll
-      for (int dt = 0; dt < HD / 16; ++dt) {
-        const v8bf kt_ = rd_tr<HD>(Ki, 2 * ks, 2 * ks + 1, dt * 16, lane);
-        dq[0][dt] = mfma(kt_, bD0, dq[0][dt]);
-        dq[1][dt] = mfma(kt_, bD1, dq[1][dt]);
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int q = (2 * qp + u) * 16 + i;
-      if (q < N) {
-#pragma unroll
-        for (int dt = 0; dt < HD / 16; ++dt) {
-          const int d = dt * 16 + 4 * g;
-          if (d < hd) store4(dq_base + (long)q * rs + d, dq[u][dt], scale);
-        }
-      }
-      if (bias_partial) {
-#pragma unroll
-        for (int dt = 0; dt < HD / 16; ++dt)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) bq[dt][r] += sum16(dq[u][dt][r]);  // padded queries: dS = 0
       }
     }
   }
@@ -458,15 +458,26 @@ hipError_t launch_fwd(const bf16_t* qkv, bf16_t* o, float* lse, int B, int N, in
   return hipGetLastError();
 }
 
+template <int HD, int NKT, int NW>
+hipError_t launch_bwd_nw(const bf16_t* qkv, const bf16_t* dout, const float* lse, bf16_t* dqkv, float* bias_partial,
+                         int B, int N, int H, int hd, float scale, hipStream_t s) {
+  const size_t lds = (size_t)2 * NKT * 16 * HD * 2 + 2 * NKT * 16 * 4 + (size_t)NW * 3 * HD * 4;
+  auto kern = attn_bwd_kernel<HD, NKT, NW>;
+  (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipLaunchKernelGGL(kern, dim3(B * H), dim3(NW * 64), lds, s, qkv, dout, lse, dqkv, bias_partial, N, H, hd, scale);
+  return hipGetLastError();
+}
+
 template <int HD, int NKT>
 hipError_t launch_bwd(const bf16_t* qkv, const bf16_t* o, const bf16_t* dout, const float* lse, bf16_t* dqkv,
                       float* bias_partial, int B, int N, int H, int hd, float scale, hipStream_t s) {
-  constexpr int NW = 8;
-  const size_t lds = (size_t)4 * NKT * 16 * HD * 2 + 2 * NKT * 16 * 4 + (size_t)NW * 3 * HD * 4;
-  auto kern = attn_bwd_kernel<HD, NKT, NW>;
-  (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL(kern, dim3(B * H), dim3(NW * 64), lds, s, qkv, o, dout, lse, dqkv, bias_partial, N, H, hd, scale);
-  return hipGetLastError();
+  (void)o;
+  static const int nw = [] {
+    const char* e = getenv("VIT_ATTN_BWD_NW");
+    return e ? atoi(e) : 4;
+  }();
+  if (nw == 8) return launch_bwd_nw<HD, NKT, 8>(qkv, dout, lse, dqkv, bias_partial, B, N, H, hd, scale, s);
+  return launch_bwd_nw<HD, NKT, 4>(qkv, dout, lse, dqkv, bias_partial, B, N, H, hd, scale, s);
 }
 
 #define VIT_NKT_CASES(X) X(2) X(4) X(6) X(8) X(10) X(12) X(14) X(16) X(18) X(20)

@@ -87,31 +87,36 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const void* __restrict__ dy
     gm[k] = c < D ? *reinterpret_cast<const float4*>(gamma + c) : make_float4(0.f, 0.f, 0.f, 0.f);
   }
   for (int row = blockIdx.x * 4 + wave; row < rows; row += gridDim.x * 4) {
+    // issue every load of the row up front (dy, x, residual grad, stats) so their latencies overlap
     const float mu = mean[row], rs = rstd[row];
-    float4 xh[NV], g[NV];
-    float s1 = 0.f, s2 = 0.f;
+    float4 d4[NV], x4[NV], r4[NV];
 #pragma unroll
     for (int k = 0; k < NV; ++k) {
       const int c = (k * 64 + lane) * 4;
       if (c < D) {
-        float4 d4;
         if (dy_f32) {
-          d4 = *reinterpret_cast<const float4*>((const float*)dy + (long)row * lddy + c);
+          d4[k] = *reinterpret_cast<const float4*>((const float*)dy + (long)row * lddy + c);
         } else {
           const uint2 u = *reinterpret_cast<const uint2*>((const bf16_t*)dy + (long)row * lddy + c);
-          d4 = make_float4(bf2f(u.x & 0xffff), bf2f(u.x >> 16), bf2f(u.y & 0xffff), bf2f(u.y >> 16));
+          d4[k] = make_float4(bf2f(u.x & 0xffff), bf2f(u.x >> 16), bf2f(u.y & 0xffff), bf2f(u.y >> 16));
         }
-        const float4 x4 = *reinterpret_cast<const float4*>(x + (long)row * ldx + c);
-        xh[k] = make_float4((x4.x - mu) * rs, (x4.y - mu) * rs, (x4.z - mu) * rs, (x4.w - mu) * rs);
-        g[k] = make_float4(d4.x * gm[k].x, d4.y * gm[k].y, d4.z * gm[k].z, d4.w * gm[k].w);
-        s1 += g[k].x + g[k].y + g[k].z + g[k].w;
-        s2 += g[k].x * xh[k].x + g[k].y * xh[k].y + g[k].z * xh[k].z + g[k].w * xh[k].w;
-        pg[k].x += d4.x * xh[k].x; pg[k].y += d4.y * xh[k].y; pg[k].z += d4.z * xh[k].z; pg[k].w += d4.w * xh[k].w;
-        pb[k].x += d4.x; pb[k].y += d4.y; pb[k].z += d4.z; pb[k].w += d4.w;
+        x4[k] = *reinterpret_cast<const float4*>(x + (long)row * ldx + c);
+        r4[k] = dres ? *reinterpret_cast<const float4*>(dres + (long)row * lddres + c) : make_float4(0.f, 0.f, 0.f, 0.f);
       } else {
-        xh[k] = make_float4(0.f, 0.f, 0.f, 0.f);
-        g[k] = xh[k];
+        d4[k] = x4[k] = r4[k] = make_float4(0.f, 0.f, 0.f, 0.f);
       }
+    }
+    float4 xh[NV], g[NV];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      xh[k] = make_float4((x4[k].x - mu) * rs, (x4[k].y - mu) * rs, (x4[k].z - mu) * rs, (x4[k].w - mu) * rs);
+      g[k] = make_float4(d4[k].x * gm[k].x, d4[k].y * gm[k].y, d4[k].z * gm[k].z, d4[k].w * gm[k].w);
+      s1 += g[k].x + g[k].y + g[k].z + g[k].w;
+      s2 += g[k].x * xh[k].x + g[k].y * xh[k].y + g[k].z * xh[k].z + g[k].w * xh[k].w;
+      pg[k].x += d4[k].x * xh[k].x; pg[k].y += d4[k].y * xh[k].y; pg[k].z += d4[k].z * xh[k].z;
+      pg[k].w += d4[k].w * xh[k].w;
+      pb[k].x += d4[k].x; pb[k].y += d4[k].y; pb[k].z += d4[k].z; pb[k].w += d4[k].w;
     }
     const float m1 = wave_sum(s1) / D, m2 = wave_sum(s2) / D;
 #pragma unroll
@@ -119,14 +124,10 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const void* __restrict__ dy
       const int c = (k * 64 + lane) * 4;
       if (c < D) {
         float4 o;
-        o.x = rs * (g[k].x - m1 - xh[k].x * m2);
-        o.y = rs * (g[k].y - m1 - xh[k].y * m2);
-        o.z = rs * (g[k].z - m1 - xh[k].z * m2);
-        o.w = rs * (g[k].w - m1 - xh[k].w * m2);
-        if (dres) {
-          const float4 r4 = *reinterpret_cast<const float4*>(dres + (long)row * lddres + c);
-          o.x += r4.x; o.y += r4.y; o.z += r4.z; o.w += r4.w;
-        }
+        o.x = rs * (g[k].x - m1 - xh[k].x * m2) + r4[k].x;
+        o.y = rs * (g[k].y - m1 - xh[k].y * m2) + r4[k].y;
+        o.z = rs * (g[k].z - m1 - xh[k].z * m2) + r4[k].z;
+        o.w = rs * (g[k].w - m1 - xh[k].w * m2) + r4[k].w;
         *reinterpret_cast<float4*>(dx + (long)row * lddx + c) = o;
         ps[k].x += o.x; ps[k].y += o.y; ps[k].z += o.z; ps[k].w += o.w;
         if (dxb) {

@@ -42,21 +42,24 @@ class GradAllReducer:
     def detach(self):
         self.engine.grad_ready_hook = None
 
-    def _launch(self, buf, start, end):
+    def _launch(self, buf, start, end, events=()):
         t = buf[start:end]
         op = dist.ReduceOp.AVG if self.native_avg else dist.ReduceOp.SUM
         if self.average and not self.native_avg:
             self._to_scale.append(t)
         if self.cuda:
-            ev = torch.cuda.Event()
-            ev.record(torch.cuda.current_stream(self.engine.dev))
-            self.stream.wait_event(ev)
+            if not events:
+                ev = torch.cuda.Event()
+                ev.record(torch.cuda.current_stream(self.engine.dev))
+                events = (ev,)
+            for ev in events:  # the bucket's producers (main and side streams of the engine)
+                self.stream.wait_event(ev)
             with torch.cuda.stream(self.stream):
                 dist.all_reduce(t, op=op, group=self.group)
         else:
             self._works.append(dist.all_reduce(t, op=op, group=self.group, async_op=True))
 
-    def hook(self, buf, name, start, end):
+    def hook(self, buf, name, start, end, events=()):
         if self.world == 1:
             return
         if self._pending is not None:
@@ -65,7 +68,7 @@ class GradAllReducer:
         if end - start < self.min_bucket and name != "embed":
             self._pending = start  # coalesce small buckets (head) with the next layer's
             return
-        self._launch(buf, start, end)
+        self._launch(buf, start, end, events)
 
     def finish(self):
         """Make the compute stream wait for every outstanding all-reduce."""

@@ -149,12 +149,14 @@ class _Acts:
         self.rsf = z(b, dt=f)
         self.logits = z(b, cfg.num_classes, dt=f)
         # backward scratch
+        # (bf16 gradient operands are double-buffered: the weight-gradient GEMMs read them on a side
+        #  stream while the main stream already produces the next layer's)
         self.dh = z(Tp, D, dt=f)
-        self.dhb = z(Tp, D)
-        self.dg = z(Tp, M)
+        self.dhb = [z(Tp, D), z(Tp, D)]
+        self.dg = [z(Tp, M), z(Tp, M)]
         self.dyln = z(Tp, D)
         self.dO = z(Tp, D)
-        self.dqkv = z(Tp, 3 * D)
+        self.dqkv = [z(Tp, 3 * D), z(Tp, 3 * D)]
         self.dlncls = z(b, D, dt=f)
         self.dlogits = z(b, cfg.num_classes, dt=f)
         self.row_stats = z(b, 3, dt=f)
@@ -192,7 +194,9 @@ class ViTEngine:
         self._mirror_sig = None
         self._ws = None
         self.step_id = 0
-        self.grad_ready_hook = None  # callable(grad_buf, bucket_name, start, end) during backward
+        self.grad_ready_hook = None  # callable(grad_buf, bucket_name, start, end, events) during backward
+        self.overlap_wgrad = True    # weight-gradient GEMMs on a side stream, overlapped with the dgrad chain
+        self._side = None
         self.probe = None  # list: (start, end) HIP events around every fc1 forward GEMM launch
 
     # ---- parameters --------------------------------------------------------------------------
@@ -333,7 +337,12 @@ class ViTEngine:
     # ---- backward --------------------------------------------------------------------------------
     def backward(self, dlogits: torch.Tensor, grad: torch.Tensor | None = None):
         """Backward of the last forward given dL/dlogits [b, C]; writes every parameter gradient
-        into `grad` (default self.grad, flat layout)."""
+        into `grad` (default self.grad, flat layout).
+
+        Two streams: the main stream runs the data-gradient chain (dgrad GEMMs, LayerNorm and
+        attention backward); the weight-gradient GEMMs, which nothing downstream waits for, run on
+        a side stream as soon as their operands exist. bf16 gradient operands are double-buffered
+        and each buffer is recycled only after the side stream has consumed it."""
         cfg = self.cfg
         b = self._last_b
         a = self.acts(b)
@@ -346,60 +355,118 @@ class ViTEngine:
         gv = lambda name: g[self.off(name):]
         dl = dlogits.to(self.dev, torch.float32).contiguous()
         hook = self.grad_ready_hook
+        main = torch.cuda.current_stream(self.dev)
+        overlap = self.overlap_wgrad
+        if overlap and self._side is None:
+            self._side = torch.cuda.Stream(device=self.dev)
+        side = self._side if overlap else main
+        free_ev = {}  # (buffer kind, index) -> event recorded on the side stream after its last read
+
+        def on_side(fn):
+            """run fn() on the side stream after everything issued so far on the main stream."""
+            if not overlap:
+                fn()
+                return
+            ev = torch.cuda.Event()
+            ev.record(main)
+            side.wait_event(ev)
+            with torch.cuda.stream(side):
+                fn()
+
+        def release(kind, idx):
+            if overlap:
+                ev = torch.cuda.Event()
+                ev.record(side)
+                free_ev[(kind, idx)] = ev
+
+        def acquire(kind, idx):
+            ev = free_ev.pop((kind, idx), None)
+            if ev is not None:
+                main.wait_event(ev)
+
+        def fire(bucket):
+            if not hook:
+                return
+            evs = []
+            if overlap:
+                for st in (main, side):
+                    ev = torch.cuda.Event()
+                    ev.record(st)
+                    evs.append(ev)
+            hook(g, *bucket, evs)
+
         # classifier head (f32): dWc = dl^T lncls, dbc = colsum(dl), dlncls = dl Wc
         ops.gemm_f32(C, D, b, dl, C, True, a.lncls, D, False, gv("classifier.weight"), D)
         ops.colsum(dl, b, C, C, a.colpart, gv("classifier.bias"))
         ops.gemm_f32(b, D, C, dl, C, False, f[self.off("classifier.weight"):], D, False, a.dlncls, D)
         # final LN backward on cls rows -> residual grad (zero elsewhere)
-        a.dh.zero_()
-        a.dhb.zero_()
         # (its dx column sum is the last layer's fc2 bias gradient: only the cls rows are non-zero)
+        wb = 0  # index of the dhb buffer holding the current residual-gradient copy
+        a.dh.zero_()
+        a.dhb[wb].zero_()
         ops.layernorm_bwd(a.dlncls, D, a.h[L], N * D, a.muf, a.rsf, f[self.off("transformer.norm.weight"):], a.dh,
-                          N * D, a.lnpart, b, D, dx_bf16=a.dhb, lddxb=N * D,
+                          N * D, a.lnpart, b, D, dx_bf16=a.dhb[wb], lddxb=N * D,
                           dgamma_dbeta=gv("transformer.norm.weight"),
                           dx_colsum=gv(self.lname(L - 1, "mlp.fc2.bias")))
-        if hook:
-            hook(g, *self.layout.buckets[0])
+        fire(self.layout.buckets[0])
         scale = 1.0 / math.sqrt(hd)
         for i in reversed(range(L)):
             ln = lambda s: self.off(self.lname(i, s))
+            li = i & 1
+            dhb = a.dhb[wb]
             # ---- MLP: h_{i+1} = hm + fc2(gelu(fc1(ln2(hm)))) ----
             # (fc2 bias grad = column sums of dh, already produced by the LayerNorm backward above)
-            self._wgrad(a.dhb, D, a.g[i], M, D, M, a.Tp, gv(self.lname(i, "mlp.fc2.weight")), M)
+            on_side(lambda: self._wgrad(dhb, D, a.g[i], M, D, M, a.Tp, gv(self.lname(i, "mlp.fc2.weight")), M))
+            release("dhb", wb)
+            dg = a.dg[li]
+            acquire("dg", li)
             kw = dict(a_layout=K_CONTIG, b_layout=MN_CONTIG, lda=D, ldb=M, ldc=M, epilogue=EPI_GELU_BWD, aux=a.u[i],
                       ldaux=M, col_partial=a.gelu_part)
-            ops.gemm(a.dhb, mv[ln("mlp.fc2.weight"):], a.dg, T, M, D, **kw)
-            tiles_m = -(-T // ops.gemm_tile_rows(a.dhb, mv, a.dg, T, M, D, **kw))
+            ops.gemm(dhb, mv[ln("mlp.fc2.weight"):], dg, T, M, D, **kw)
+            tiles_m = -(-T // ops.gemm_tile_rows(dhb, mv, dg, T, M, D, **kw))
             ops.colsum(a.gelu_part, tiles_m, M, M, a.colpart, gv(self.lname(i, "mlp.fc1.bias")))
-            self._wgrad(a.dg, M, a.ln2[i], D, M, D, a.Tp, gv(self.lname(i, "mlp.fc1.weight")), D)
-            ops.gemm(a.dg, mv[ln("mlp.fc1.weight"):], a.dyln, T, D, M, a_layout=K_CONTIG, b_layout=MN_CONTIG, lda=M,
+            on_side(lambda: self._wgrad(dg, M, a.ln2[i], D, M, D, a.Tp, gv(self.lname(i, "mlp.fc1.weight")), D))
+            release("dg", li)
+            ops.gemm(dg, mv[ln("mlp.fc1.weight"):], a.dyln, T, D, M, a_layout=K_CONTIG, b_layout=MN_CONTIG, lda=M,
                      ldb=D, ldc=D, epilogue=EPI_BF16)
+            wb ^= 1
+            acquire("dhb", wb)
+            dhb = a.dhb[wb]
             ops.layernorm_bwd(a.dyln, D, a.hm[i], D, a.mu2[i], a.rs2[i], f[ln("norm2.weight"):], a.dh, D, a.lnpart, T,
-                              D, dres=a.dh, lddres=D, dx_bf16=a.dhb, lddxb=D,
+                              D, dres=a.dh, lddres=D, dx_bf16=dhb, lddxb=D,
                               dgamma_dbeta=gv(self.lname(i, "norm2.weight")),
                               dx_colsum=gv(self.lname(i, "attn.out.bias")))
             # ---- attention: hm = h + out(attn(ln1(h))) ----
-            self._wgrad(a.o[i], D, a.dhb, D, D, D, a.Tp, gv(self.lname(i, "attn.out.weight")), D)
-            ops.gemm(a.dhb, mv[ln("attn.out.weight"):], a.dO, T, D, D, a_layout=K_CONTIG, b_layout=K_CONTIG, lda=D,
+            on_side(lambda: self._wgrad(a.o[i], D, dhb, D, D, D, a.Tp, gv(self.lname(i, "attn.out.weight")), D))
+            release("dhb", wb)
+            ops.gemm(dhb, mv[ln("attn.out.weight"):], a.dO, T, D, D, a_layout=K_CONTIG, b_layout=K_CONTIG, lda=D,
                      ldb=D, ldc=D, epilogue=EPI_BF16)
-            ops.attention_bwd(a.qkv[i], a.o[i], a.dO, a.lse[i], a.dqkv, b, N, H, hd, scale, bias_partial=a.qkv_bpart)
+            dqkv = a.dqkv[li]
+            acquire("dqkv", li)
+            ops.attention_bwd(a.qkv[i], a.o[i], a.dO, a.lse[i], dqkv, b, N, H, hd, scale, bias_partial=a.qkv_bpart)
             qo = ln("attn.query.weight")
             zs = ln("attn.key.weight") - qo
             for z in range(3):
                 ops.colsum(a.qkv_bpart[:, z * D:], b, D, 3 * D, a.colpart, g[ln("attn.query.bias") + z * zs:])
-            self._wgrad(a.ln1[i], D, a.dqkv, 3 * D, D, D, a.Tp, g[qo:], D, batch=3, b_bs=D, out_bs=zs)
-            ops.gemm(a.dqkv, self.wqkv[i], a.dyln, T, D, 3 * D, a_layout=K_CONTIG, b_layout=K_CONTIG, lda=3 * D,
+            on_side(lambda: self._wgrad(a.ln1[i], D, dqkv, 3 * D, D, D, a.Tp, g[qo:], D, batch=3, b_bs=D,
+                                        out_bs=zs))
+            release("dqkv", li)
+            ops.gemm(dqkv, self.wqkv[i], a.dyln, T, D, 3 * D, a_layout=K_CONTIG, b_layout=K_CONTIG, lda=3 * D,
                      ldb=3 * D, ldc=D, epilogue=EPI_BF16)
+            wb ^= 1
+            acquire("dhb", wb)
             ops.layernorm_bwd(a.dyln, D, a.h[i], D, a.mu1[i], a.rs1[i], f[ln("norm1.weight"):], a.dh, D, a.lnpart, T,
-                              D, dres=a.dh, lddres=D, dx_bf16=a.dhb, lddxb=D,
+                              D, dres=a.dh, lddres=D, dx_bf16=a.dhb[wb], lddxb=D,
                               dgamma_dbeta=gv(self.lname(i, "norm1.weight")),
                               dx_colsum=gv(self.lname(i - 1, "mlp.fc2.bias")) if i > 0 else None)
-            if hook:
-                hook(g, *self.layout.buckets[L - i])
+            fire(self.layout.buckets[L - i])
         # ---- embedding: conv weight grad (wgrad over patches), bias / pos / cls ----
-        self._wgrad(a.dhb, D, a.patches, a.kpad, D, cfg.patch_k, a.Tp, gv("embedding.weight"), cfg.patch_k)
+        dhb = a.dhb[wb]
+        on_side(lambda: self._wgrad(dhb, D, a.patches, a.kpad, D, cfg.patch_k, a.Tp, gv("embedding.weight"),
+                                    cfg.patch_k))
         ops.embed_grad(a.dh, b, N, D, gv("transformer.pos_embedding.pos_embedding"), gv("cls_token"),
                        gv("embedding.bias"))
-        if hook:
-            hook(g, *self.layout.buckets[-1])
+        fire(self.layout.buckets[-1])
+        if overlap:
+            main.wait_stream(side)
         return g
