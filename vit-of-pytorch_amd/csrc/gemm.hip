@@ -16,6 +16,7 @@
 //   * Buffer descriptors bound every operand, so M/N tails read zeros instead of faulting.
 //   * XCD-aware bijective block remap so consecutive tiles (same A rows) share an XCD's L2.
 #include "common.h"
+#include <stdlib.h>
 
 namespace {
 
@@ -43,7 +44,25 @@ struct GemmDev {
   int tokens;
   int vec;  // every pointer / leading dim allows 8-column (16/32-B) vector access
   float* col_partial;  // optional per-M-tile column sums of the output
+  int group_m;         // tile order: groups of group_m tile rows, column-major inside (0: row-major)
+  int nt;              // non-temporal output stores (keep the operands resident in L2)
 };
+
+// blockIdx (after the XCD remap) -> output tile. Grouping tile rows keeps the weight panels a
+// group's concurrent workgroups share hot in the XCD's L2.
+__device__ __forceinline__ void tile_coords(int wg, int tiles_m, int tiles_n, int gm, int& tm, int& tn) {
+  if (gm <= 1) {
+    tm = wg / tiles_n;
+    tn = wg % tiles_n;
+    return;
+  }
+  const int per = gm * tiles_n;
+  const int first = (wg / per) * gm;
+  const int rows = tiles_m - first < gm ? tiles_m - first : gm;
+  const int r = wg % per;
+  tm = first + r % rows;
+  tn = r / rows;
+}
 
 // K-contiguous image [rows][BK]: XOR of the 16-B chunk index, conflict-free for the 16x16x32
 // fragment read (16 rows x 16 B per ds_read_b128 lane group).
@@ -161,14 +180,24 @@ __device__ __forceinline__ void ld8f(const float* p, float* v) {
   const float4 b = *reinterpret_cast<const float4*>(p + 4);
   v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
 }
-__device__ __forceinline__ void st8f(float* p, const float* v) {
-  *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
-  *reinterpret_cast<float4*>(p + 4) = make_float4(v[4], v[5], v[6], v[7]);
+typedef float v4f_t __attribute__((ext_vector_type(4)));
+typedef unsigned v4u_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void st8f(float* p, const float* v, bool nt = false) {
+  const v4f_t a = {v[0], v[1], v[2], v[3]}, b = {v[4], v[5], v[6], v[7]};
+  if (nt) {
+    __builtin_nontemporal_store(a, reinterpret_cast<v4f_t*>(p));
+    __builtin_nontemporal_store(b, reinterpret_cast<v4f_t*>(p + 4));
+  } else {
+    *reinterpret_cast<v4f_t*>(p) = a;
+    *reinterpret_cast<v4f_t*>(p + 4) = b;
+  }
 }
-__device__ __forceinline__ void st8bf(bf16_t* p, const float* v) {
-  uint4 u;
-  u.x = pack2bf(v[0], v[1]); u.y = pack2bf(v[2], v[3]); u.z = pack2bf(v[4], v[5]); u.w = pack2bf(v[6], v[7]);
-  *reinterpret_cast<uint4*>(p) = u;
+__device__ __forceinline__ void st8bf(bf16_t* p, const float* v, bool nt = false) {
+  const v4u_t u = {pack2bf(v[0], v[1]), pack2bf(v[2], v[3]), pack2bf(v[4], v[5]), pack2bf(v[6], v[7])};
+  if (nt)
+    __builtin_nontemporal_store(u, reinterpret_cast<v4u_t*>(p));
+  else
+    *reinterpret_cast<v4u_t*>(p) = u;
 }
 __device__ __forceinline__ void ld8bf(const bf16_t* p, float* v) {
   const uint4 u = *reinterpret_cast<const uint4*>(p);
@@ -184,13 +213,13 @@ __device__ __forceinline__ void epi_store8(const GemmDev& p, int z, int split_id
     if (p.bias) ld8f(p.bias + z * p.bias_bs + n, b);
   }
   if constexpr (EPI == VIT_EPI_F32) {
-    st8f((float*)p.C + z * p.c_bs + (long)m * p.ldc + n, v);
+    st8f((float*)p.C + z * p.c_bs + (long)m * p.ldc + n, v, p.nt);
   } else if constexpr (EPI == VIT_EPI_BF16) {
-    st8bf((bf16_t*)p.C + z * p.c_bs + (long)m * p.ldc + n, v);
+    st8bf((bf16_t*)p.C + z * p.c_bs + (long)m * p.ldc + n, v, p.nt);
   } else if constexpr (EPI == VIT_EPI_BIAS_BF16) {
 #pragma unroll
     for (int k = 0; k < 8; ++k) v[k] += b[k];
-    st8bf((bf16_t*)p.C + z * p.c_bs + (long)m * p.ldc + n, v);
+    st8bf((bf16_t*)p.C + z * p.c_bs + (long)m * p.ldc + n, v, p.nt);
   } else if constexpr (EPI == VIT_EPI_BIAS_GELU) {
     float gl[8];
 #pragma unroll
@@ -198,20 +227,20 @@ __device__ __forceinline__ void epi_store8(const GemmDev& p, int z, int split_id
       v[k] += b[k];
       gl[k] = gelu_f(v[k]);
     }
-    st8bf((bf16_t*)p.C + z * p.c_bs + (long)m * p.ldc + n, v);
-    st8bf((bf16_t*)p.C2 + z * p.c_bs + (long)m * p.ldc2 + n, gl);
+    st8bf((bf16_t*)p.C + z * p.c_bs + (long)m * p.ldc + n, v, p.nt);
+    st8bf((bf16_t*)p.C2 + z * p.c_bs + (long)m * p.ldc2 + n, gl, p.nt);
   } else if constexpr (EPI == VIT_EPI_BIAS_RESID_F32) {
     float r[8];
     ld8f((const float*)p.aux + (long)m * p.ldaux + n, r);
 #pragma unroll
     for (int k = 0; k < 8; ++k) v[k] += b[k] + r[k];
-    st8f((float*)p.C + z * p.c_bs + (long)m * p.ldc + n, v);
+    st8f((float*)p.C + z * p.c_bs + (long)m * p.ldc + n, v, p.nt);
   } else if constexpr (EPI == VIT_EPI_GELU_BWD) {
     float u[8];
     ld8bf((const bf16_t*)p.aux + (long)m * p.ldaux + n, u);
 #pragma unroll
     for (int k = 0; k < 8; ++k) v[k] *= gelu_grad_f(u[k]);
-    st8bf((bf16_t*)p.C + z * p.c_bs + (long)m * p.ldc + n, v);
+    st8bf((bf16_t*)p.C + z * p.c_bs + (long)m * p.ldc + n, v, p.nt);
   } else if constexpr (EPI == VIT_EPI_PATCH) {
     const int t = m % p.tokens;
     float ps[8];
@@ -225,9 +254,9 @@ __device__ __forceinline__ void epi_store8(const GemmDev& p, int z, int split_id
 #pragma unroll
       for (int k = 0; k < 8; ++k) v[k] += b[k] + ps[k];
     }
-    st8f((float*)p.C + (long)m * p.ldc + n, v);
+    st8f((float*)p.C + (long)m * p.ldc + n, v, p.nt);
   } else if constexpr (EPI == VIT_EPI_SPLITK) {
-    st8f((float*)p.C + ((long)z * p.split_k + split_idx) * (long)p.M * p.N + (long)m * p.N + n, v);
+    st8f((float*)p.C + ((long)z * p.split_k + split_idx) * (long)p.M * p.N + (long)m * p.N + n, v, p.nt);
   }
 }
 
@@ -272,7 +301,8 @@ __global__ void __launch_bounds__(WM* WN * 64, (gemm_min_waves<BM, BN, BK, STAGE
   const int orig = blockIdx.x;
   const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
   const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
-  const int tm = wg / tiles_n, tn = wg % tiles_n;
+  int tm, tn;
+  tile_coords(wg, tiles_m, tiles_n, p.group_m, tm, tn);
   const int m0 = tm * BM, n0 = tn * BN;
   const int z = blockIdx.z;
   const int split_idx = blockIdx.y;
@@ -399,6 +429,212 @@ __global__ void __launch_bounds__(WM* WN * 64, (gemm_min_waves<BM, BN, BK, STAGE
   }
 }
 
+// ---- ping-pong kernel ---------------------------------------------------------------------------
+// 256 x BN x 64 workgroup tile, 8 waves in two groups of 4: group g owns output rows 128g..128g+127,
+// wave w of a group owns columns w*BN/4 .. +BN/4 (8 x BN/64 accumulator fragments). Time is cut into
+// slots separated by workgroup barriers. In every slot one group reads the fragments of a 64-deep
+// k-tile from LDS while the other group multiplies the fragments it read in the previous slot, so on
+// each SIMD (one wave of each group) LDS reads and MFMA chains of the two waves alternate instead of
+// serialising. Two LDS k-tile buffers: the LDS-DMA of k-tile u+1 is issued at the start of the slot
+// in which group 0 starts on k-tile u (both groups are done reading k-tile u-1 from that buffer) and
+// is waited for at the end of the following slot, before group 0 first reads it: two slots of flight,
+// raw s_barrier (no vmcnt(0) drain at the barriers in between).
+// Epilogue: wave-private fp32 staging in the then idle LDS (32 rows per pass), 8-column chunks.
+template <int BN, int NBUF, bool AK, bool BKC, int EPI>
+__global__ void __launch_bounds__(512) gemm_pp_kernel(const GemmDev p) {
+  constexpr int BM = 256, BK = 64, NWAVE = 8;
+  constexpr int TN = BN / 4, FM = 8, FN = TN / 16;
+  constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
+  constexpr int LPT = STAGE / 1024 / NWAVE;  // DMA instructions per wave per k-tile
+  constexpr int LDW = TN + 4;                // staging row stride (floats): conflict-free ds_write_b32
+  constexpr int PR = 32;                     // staged rows per pass (4 passes over the wave's 128 rows)
+  constexpr int WST = PR * LDW * 4;          // staging bytes per wave
+  static_assert(NWAVE * WST <= NBUF * STAGE, "staging must fit in the pipeline buffers");
+  static_assert(NBUF == 2 || NBUF == 3, "k-tile buffers");
+  static_assert(NBUF * STAGE <= 160 * 1024, "LDS budget");
+  __shared__ __attribute__((aligned(16))) char smem[NBUF * STAGE];
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int grp = wave >> 2, wn = wave & 3;
+
+  const int tiles_m = (p.M + BM - 1) / BM, tiles_n = (p.N + BN - 1) / BN;
+  const int nwg = tiles_m * tiles_n;
+  const int orig = blockIdx.x;
+  const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  int tm, tn;
+  tile_coords(wg, tiles_m, tiles_n, p.group_m, tm, tn);
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int z = blockIdx.z;
+  const int split_idx = blockIdx.y;
+
+  const char* Ab = p.A + (long)z * p.a_bs * 2;
+  const char* Bb = p.B + (long)z * p.b_bs * 2;
+  const long a_shift = AK ? (long)m0 * p.lda * 2 : (long)m0 * 2;
+  const long b_shift = BKC ? (long)n0 * p.ldb * 2 : (long)n0 * 2;
+  const uint32_t a_rec = (long)p.a_bytes > a_shift ? (uint32_t)(p.a_bytes - a_shift) : 0u;
+  const uint32_t b_rec = (long)p.b_bytes > b_shift ? (uint32_t)(p.b_bytes - b_shift) : 0u;
+  const __amdgpu_buffer_rsrc_t rsA = make_rsrc(Ab + a_shift, a_rec);
+  const __amdgpu_buffer_rsrc_t rsB = make_rsrc(Bb + b_shift, b_rec);
+
+  const int nkt = p.K / BK;
+  const int kt0 = (int)((long)nkt * split_idx / p.split_k);
+  const int kt1 = (int)((long)nkt * (split_idx + 1) / p.split_k);
+  const int nk = kt1 - kt0;
+
+  v4f acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+  v8s af[2][FM], bfr[2][FN];
+  const int wm0 = grp * 128, wn0 = wn * TN;
+
+  auto issue = [&](int t) {
+    const int buf = (t % NBUF) * STAGE;
+    stage_tile<BM, BK, AK, NWAVE>(smem, buf, rsA, p.lda, kt0 + t, wave, lane);
+    stage_tile<BN, BK, BKC, NWAVE>(smem, buf + A_BYTES, rsB, p.ldb, kt0 + t, wave, lane);
+  };
+  auto mem = [&](int j) {
+    const int cur = (j % NBUF) * STAGE;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+#pragma unroll
+      for (int jn = 0; jn < FN; ++jn) bfr[kk][jn] = read_frag<BN, BK, BKC>(smem, cur + A_BYTES, wn0 + jn * 16, kk, lane);
+#pragma unroll
+      for (int i = 0; i < FM; ++i) af[kk][i] = read_frag<BM, BK, AK>(smem, cur, wm0 + i * 16, kk, lane);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  };
+  auto compute = [&]() {
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int jn = 0; jn < FN; ++jn)
+          acc[i][jn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(v8bf, af[kk][i]),
+                                                               __builtin_bit_cast(v8bf, bfr[kk][jn]), acc[i][jn], 0, 0, 0);
+  };
+
+  // prologue: k-tiles 0 .. L-1 in flight, k-tile 0 landed
+  constexpr int L = NBUF - 1;
+#pragma unroll
+  for (int t = 0; t < L; ++t)
+    if (t < nk) issue(t);
+  if (L == 2 && nk > 1)
+    wait_vm<LPT>();
+  else
+    wait_vm<0>();
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+
+  // slot s: group g reads k-tile j in slot 2j+g and multiplies it in slot 2j+g+1. At the start of
+  // slot 2u, k-tile u+L goes into the buffer k-tile u-1 used (read by group 1 in slot 2u-1); at the
+  // end of slot 2u+1 k-tile u+1 has landed (group 0 reads it in slot 2u+2). The two groups run
+  // separate straight-line loops (a slot-role branch inside one loop makes the compiler copy the
+  // accumulators at every join).
+  auto end_odd = [&](int u) {  // end of slot 2u+1
+    const int issued = u + L < nk ? u + L : nk - 1;
+    __builtin_amdgcn_sched_barrier(0);
+    if (L == 2 && issued >= u + 2)
+      wait_vm<LPT>();
+    else
+      wait_vm<0>();
+    asm volatile("s_barrier" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  auto end_even = [&]() {
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_barrier" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  if (grp == 0) {
+    for (int j = 0; j < nk; ++j) {
+      if (j + L < nk) issue(j + L);  // slot 2j
+      mem(j);
+      end_even();
+      compute();  // slot 2j+1
+      end_odd(j);
+    }
+  } else if (nk > 0) {
+    if (L < nk) issue(L);  // slot 0
+    end_even();
+    for (int j = 0; j < nk - 1; ++j) {
+      mem(j);  // slot 2j+1
+      end_odd(j);
+      if (j + 1 + L < nk) issue(j + 1 + L);  // slot 2j+2
+      compute();
+      end_even();
+    }
+    mem(nk - 1);  // slot 2nk-1
+    end_odd(nk - 1);
+    compute();  // slot 2nk: LDS is free from here on
+  }
+
+  // ---- epilogue ----
+  const int g = lane >> 4, c = lane & 15;
+  float* ws = reinterpret_cast<float*>(smem + wave * WST);
+  constexpr int CPR = TN / 8;  // 8-column chunks per staged row
+  float csum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int pass = 0; pass < 128 / PR; ++pass) {
+#pragma unroll
+    for (int i = 0; i < PR / 16; ++i)
+#pragma unroll
+      for (int jn = 0; jn < FN; ++jn)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) ws[(i * 16 + 4 * g + r) * LDW + jn * 16 + c] = acc[pass * (PR / 16) + i][jn][r];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll 2
+    for (int e = lane; e < PR * CPR; e += 64) {
+      const int row = e / CPR, ch = e % CPR;
+      const int m = m0 + wm0 + pass * PR + row, n = n0 + wn0 + ch * 8;
+      float v[8];
+      ld8f(ws + row * LDW + ch * 8, v);
+      if (m >= p.M || n >= p.N) continue;
+      if (p.vec && n + 8 <= p.N) {
+        epi_store8<EPI>(p, z, split_idx, m, n, v);
+        if (p.col_partial) {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) csum[k] += v[k];
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) epi_store<EPI>(p, z, split_idx, m, n + k, v[k]);
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+  }
+  if (p.col_partial) {
+    // lanes with equal (lane % CPR) hold the same 8 columns: reduce over the rest of the wave
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+#pragma unroll
+      for (int o = CPR; o < 64; o <<= 1) csum[k] += __shfl_xor(csum[k], o, 64);
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(smem);  // [group][BN]
+    if (lane < CPR) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) red[grp * BN + wn0 + lane * 8 + k] = csum[k];
+    }
+    __syncthreads();
+    for (int col = threadIdx.x; col < BN; col += 512)
+      if (n0 + col < p.N) p.col_partial[(long)tm * p.N + n0 + col] = red[col] + red[BN + col];
+  }
+}
+
+template <int BN, int NBUF, bool AK, bool BKC, int EPI>
+hipError_t launch_pp(const GemmDev& d, int batch, int split, hipStream_t s) {
+  const int tiles = ((d.M + 255) / 256) * ((d.N + BN - 1) / BN);
+  dim3 grid(tiles, split, batch);
+  hipLaunchKernelGGL((gemm_pp_kernel<BN, NBUF, AK, BKC, EPI>), grid, dim3(512), 0, s, d);
+  return hipGetLastError();
+}
+
 template <int BM, int BN, int BK, int STAGES, int WM, int WN, bool AK, bool BKC, int EPI>
 hipError_t launch_t(const GemmDev& d, int batch, int split, hipStream_t s) {
   const int tiles = ((d.M + BM - 1) / BM) * ((d.N + BN - 1) / BN);
@@ -420,6 +656,8 @@ hipError_t launch_cfg(int cfg, const GemmDev& d, int batch, int split, hipStream
     case 2: return launch_t<256, 128, 64, 3, 4, 2, AK, BKC, EPI>(d, batch, split, s);
     case 3: return launch_t<256, 128, 32, 3, 4, 2, AK, BKC, EPI>(d, batch, split, s);
     case 4: return launch_t<128, 128, 32, 4, 2, 2, AK, BKC, EPI>(d, batch, split, s);
+    case 5: return launch_pp<256, 2, AK, BKC, EPI>(d, batch, split, s);
+    case 6: return launch_pp<128, 3, AK, BKC, EPI>(d, batch, split, s);
     default: return launch_t<128, 128, 64, 2, 2, 2, AK, BKC, EPI>(d, batch, split, s);
   }
 }
@@ -446,7 +684,7 @@ int pick_tile(const vit_gemm_args* a) {
 extern "C" int64_t vit_gemm_tile_rows(const vit_gemm_args* a) {
   if (!a) return 0;
   switch (pick_tile(a)) {
-    case 1: case 2: case 3: return 256;
+    case 1: case 2: case 3: case 5: case 6: return 256;
     default: return 128;
   }
 }
@@ -505,6 +743,18 @@ extern "C" int vit_gemm_bf16(const vit_gemm_args* a, vit_stream_t stream) {
     d.vec = v ? 1 : 0;
   }
   d.col_partial = a->col_partial;
+  {
+    static const int env_gm = [] {
+      const char* e = getenv("VIT_GEMM_GROUP_M");
+      return e ? atoi(e) : 0;
+    }();
+    static const int env_nt = [] {
+      const char* e = getenv("VIT_GEMM_NT");
+      return e ? atoi(e) : 0;
+    }();
+    d.group_m = env_gm;
+    d.nt = env_nt;
+  }
   if (a->col_partial) {
     VIT_CHECK_ARG(a->batch == 1 && a->split_k == 1 && d.vec && a->N % 8 == 0 &&
                       (a->epilogue == VIT_EPI_F32 || a->epilogue == VIT_EPI_BF16 || a->epilogue == VIT_EPI_GELU_BWD ||
@@ -515,7 +765,7 @@ extern "C" int vit_gemm_bf16(const vit_gemm_args* a, vit_stream_t stream) {
   const int batch = (int)a->batch, split = (int)a->split_k;
   hipError_t e;
   const int cfg = pick_tile(a);
-  VIT_CHECK_ARG(cfg >= 0 && cfg <= 4, "vit_gemm_bf16: bad tile config %d", cfg);
+  VIT_CHECK_ARG(cfg >= 0 && cfg <= 6, "vit_gemm_bf16: bad tile config %d", cfg);
   VIT_CHECK_ARG(cfg != 1 || a->K % 32 == 0, "vit_gemm_bf16: K");
   switch (a->epilogue) {
     case VIT_EPI_F32: e = launch_layout<VIT_EPI_F32>(cfg, d, ak, bk, batch, split, s); break;
