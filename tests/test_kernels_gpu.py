@@ -206,7 +206,8 @@ def _attn_ref(qkv, B, N, H, hd):
     return o, lse
 
 
-@pytest.mark.parametrize("B,N,H,hd", [(2, 197, 12, 64), (3, 17, 2, 32), (2, 50, 4, 64), (1, 5, 3, 64), (2, 257, 2, 64)])
+@pytest.mark.parametrize("B,N,H,hd", [(2, 197, 12, 64), (3, 17, 2, 32), (2, 50, 4, 64), (1, 5, 3, 64), (2, 257, 2, 64),
+                                      (2, 257, 3, 80), (1, 197, 2, 48), (2, 33, 2, 96)])
 def test_attention(B, N, H, hd):
     D = H * hd
     qkv = (torch.randn(B * N, 3 * D, device=DEV) * 1.5).bfloat16().requires_grad_(True)

@@ -454,7 +454,9 @@ hipError_t launch_fwd(const bf16_t* qkv, bf16_t* o, float* lse, int B, int N, in
                       hipStream_t s) {
   constexpr int NW = 4;
   const size_t lds = (size_t)2 * NKT * 16 * HD * 2;
-  hipLaunchKernelGGL((attn_fwd_kernel<HD, NKT, NW>), dim3(B * H), dim3(NW * 64), lds, s, qkv, o, lse, N, H, hd, scale);
+  auto kern = attn_fwd_kernel<HD, NKT, NW>;
+  if (lds > 64 * 1024) (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipLaunchKernelGGL(kern, dim3(B * H), dim3(NW * 64), lds, s, qkv, o, lse, N, H, hd, scale);
   return hipGetLastError();
 }
 
@@ -509,9 +511,14 @@ int check_shape(int64_t B, int64_t N, int64_t H, int64_t hd) {
   VIT_CHECK_ARG(B >= 1 && H >= 1 && N >= 1, "attention: bad sizes B=%lld N=%lld H=%lld", (long long)B, (long long)N,
                 (long long)H);
   VIT_CHECK_ARG(N <= 320, "attention: N=%lld > 320 unsupported", (long long)N);
-  VIT_CHECK_ARG(hd == 32 || hd == 64, "attention: head_dim %lld unsupported (32, 64)", (long long)hd);
+  VIT_CHECK_ARG(hd >= 16 && hd <= 96 && hd % 16 == 0, "attention: head_dim %lld unsupported (multiple of 16, <= 96)",
+                (long long)hd);
   return VIT_OK;
 }
+
+// LDS image width: the head dim rounded up to the MFMA k-depth (32): 32, 64 or 96 (hd 80 of ViT-H/14
+// runs on 96-wide images whose last 16 columns are zero).
+int image_width(int64_t hd) { return hd <= 32 ? 32 : hd <= 64 ? 64 : 96; }
 
 }  // namespace
 
@@ -521,10 +528,14 @@ extern "C" int vit_attention_fwd(const void* qkv, void* o, float* lse, int64_t B
   if (st) return st;
   VIT_CHECK_ARG(qkv && o && lse, "vit_attention_fwd: null pointer");
   const int nkt = (int)((N + 31) / 32) * 2;
-  hipError_t e = hd == 64 ? dispatch_fwd<64>(nkt, (const bf16_t*)qkv, (bf16_t*)o, lse, (int)B, (int)N, (int)H, (int)hd,
-                                             scale, (hipStream_t)stream)
-                          : dispatch_fwd<32>(nkt, (const bf16_t*)qkv, (bf16_t*)o, lse, (int)B, (int)N, (int)H, (int)hd,
-                                             scale, (hipStream_t)stream);
+  const bf16_t* q = (const bf16_t*)qkv;
+  hipStream_t s = (hipStream_t)stream;
+  hipError_t e;
+  switch (image_width(hd)) {
+    case 32: e = dispatch_fwd<32>(nkt, q, (bf16_t*)o, lse, (int)B, (int)N, (int)H, (int)hd, scale, s); break;
+    case 64: e = dispatch_fwd<64>(nkt, q, (bf16_t*)o, lse, (int)B, (int)N, (int)H, (int)hd, scale, s); break;
+    default: e = dispatch_fwd<96>(nkt, q, (bf16_t*)o, lse, (int)B, (int)N, (int)H, (int)hd, scale, s); break;
+  }
   return vit::check_hip(e, "vit_attention_fwd launch");
 }
 
@@ -535,12 +546,19 @@ extern "C" int vit_attention_bwd(const void* qkv, const void* o, const void* dou
   if (st) return st;
   VIT_CHECK_ARG(qkv && o && dout && lse && dqkv, "vit_attention_bwd: null pointer");
   const int nkt = (int)((N + 31) / 32) * 2;
-  hipError_t e = hd == 64
-                     ? dispatch_bwd<64>(nkt, (const bf16_t*)qkv, (const bf16_t*)o, (const bf16_t*)dout, lse,
-                                        (bf16_t*)dqkv, bias_partial, (int)B, (int)N, (int)H, (int)hd, scale,
-                                        (hipStream_t)stream)
-                     : dispatch_bwd<32>(nkt, (const bf16_t*)qkv, (const bf16_t*)o, (const bf16_t*)dout, lse,
-                                        (bf16_t*)dqkv, bias_partial, (int)B, (int)N, (int)H, (int)hd, scale,
-                                        (hipStream_t)stream);
+  const bf16_t *q = (const bf16_t*)qkv, *ob = (const bf16_t*)o, *d = (const bf16_t*)dout;
+  hipStream_t s = (hipStream_t)stream;
+  hipError_t e;
+  switch (image_width(hd)) {
+    case 32:
+      e = dispatch_bwd<32>(nkt, q, ob, d, lse, (bf16_t*)dqkv, bias_partial, (int)B, (int)N, (int)H, (int)hd, scale, s);
+      break;
+    case 64:
+      e = dispatch_bwd<64>(nkt, q, ob, d, lse, (bf16_t*)dqkv, bias_partial, (int)B, (int)N, (int)H, (int)hd, scale, s);
+      break;
+    default:
+      e = dispatch_bwd<96>(nkt, q, ob, d, lse, (bf16_t*)dqkv, bias_partial, (int)B, (int)N, (int)H, (int)hd, scale, s);
+      break;
+  }
   return vit::check_hip(e, "vit_attention_bwd launch");
 }

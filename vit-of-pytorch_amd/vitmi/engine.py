@@ -172,8 +172,9 @@ class ViTEngine:
     def __init__(self, cfg: ArchConfig, device="cuda", flat: torch.Tensor | None = None):
         if cfg.emb_dim % cfg.num_heads:
             raise ValueError("emb_dim must be divisible by num_heads")
-        if cfg.head_dim not in (32, 64):
-            raise NotImplementedError(f"head_dim {cfg.head_dim} not supported by the HIP attention kernel yet")
+        if cfg.head_dim % 16 or cfg.head_dim > 96:
+            raise NotImplementedError(f"head_dim {cfg.head_dim} not supported by the HIP attention kernel "
+                                      "(multiples of 16 up to 96)")
         if cfg.emb_dim % 64 or cfg.mlp_dim % 64:
             raise NotImplementedError("emb_dim and mlp_dim must be multiples of 64")
         if cfg.tokens > 320:
