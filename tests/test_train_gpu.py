@@ -68,11 +68,12 @@ if rank == 0:
     assert rel < 1e-3, rel
 dist.barrier()
 dist.destroy_process_group()
-print("rank", rank, "ok")
+open(os.path.join(os.environ["OUTDIR"], f"rank{rank}.ok"), "w").write("ok")
 ''')
-    env = dict(os.environ, REPO=REPO, MASTER_ADDR="127.0.0.1", MASTER_PORT="29533")
+    env = dict(os.environ, REPO=REPO, OUTDIR=str(tmp_path), MASTER_ADDR="127.0.0.1", MASTER_PORT="29533")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr", "127.0.0.1", "--master-port", "29533", str(script)]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
-    assert "rank 0 ok" in r.stdout and "rank 1 ok" in r.stdout
+    # (the ranks' stdout interleaves: each rank leaves a marker file instead)
+    assert (tmp_path / "rank0.ok").exists() and (tmp_path / "rank1.ok").exists()

@@ -1,2 +1,3 @@
-for sh in sq8k sq4k fc1k4; do for t in 3 5 6; do VIT_GEMM_GROUP_M=8 timeout -k 10 60 python tools/gemm_one.py $sh $t 1 || exit 1; done; done
-VIT_GEMM_GROUP_M=8 bash tools/gemm_pmc.sh sq8k 5 1
+set -e
+timeout -k 10 400 python -u tools/gemm_bench.py --tiles 3,5 --shapes fc1:3,fc2:4,qkv:2,out:4,fc2dg:5,fc1dg:1,qkvdg:1,out:1 --rounds 2 --wgrad --splits 4,7,9,16,28 > gpurun_out/gemm_epi.log 2>&1
+cat gpurun_out/gemm_epi.log

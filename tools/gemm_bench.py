@@ -18,7 +18,8 @@ sys.path.insert(0, os.path.join(REPO, "vit-of-pytorch_amd"))
 import torch  # noqa: E402
 
 from vitmi import ops  # noqa: E402
-from vitmi._lib import EPI_BF16, EPI_BIAS_GELU, EPI_GELU_BWD, EPI_SPLITK, K_CONTIG, MN_CONTIG  # noqa: E402
+from vitmi._lib import (EPI_BF16, EPI_BIAS_BF16, EPI_BIAS_GELU, EPI_BIAS_RESID_F32, EPI_GELU_BWD, EPI_SPLITK,  # noqa: E402
+                        K_CONTIG, MN_CONTIG)
 
 
 def bench(fn, iters=20):
@@ -58,9 +59,11 @@ def main():
     tiles = [int(t) for t in args.tiles.split(",")]
     epis = [int(e) for e in args.epis.split(",")]
     SH = shapes(args.T, args.D, args.M)
-    for name in args.shapes.split(","):
-        if not name:
+    for spec in args.shapes.split(","):
+        if not spec:
             continue
+        name, _, e = spec.partition(":")
+        shape_epis = [int(x) for x in e.split("/")] if e else epis
         M, N, K, al, bl = SH[name]
         A = (torch.rand(M, K, device=dev) * 2 - 1).bfloat16()
         B = ((torch.rand(N, K, device=dev) if bl == K_CONTIG else torch.rand(K, N, device=dev)) * 2 - 1).bfloat16()
@@ -68,18 +71,25 @@ def main():
         C = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
         C2 = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
         U = torch.randn(M, N, device=dev).bfloat16()
+        Cf = torch.randn(M, N, device=dev)
         bias = torch.randn(N, device=dev)
         flop = 2.0 * M * N * K
         variants = []
         for tile in tiles:
-            for epi in epis:
+            for epi in shape_epis:
                 extra = {}
-                if epi == EPI_BIAS_GELU:
+                out = C
+                if epi == EPI_BIAS_BF16:
+                    extra = dict(bias=bias)
+                elif epi == EPI_BIAS_RESID_F32:
+                    extra = dict(bias=bias, aux=Cf, ldaux=N)
+                    out = Cf
+                elif epi == EPI_BIAS_GELU:
                     extra = dict(bias=bias, C2=C2, ldc2=N)
                 elif epi == EPI_GELU_BWD:
                     extra = dict(aux=U, ldaux=N)
-                fn = (lambda tile=tile, epi=epi, extra=extra:
-                      ops.gemm(A, B, C, M, N, K, a_layout=al, b_layout=bl, lda=K, ldb=ldb, ldc=N, epilogue=epi,
+                fn = (lambda tile=tile, epi=epi, extra=extra, out=out:
+                      ops.gemm(A, B, out, M, N, K, a_layout=al, b_layout=bl, lda=K, ldb=ldb, ldc=N, epilogue=epi,
                                tile=tile, **extra))
                 variants.append((f"tile={tile} epi={epi}", fn))
         if args.blas:
@@ -109,13 +119,18 @@ def main():
             for tile in tiles:
                 for S in [int(s) for s in args.splits.split(",")]:
                     ws = torch.empty(S, M, N, device=dev)
+                    outw = torch.empty(M, N, device=dev)
+
+                    def run(S=S, tile=tile, ws=ws, outw=outw):
+                        ops.gemm(A, B, ws, M, N, K, a_layout=MN_CONTIG, b_layout=MN_CONTIG, lda=M, ldb=N, ldc=N,
+                                 epilogue=EPI_SPLITK, split_k=S, tile=tile)
+                        ops.splitk_reduce(ws, 1, S, M, N, outw, N)
                     try:
-                        us = bench(lambda: ops.gemm(A, B, ws, M, N, K, a_layout=MN_CONTIG, b_layout=MN_CONTIG, lda=M,
-                                                    ldb=N, ldc=N, epilogue=EPI_SPLITK, split_k=S, tile=tile))
+                        us = bench(run)
                     except Exception as ex:  # noqa: BLE001
                         print(name, tile, S, "ERR", ex, flush=True)
                         continue
-                    print(f"{name:10s} M={M} N={N} K={K} tile={tile} S={S}: {us:8.1f} us  {flop / us / 1e6:7.1f} TF/s",
+                    print(f"{name:10s} M={M} N={N} K={K} tile={tile} S={S} (+reduce): {us:8.1f} us  {flop / us / 1e6:7.1f} TF/s",
                           flush=True)
             if args.blas:
                 us = bench(lambda: torch.matmul(A.t(), B))

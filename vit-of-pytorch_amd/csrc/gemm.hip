@@ -672,10 +672,21 @@ hipError_t launch_layout(int cfg, const GemmDev& d, bool ak, bool bk, int batch,
 
 int pick_tile(const vit_gemm_args* a) {
   if (a->tile > 0) return (int)a->tile;
-  // measured on MI355X (tools/gemm_bench.py): 256x128x32 with 2 resident workgroups per CU is the
-  // fastest or within 4% for every ViT-B/16 shape (fwd, dgrad, split-K wgrad); 128x128 for small M
-  if (a->M >= 1024 && a->N >= 256) return 3;
-  if (a->epilogue == VIT_EPI_SPLITK && a->M >= 256 && a->N >= 256) return 3;
+  // measured on MI355X (tools/gemm_bench.py, ViT-B/16 bs256 shapes, profiles/r01/gemm_*):
+  //  * split-K weight gradients: the 256x256 ping-pong kernel with the split sized to one wave
+  //    (fc1/fc2 wgrad 244 us vs 340 us for 256x128 at split 16);
+  //  * wide outputs (N >= 2048: fc1 fwd, qkv fwd) and long-K MN-contiguous-B dgrads (fc1 dgrad):
+  //    ping-pong; the GELU-backward epilogue (fc2 dgrad) and the N = 768 K-contiguous-B shapes
+  //    are faster on 256x128x32 with 2 resident workgroups per CU (one's epilogue under the
+  //    other's MFMAs);
+  //  * 128x128 for small problems.
+  const bool bk = a->b_layout == VIT_K_CONTIG;
+  if (a->epilogue == VIT_EPI_SPLITK && a->M >= 256 && a->N >= 256) return 5;
+  if (a->M >= 1024 && a->N >= 256) {
+    if (a->N >= 2048 && a->epilogue != VIT_EPI_GELU_BWD) return 5;
+    if (!bk && a->K >= 3072) return 5;
+    return 3;
+  }
   return 0;
 }
 
