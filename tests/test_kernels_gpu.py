@@ -61,7 +61,9 @@ def test_gemm_exact_integers(al, bl, M, N, K):
 @pytest.mark.parametrize("al,bl", LAYOUTS)
 @pytest.mark.parametrize("tile,M,N,K", [(1, 600, 520, 128), (2, 600, 300, 192), (0, 300, 200, 128), (1, 2100, 1600, 64),
                                         (2, 2100, 768, 128), (6, 600, 520, 128), (6, 2100, 768, 64),
-                                        (6, 700, 300, 320), (5, 600, 520, 192)])
+                                        (6, 700, 300, 320), (5, 600, 520, 192), (7, 600, 520, 192),
+                                        (8, 2100, 768, 320), (7, 300, 256, 64), (9, 600, 520, 192),
+                                        (9, 2100, 768, 320), (9, 300, 256, 64), (9, 513, 300, 128)])
 def test_gemm_tiles_exact(al, bl, tile, M, N, K):
     A, B, Am, Bm, lda, ldb = _mats(M, N, K, al, bl, ints=True)
     C = torch.full((M, N), float("nan"), device=DEV)
@@ -69,7 +71,7 @@ def test_gemm_tiles_exact(al, bl, tile, M, N, K):
     assert torch.equal(C, A.float() @ B.float())
 
 
-@pytest.mark.parametrize("tile", [0, 3, 6])
+@pytest.mark.parametrize("tile", [0, 3, 6, 9])
 def test_gemm_col_partial(tile):
     M, N, K = 1000, 384, 256
     A, B, Am, Bm, lda, ldb = _mats(M, N, K, K_CONTIG, MN_CONTIG)
@@ -86,7 +88,7 @@ def test_gemm_col_partial(tile):
     assert rel(C.float(), gref) < 5e-3
 
 
-@pytest.mark.parametrize("tile", [1, 2, 6])
+@pytest.mark.parametrize("tile", [1, 2, 6, 9])
 def test_gemm_tiles_epilogue_splitk(tile):
     M, N, K = 700, 520, 512
     A, B, Am, Bm, lda, ldb = _mats(M, N, K, K_CONTIG, MN_CONTIG)

@@ -20,6 +20,7 @@
 namespace {
 
 constexpr float LOG2E = 1.4426950408889634f;
+typedef unsigned v4u __attribute__((ext_vector_type(4)));
 
 template <int HD>
 __device__ __forceinline__ int aswz(int row) {
@@ -32,17 +33,37 @@ __device__ __forceinline__ int img_off(int row, int chunk) {
   return row * HD * 2 + ((chunk ^ aswz<HD>(row)) << 4);
 }
 
-// Load rows [0, NP) x [0, HD) of a strided bf16 matrix into a swizzled LDS image (zero padded).
-template <int HD>
-__device__ __forceinline__ void load_image(char* img, const bf16_t* __restrict__ src, long row_stride, int N, int hd,
-                                           int NP) {
+// Load rows [0, NP) x [0, HD) of two strided bf16 matrices into swizzled LDS images (zero padded).
+// Every load of the thread is issued before the first LDS write (one HBM latency per image pair
+// instead of one per 16-B chunk): buffer loads against a descriptor that covers the valid rows, so
+// padding rows / columns >= hd read as zero without a branch around the load.
+template <int HD, int NP, int NT>
+__device__ __forceinline__ void load_images(char* imgA, const bf16_t* srcA, long strideA, char* imgB,
+                                            const bf16_t* srcB, long strideB, int N, int hd) {
   constexpr int CPR = HD / 8;
-  const int total = NP * CPR;
-  for (int c = threadIdx.x; c < total; c += blockDim.x) {
+  constexpr int TOTAL = NP * CPR;
+  constexpr int PER = (TOTAL + NT - 1) / NT;
+  const __amdgpu_buffer_rsrc_t ra = make_rsrc(srcA, (uint32_t)(((long)(N - 1) * strideA + hd) * 2));
+  const __amdgpu_buffer_rsrc_t rb = make_rsrc(srcB, (uint32_t)(((long)(N - 1) * strideB + hd) * 2));
+  v4u a[PER], b[PER];
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const int c = threadIdx.x + k * NT;
     const int row = c / CPR, ch = c % CPR;
-    v8s v = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (row < N && ch * 8 < hd) v = *reinterpret_cast<const v8s*>(src + (long)row * row_stride + ch * 8);
-    *reinterpret_cast<v8s*>(img + img_off<HD>(row, ch)) = v;
+    const bool ok = c < TOTAL && row < N && ch * 8 < hd;
+    const int offa = ok ? (int)(((long)row * strideA + ch * 8) * 2) : 0x7ffffff0;
+    const int offb = ok ? (int)(((long)row * strideB + ch * 8) * 2) : 0x7ffffff0;
+    a[k] = __builtin_amdgcn_raw_buffer_load_b128(ra, offa, 0, 0);
+    b[k] = __builtin_amdgcn_raw_buffer_load_b128(rb, offb, 0, 0);
+  }
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const int c = threadIdx.x + k * NT;
+    if (c < TOTAL) {
+      const int row = c / CPR, ch = c % CPR;
+      *reinterpret_cast<v4u*>(imgA + img_off<HD>(row, ch)) = a[k];
+      *reinterpret_cast<v4u*>(imgB + img_off<HD>(row, ch)) = b[k];
+    }
   }
 }
 
@@ -100,8 +121,7 @@ __global__ void __launch_bounds__(NW * 64) attn_fwd_kernel(const bf16_t* __restr
   const int D = H * hd;
   const long rs = 3L * D;
   const bf16_t* base = qkv + (long)b * N * rs + (long)h * hd;
-  load_image<HD>(Ki, base + D, rs, N, hd, NP);
-  load_image<HD>(Vi, base + 2 * D, rs, N, hd, NP);
+  load_images<HD, NP, NW * 64>(Ki, base + D, rs, Vi, base + 2 * D, rs, N, hd);
   __syncthreads();
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -217,8 +237,7 @@ __global__ void __launch_bounds__(NW * 64, 2) attn_bwd_kernel(const bf16_t* __re
   const bf16_t* dob = dout + (long)b * N * D + (long)h * hd;
   bf16_t* dq_base = dqkv + (long)b * N * rs + (long)h * hd;
 
-  load_image<HD>(ImA, base + D, rs, N, hd, NP);
-  load_image<HD>(ImB, base + 2 * D, rs, N, hd, NP);
+  load_images<HD, NP, NW * 64>(ImA, base + D, rs, ImB, base + 2 * D, rs, N, hd);
   for (int r = threadIdx.x; r < NP; r += blockDim.x) lse_s[r] = r < N ? lse[(long)bh * N + r] * LOG2E : INFINITY;
   __syncthreads();
 
@@ -338,8 +357,7 @@ __global__ void __launch_bounds__(NW * 64, 2) attn_bwd_kernel(const bf16_t* __re
   __syncthreads();  // K / V images no longer read; delta complete
 
   // ---- stage 2: dK and dV, key-tile pairs ----
-  load_image<HD>(ImA, base, rs, N, hd, NP);   // Q
-  load_image<HD>(ImB, dob, D, N, hd, NP);     // dO
+  load_images<HD, NP, NW * 64>(ImA, base, rs, ImB, dob, D, N, hd);  // Q, dO
   __syncthreads();
   for (int kp = wave; kp < npair; kp += NW) {
     v8bf kf[2][HD / 32], vf[2][HD / 32];

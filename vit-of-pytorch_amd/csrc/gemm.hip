@@ -77,7 +77,7 @@ __device__ __forceinline__ int swz_mn(int row) { return (row & 3) | (((row >> 3)
 // Issue the LDS-DMA of one operand k-tile (ROWS rows of the M/N dim x BK k) to byte offset lds_off.
 template <int ROWS, int BK, bool KC, int NWAVE>
 __device__ __forceinline__ void stage_tile(char* smem, int lds_off, __amdgpu_buffer_rsrc_t rs, long ld, int kt,
-                                           int wave, int lane) {
+                                           int wave, int lane, int vbase = 0) {
   constexpr int BYTES = ROWS * BK * 2;
   constexpr int INSTR = BYTES / 1024 / NWAVE;
   static_assert(INSTR * 1024 * NWAVE == BYTES, "tile must split evenly over waves");
@@ -97,7 +97,8 @@ __device__ __forceinline__ void stage_tile(char* smem, int lds_off, __amdgpu_buf
       const int lb = (pc * 16) ^ (swz_mn(r) << 5);
       voff = (int)((long)(kt * BK + r) * ld * 2) + lb;
     }
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, LDS_PTR(void, smem + lds_off + piece * 1024), 16, voff, 0, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, LDS_PTR(void, smem + lds_off + piece * 1024), 16, vbase + voff, 0, 0,
+                                             0);
   }
 }
 
@@ -440,9 +441,42 @@ __global__ void __launch_bounds__(WM* WN * 64, (gemm_min_waves<BM, BN, BK, STAGE
 // is waited for at the end of the following slot, before group 0 first reads it: two slots of flight,
 // raw s_barrier (no vmcnt(0) drain at the barriers in between).
 // Epilogue: wave-private fp32 staging in the then idle LDS (32 rows per pass), 8-column chunks.
-template <int BN, int NBUF, bool AK, bool BKC, int EPI>
+// Outstanding-DMA wait with a runtime count of younger k-tiles (0 .. L-1) and compile-time vmcnt.
+template <int LPT, int L>
+__device__ __forceinline__ void wait_tiles(int younger) {
+  if constexpr (L >= 4) {
+    if (younger >= 3) { wait_vm<3 * LPT>(); return; }
+  }
+  if constexpr (L >= 3) {
+    if (younger == 2) { wait_vm<2 * LPT>(); return; }
+  }
+  if constexpr (L >= 2) {
+    if (younger == 1) { wait_vm<LPT>(); return; }
+  }
+  wait_vm<0>();
+}
+
+#ifdef VIT_GEMM_STAMPS
+// Diagnostic build only (tools/gemm_diag.hip): s_memtime stamps of waves 0 and 4 of one workgroup,
+// kept in spare LDS (no vmcnt traffic inside the loop) and copied out at the end.
+__device__ int g_stamp_wg = -1;
+__device__ unsigned long long g_stamps[2][1024];
+#define PP_STAMP()                                                                        \
+  do {                                                                                    \
+    if (stamp_on && si < 1024) st_lds[si] = __builtin_amdgcn_s_memtime();                 \
+    ++si;                                                                                 \
+  } while (0)
+constexpr int PP_STAMP_LDS = 16 * 1024;  // dropped (no stamps) where the pipeline leaves no room
+#else
+#define PP_STAMP() \
+  do {             \
+  } while (0)
+constexpr int PP_STAMP_LDS = 0;
+#endif
+
+template <int BN, int BK, int NBUF, bool AK, bool BKC, int EPI>
 __global__ void __launch_bounds__(512) gemm_pp_kernel(const GemmDev p) {
-  constexpr int BM = 256, BK = 64, NWAVE = 8;
+  constexpr int BM = 256, NWAVE = 8, KK = BK / 32;
   constexpr int TN = BN / 4, FM = 8, FN = TN / 16;
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
   constexpr int LPT = STAGE / 1024 / NWAVE;  // DMA instructions per wave per k-tile
@@ -450,13 +484,21 @@ __global__ void __launch_bounds__(512) gemm_pp_kernel(const GemmDev p) {
   constexpr int PR = 32;                     // staged rows per pass (4 passes over the wave's 128 rows)
   constexpr int WST = PR * LDW * 4;          // staging bytes per wave
   static_assert(NWAVE * WST <= NBUF * STAGE, "staging must fit in the pipeline buffers");
-  static_assert(NBUF == 2 || NBUF == 3, "k-tile buffers");
+  static_assert(NBUF >= 2 && NBUF <= 5, "k-tile buffers");
+  static_assert(BK == 32 || BK == 64, "k-tile depth");
+  constexpr int STL = NBUF * STAGE + PP_STAMP_LDS <= 160 * 1024 ? PP_STAMP_LDS : 0;
   static_assert(NBUF * STAGE <= 160 * 1024, "LDS budget");
-  __shared__ __attribute__((aligned(16))) char smem[NBUF * STAGE];
+  __shared__ __attribute__((aligned(16))) char smem[NBUF * STAGE + STL];
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int grp = wave >> 2, wn = wave & 3;
+#ifdef VIT_GEMM_STAMPS
+  const bool stamp_on = STL > 0 && (int)blockIdx.x == g_stamp_wg && blockIdx.y == 0 && wn == 0 && lane == 0;
+  unsigned long long* st_lds = reinterpret_cast<unsigned long long*>(smem + NBUF * STAGE) + grp * 1024;
+  int si = 0;
+  PP_STAMP();
+#endif
 
   const int tiles_m = (p.M + BM - 1) / BM, tiles_n = (p.N + BN - 1) / BN;
   const int nwg = tiles_m * tiles_n;
@@ -488,7 +530,7 @@ __global__ void __launch_bounds__(512) gemm_pp_kernel(const GemmDev p) {
   for (int i = 0; i < FM; ++i)
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
-  v8s af[2][FM], bfr[2][FN];
+  v8s af[KK][FM], bfr[KK][FN];
   const int wm0 = grp * 128, wn0 = wn * TN;
 
   auto issue = [&](int t) {
@@ -499,7 +541,7 @@ __global__ void __launch_bounds__(512) gemm_pp_kernel(const GemmDev p) {
   auto mem = [&](int j) {
     const int cur = (j % NBUF) * STAGE;
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
+    for (int kk = 0; kk < KK; ++kk) {
 #pragma unroll
       for (int jn = 0; jn < FN; ++jn) bfr[kk][jn] = read_frag<BN, BK, BKC>(smem, cur + A_BYTES, wn0 + jn * 16, kk, lane);
 #pragma unroll
@@ -509,7 +551,7 @@ __global__ void __launch_bounds__(512) gemm_pp_kernel(const GemmDev p) {
   };
   auto compute = [&]() {
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
+    for (int kk = 0; kk < KK; ++kk)
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -523,10 +565,7 @@ __global__ void __launch_bounds__(512) gemm_pp_kernel(const GemmDev p) {
 #pragma unroll
   for (int t = 0; t < L; ++t)
     if (t < nk) issue(t);
-  if (L == 2 && nk > 1)
-    wait_vm<LPT>();
-  else
-    wait_vm<0>();
+  wait_tiles<LPT, L>((nk < L ? nk : L) - 1);
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
 
@@ -538,10 +577,7 @@ __global__ void __launch_bounds__(512) gemm_pp_kernel(const GemmDev p) {
   auto end_odd = [&](int u) {  // end of slot 2u+1
     const int issued = u + L < nk ? u + L : nk - 1;
     __builtin_amdgcn_sched_barrier(0);
-    if (L == 2 && issued >= u + 2)
-      wait_vm<LPT>();
-    else
-      wait_vm<0>();
+    wait_tiles<LPT, L>(issued - u - 1);
     asm volatile("s_barrier" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
   };
@@ -550,28 +586,37 @@ __global__ void __launch_bounds__(512) gemm_pp_kernel(const GemmDev p) {
     asm volatile("s_barrier" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
   };
+  PP_STAMP();
   if (grp == 0) {
     for (int j = 0; j < nk; ++j) {
       if (j + L < nk) issue(j + L);  // slot 2j
       mem(j);
+      PP_STAMP();
       end_even();
+      PP_STAMP();
       compute();  // slot 2j+1
       end_odd(j);
+      PP_STAMP();
     }
   } else if (nk > 0) {
     if (L < nk) issue(L);  // slot 0
     end_even();
+    PP_STAMP();
     for (int j = 0; j < nk - 1; ++j) {
       mem(j);  // slot 2j+1
+      PP_STAMP();
       end_odd(j);
+      PP_STAMP();
       if (j + 1 + L < nk) issue(j + 1 + L);  // slot 2j+2
       compute();
       end_even();
+      PP_STAMP();
     }
     mem(nk - 1);  // slot 2nk-1
     end_odd(nk - 1);
     compute();  // slot 2nk: LDS is free from here on
   }
+  PP_STAMP();
 
   // ---- epilogue ----
   const int g = lane >> 4, c = lane & 15;
@@ -625,13 +670,22 @@ __global__ void __launch_bounds__(512) gemm_pp_kernel(const GemmDev p) {
     for (int col = threadIdx.x; col < BN; col += 512)
       if (n0 + col < p.N) p.col_partial[(long)tm * p.N + n0 + col] = red[col] + red[BN + col];
   }
+#ifdef VIT_GEMM_STAMPS
+  PP_STAMP();
+  if (stamp_on) {
+    for (int k = 0; k < si && k < 1024; ++k) g_stamps[grp][k] = st_lds[k];
+    if (si < 1024) g_stamps[grp][si] = 0;
+  }
+#endif
 }
 
-template <int BN, int NBUF, bool AK, bool BKC, int EPI>
+#include "gemm_pp2.inc"
+
+template <int BN, int BK, int NBUF, bool AK, bool BKC, int EPI>
 hipError_t launch_pp(const GemmDev& d, int batch, int split, hipStream_t s) {
   const int tiles = ((d.M + 255) / 256) * ((d.N + BN - 1) / BN);
   dim3 grid(tiles, split, batch);
-  hipLaunchKernelGGL((gemm_pp_kernel<BN, NBUF, AK, BKC, EPI>), grid, dim3(512), 0, s, d);
+  hipLaunchKernelGGL((gemm_pp_kernel<BN, BK, NBUF, AK, BKC, EPI>), grid, dim3(512), 0, s, d);
   return hipGetLastError();
 }
 
@@ -656,8 +710,11 @@ hipError_t launch_cfg(int cfg, const GemmDev& d, int batch, int split, hipStream
     case 2: return launch_t<256, 128, 64, 3, 4, 2, AK, BKC, EPI>(d, batch, split, s);
     case 3: return launch_t<256, 128, 32, 3, 4, 2, AK, BKC, EPI>(d, batch, split, s);
     case 4: return launch_t<128, 128, 32, 4, 2, 2, AK, BKC, EPI>(d, batch, split, s);
-    case 5: return launch_pp<256, 2, AK, BKC, EPI>(d, batch, split, s);
-    case 6: return launch_pp<128, 3, AK, BKC, EPI>(d, batch, split, s);
+    case 5: return launch_pp<256, 64, 2, AK, BKC, EPI>(d, batch, split, s);
+    case 6: return launch_pp<128, 64, 3, AK, BKC, EPI>(d, batch, split, s);
+    case 7: return launch_pp<256, 32, 4, AK, BKC, EPI>(d, batch, split, s);
+    case 8: return launch_pp<256, 32, 5, AK, BKC, EPI>(d, batch, split, s);
+    case 9: return launch_pp2<AK, BKC, EPI>(d, batch, split, s);
     default: return launch_t<128, 128, 64, 2, 2, 2, AK, BKC, EPI>(d, batch, split, s);
   }
 }
@@ -680,9 +737,13 @@ int pick_tile(const vit_gemm_args* a) {
   //    are faster on 256x128x32 with 2 resident workgroups per CU (one's epilogue under the
   //    other's MFMAs);
   //  * 128x128 for small problems.
-  const bool bk = a->b_layout == VIT_K_CONTIG;
+  //  * both operands K-contiguous (fc1 / fc2 fwd, qkv and out-proj dgrad): the half-tile scheduled
+  //    ping-pong (fc2 fwd 260 vs 309 us, qkv dgrad 167 vs 195 us); with an M/N-contiguous operand
+  //    it loses to the plain ping-pong, so those keep config 5 / 3.
+  const bool ak = a->a_layout == VIT_K_CONTIG, bk = a->b_layout == VIT_K_CONTIG;
   if (a->epilogue == VIT_EPI_SPLITK && a->M >= 256 && a->N >= 256) return 5;
   if (a->M >= 1024 && a->N >= 256) {
+    if (ak && bk && a->K >= 512) return 9;
     if (a->N >= 2048 && a->epilogue != VIT_EPI_GELU_BWD) return 5;
     if (!bk && a->K >= 3072) return 5;
     return 3;
@@ -695,7 +756,7 @@ int pick_tile(const vit_gemm_args* a) {
 extern "C" int64_t vit_gemm_tile_rows(const vit_gemm_args* a) {
   if (!a) return 0;
   switch (pick_tile(a)) {
-    case 1: case 2: case 3: case 5: case 6: return 256;
+    case 1: case 2: case 3: case 5: case 6: case 7: case 8: case 9: return 256;
     default: return 128;
   }
 }
@@ -776,7 +837,7 @@ extern "C" int vit_gemm_bf16(const vit_gemm_args* a, vit_stream_t stream) {
   const int batch = (int)a->batch, split = (int)a->split_k;
   hipError_t e;
   const int cfg = pick_tile(a);
-  VIT_CHECK_ARG(cfg >= 0 && cfg <= 6, "vit_gemm_bf16: bad tile config %d", cfg);
+  VIT_CHECK_ARG(cfg >= 0 && cfg <= 9, "vit_gemm_bf16: bad tile config %d", cfg);
   VIT_CHECK_ARG(cfg != 1 || a->K % 32 == 0, "vit_gemm_bf16: K");
   switch (a->epilogue) {
     case VIT_EPI_F32: e = launch_layout<VIT_EPI_F32>(cfg, d, ak, bk, batch, split, s); break;
