@@ -188,6 +188,11 @@ int vit_cast_pad_rows(const float* in, int64_t rows, int64_t cols, void* out, in
  * Packs q/k/v LinearGeneral weights [D][H,hd] (src/model.py:73-75) into one [D][3D] operand. */
 int vit_pack_cols(const float* in, int64_t zstride, int64_t ldi, int64_t rows, int64_t cols, int64_t Z,
                   void* out, int64_t ldo, int32_t out_bf16, vit_stream_t stream);
+/* out bf16 [cols][ldo] <- transpose of in f32 [rows][ldi]: out[c*ldo + r] = bf16(in[r*ldi + c]).
+ * K-contiguous weight copies for the dgrad / projection GEMMs (fc1/fc2 weights src/model.py:31-32,
+ * LinearGeneral q/k/v/out src/model.py:73-76). */
+int vit_transpose_f32_bf16(const float* in, int64_t rows, int64_t cols, int64_t ldi, void* out, int64_t ldo,
+                           vit_stream_t stream);
 /* y = a*x + b*y (f32), used for gradient scaling / accumulation. */
 int vit_axpby(const float* x, float* y, int64_t n, float a, float b, vit_stream_t stream);
 

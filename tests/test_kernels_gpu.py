@@ -316,3 +316,11 @@ def test_colsum_ce_gemm_f32_sgd():
     ops.sgd_step(p, g, buf, pb, n, 0.1, 0.9, 1e-2, False)
     d2 = 0.9 * d + g + 1e-2 * p1
     assert rel(p, p1 - 0.1 * d2) < 1e-6
+
+
+@pytest.mark.parametrize("rows,cols", [(768, 3072), (3072, 768), (100, 70), (64, 64)])
+def test_transpose_bf16(rows, cols):
+    x = torch.randn(rows, cols + 5, device=DEV)
+    out = torch.full((cols, rows + 3), float("nan"), device=DEV).bfloat16()
+    ops.transpose_bf16(x, rows, cols, cols + 5, out, rows + 3)
+    assert torch.equal(out[:, :rows], x[:, :cols].t().bfloat16())

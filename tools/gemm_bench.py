@@ -39,7 +39,10 @@ def shapes(T, D, M):
     return {"fc1": (T, M, D, K_CONTIG, K_CONTIG), "fc2": (T, D, M, K_CONTIG, K_CONTIG),
             "qkv": (T, 3 * D, D, K_CONTIG, MN_CONTIG), "out": (T, D, D, K_CONTIG, MN_CONTIG),
             "fc2dg": (T, M, D, K_CONTIG, MN_CONTIG), "fc1dg": (T, D, M, K_CONTIG, MN_CONTIG),
-            "qkvdg": (T, D, 3 * D, K_CONTIG, K_CONTIG), "sq8k": (8192, 8192, 8192, K_CONTIG, K_CONTIG)}
+            "qkvdg": (T, D, 3 * D, K_CONTIG, K_CONTIG), "sq8k": (8192, 8192, 8192, K_CONTIG, K_CONTIG),
+            # the same GEMMs on K-contiguous (transposed) weight copies
+            "qkvk": (T, 3 * D, D, K_CONTIG, K_CONTIG), "outk": (T, D, D, K_CONTIG, K_CONTIG),
+            "fc2dgk": (T, M, D, K_CONTIG, K_CONTIG), "fc1dgk": (T, D, M, K_CONTIG, K_CONTIG)}
 
 
 def main():

@@ -389,3 +389,37 @@ extern "C" int vit_pack_cols(const float* in, int64_t zstride, int64_t ldi, int6
                        (long)zstride, (long)ldi, (int)rows, (int)cols, (int)Z, out, (long)ldo);
   VIT_LAUNCH_CHECK("vit_pack_cols");
 }
+
+// ---- transposed bf16 weight copies: out[c*ldo + r] = bf16(in[r*ldi + c]) ---------------------------
+// Keeps a K-contiguous copy of every weight whose natural layout would make a GEMM operand
+// M/N-contiguous (fc1 / fc2 dgrad, out-proj and fused-QKV forward), so every forward and dgrad GEMM
+// runs on the both-K-contiguous ping-pong kernel. 64 x 64 tiles through LDS, coalesced both ways.
+namespace {
+__global__ void __launch_bounds__(256) transpose_f32_bf16_kernel(const float* __restrict__ in, long ldi, int rows,
+                                                                 int cols, bf16_t* __restrict__ out, long ldo) {
+  __shared__ float tile[64][65];
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int c0 = blockIdx.x * 64, r0 = blockIdx.y * 64;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int r = r0 + ty + 4 * k, c = c0 + tx;
+    tile[ty + 4 * k][tx] = (r < rows && c < cols) ? in[(long)r * ldi + c] : 0.f;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int c = c0 + ty + 4 * k, r = r0 + tx;  // output row c, column r
+    if (c < cols && r < rows) out[(long)c * ldo + r] = f2bf(tile[tx][ty + 4 * k]);
+  }
+}
+}  // namespace
+
+extern "C" int vit_transpose_f32_bf16(const float* in, int64_t rows, int64_t cols, int64_t ldi, void* out,
+                                      int64_t ldo, vit_stream_t stream) {
+  VIT_CHECK_ARG(in && out && rows >= 0 && cols >= 0 && ldi >= cols && ldo >= rows, "vit_transpose_f32_bf16: bad args");
+  if (rows == 0 || cols == 0) return VIT_OK;
+  dim3 grid((unsigned)((cols + 63) / 64), (unsigned)((rows + 63) / 64));
+  hipLaunchKernelGGL(transpose_f32_bf16_kernel, grid, dim3(256), 0, (hipStream_t)stream, in, (long)ldi, (int)rows,
+                     (int)cols, (bf16_t*)out, (long)ldo);
+  VIT_LAUNCH_CHECK("vit_transpose_f32_bf16");
+}

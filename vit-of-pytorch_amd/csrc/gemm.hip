@@ -75,30 +75,39 @@ __device__ __forceinline__ int swz_k(int row) {
 __device__ __forceinline__ int swz_mn(int row) { return (row & 3) | (((row >> 3) & 1) << 2); }
 
 // Issue the LDS-DMA of one operand k-tile (ROWS rows of the M/N dim x BK k) to byte offset lds_off.
+// Instruction i of a wave covers image rows advanced by a multiple of the swizzle period (16) from
+// instruction 0, so its per-lane source offset is instruction 0's plus a wave-uniform step: one
+// lane-offset VGPR per call instead of one per instruction (the per-instruction offsets of the four
+// half-image loads of gemm_pp2_kernel spilled to scratch, and hipcc waited vmcnt(0) on every reload).
 template <int ROWS, int BK, bool KC, int NWAVE>
 __device__ __forceinline__ void stage_tile(char* smem, int lds_off, __amdgpu_buffer_rsrc_t rs, long ld, int kt,
                                            int wave, int lane, int vbase = 0) {
   constexpr int BYTES = ROWS * BK * 2;
   constexpr int INSTR = BYTES / 1024 / NWAVE;
   static_assert(INSTR * 1024 * NWAVE == BYTES, "tile must split evenly over waves");
+  constexpr int CPR = KC ? BK / 8 : ROWS * 2 / 16;  // 16-B chunks per image row
+  constexpr int RSTEP = NWAVE * 64 / CPR;             // image rows between a wave's instructions
+  static_assert(RSTEP % 16 == 0, "swizzle must repeat between a wave's instructions");
+  const int c = wave * 64 + lane;  // chunk of instruction 0
+  const int r = c / CPR, pc = c % CPR;
+  int lane_off, step, base;
+  if constexpr (KC) {
+    const int lc = pc ^ swz_k<BK>(r);
+    lane_off = (int)(r * ld * 2) + lc * 16;
+    step = (int)(RSTEP * ld * 2);
+    base = kt * BK * 2 + vbase;
+  } else {
+    lane_off = (int)(r * ld * 2) + ((pc * 16) ^ (swz_mn(r) << 5));
+    step = (int)(RSTEP * ld * 2);
+    base = (int)((long)kt * BK * ld * 2) + vbase;
+  }
+  base = __builtin_amdgcn_readfirstlane(base);
+  step = __builtin_amdgcn_readfirstlane(step);
 #pragma unroll
   for (int i = 0; i < INSTR; ++i) {
     const int piece = i * NWAVE + wave;  // 1 KiB piece of the LDS image
-    const int c = piece * 64 + lane;     // 16-B chunk index in the image
-    int voff;
-    if constexpr (KC) {
-      constexpr int CPR = BK / 8;
-      const int r = c / CPR, pc = c % CPR;
-      const int lc = pc ^ swz_k<BK>(r);
-      voff = (int)(r * ld * 2) + kt * BK * 2 + lc * 16;
-    } else {
-      constexpr int CPR = ROWS * 2 / 16;
-      const int r = c / CPR, pc = c % CPR;
-      const int lb = (pc * 16) ^ (swz_mn(r) << 5);
-      voff = (int)((long)(kt * BK + r) * ld * 2) + lb;
-    }
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, LDS_PTR(void, smem + lds_off + piece * 1024), 16, vbase + voff, 0, 0,
-                                             0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, LDS_PTR(void, smem + lds_off + piece * 1024), 16,
+                                             lane_off + (base + i * step), 0, 0, 0);
   }
 }
 
@@ -743,7 +752,9 @@ int pick_tile(const vit_gemm_args* a) {
   const bool ak = a->a_layout == VIT_K_CONTIG, bk = a->b_layout == VIT_K_CONTIG;
   if (a->epilogue == VIT_EPI_SPLITK && a->M >= 256 && a->N >= 256) return 5;
   if (a->M >= 1024 && a->N >= 256) {
-    if (ak && bk && a->K >= 512) return 9;
+    // (the GELU-backward epilogue and short-K f32 residual outputs keep 2 workgroups per CU)
+    if (ak && bk && a->epilogue != VIT_EPI_GELU_BWD && !(a->epilogue == VIT_EPI_BIAS_RESID_F32 && a->K < 2048))
+      return 9;
     if (a->N >= 2048 && a->epilogue != VIT_EPI_GELU_BWD) return 5;
     if (!bk && a->K >= 3072) return 5;
     return 3;

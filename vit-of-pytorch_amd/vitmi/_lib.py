@@ -61,6 +61,7 @@ _SIGS = {
     "vit_cast_pad_rows": (c_i32, [c_vp, c_i64, c_i64, c_vp, c_i64, c_vp]),
     "vit_axpby": (c_i32, [c_vp, c_vp, c_i64, c_f32, c_f32, c_vp]),
     "vit_pack_cols": (c_i32, [c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp, c_i64, c_i32, c_vp]),
+    "vit_transpose_f32_bf16": (c_i32, [c_vp, c_i64, c_i64, c_i64, c_vp, c_i64, c_vp]),
 }
 
 EXPORTED = tuple(_SIGS)

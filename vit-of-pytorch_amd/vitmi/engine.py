@@ -187,8 +187,16 @@ class ViTEngine:
         self.grad = torch.zeros(n, device=self.dev)
         self.mirror = torch.zeros(n, device=self.dev, dtype=torch.bfloat16)
         D, L = cfg.emb_dim, cfg.num_layers
-        self.wqkv = torch.zeros(L, D, 3 * D, device=self.dev, dtype=torch.bfloat16)
+        M = cfg.mlp_dim
+        bf = torch.bfloat16
+        self.wqkv = torch.zeros(L, D, 3 * D, device=self.dev, dtype=bf)   # [in][q|k|v out]: qkv dgrad operand
         self.bqkv = torch.zeros(L, 3 * D, device=self.dev)
+        # K-contiguous (transposed) bf16 copies: with them every forward and dgrad GEMM has both
+        # operands K-contiguous and runs on the half-tile ping-pong kernel (tile config 9)
+        self.wqkvt = torch.zeros(L, 3 * D, D, device=self.dev, dtype=bf)  # qkv forward
+        self.woutt = torch.zeros(L, D, D, device=self.dev, dtype=bf)      # out-proj forward
+        self.w1t = torch.zeros(L, D, M, device=self.dev, dtype=bf)        # fc1 dgrad
+        self.w2t = torch.zeros(L, M, D, device=self.dev, dtype=bf)        # fc2 dgrad
         kp = _rup(cfg.patch_k, 64)
         self.wconv = torch.zeros(D, kp, device=self.dev, dtype=torch.bfloat16) if kp != cfg.patch_k else None
         self._acts = {}
@@ -233,6 +241,12 @@ class ViTEngine:
             ops.pack_cols(self.flat[qo:], zs, D, D, D, 3, self.wqkv[i], 3 * D)
             bo = self.off(self.lname(i, "attn.query.bias"))
             ops.pack_cols(self.flat[bo:], zs, D, 1, D, 3, self.bqkv[i], 3 * D)
+            M = cfg.mlp_dim
+            for z in range(3):
+                ops.transpose_bf16(self.flat[qo + z * zs:], D, D, D, self.wqkvt[i, z * D:], D)
+            ops.transpose_bf16(self.flat[self.off(self.lname(i, "attn.out.weight")):], D, D, D, self.woutt[i], D)
+            ops.transpose_bf16(self.flat[self.off(self.lname(i, "mlp.fc1.weight")):], M, D, D, self.w1t[i], M)
+            ops.transpose_bf16(self.flat[self.off(self.lname(i, "mlp.fc2.weight")):], D, M, M, self.w2t[i], D)
         if self.wconv is not None:
             w = self.off("embedding.weight")
             ops.cast_pad_rows(self.flat[w:], D, cfg.patch_k, self.wconv, self.wconv.shape[1])
@@ -297,10 +311,10 @@ class ViTEngine:
             ln = lambda s: self.off(self.lname(i, s))
             ops.layernorm_fwd(a.h[i], D, f[ln("norm1.weight"):], f[ln("norm1.bias"):], a.ln1[i], D, a.mu1[i],
                               a.rs1[i], T, D)
-            ops.gemm(a.ln1[i], self.wqkv[i], a.qkv[i], T, 3 * D, D, a_layout=K_CONTIG, b_layout=MN_CONTIG, lda=D,
-                     ldb=3 * D, ldc=3 * D, epilogue=EPI_BIAS_BF16, bias=self.bqkv[i])
+            ops.gemm(a.ln1[i], self.wqkvt[i], a.qkv[i], T, 3 * D, D, a_layout=K_CONTIG, b_layout=K_CONTIG, lda=D,
+                     ldb=D, ldc=3 * D, epilogue=EPI_BIAS_BF16, bias=self.bqkv[i])
             ops.attention_fwd(a.qkv[i], a.o[i], a.lse[i], b, N, H, hd, scale)
-            ops.gemm(a.o[i], mv[ln("attn.out.weight"):], a.hm[i], T, D, D, a_layout=K_CONTIG, b_layout=MN_CONTIG,
+            ops.gemm(a.o[i], self.woutt[i], a.hm[i], T, D, D, a_layout=K_CONTIG, b_layout=K_CONTIG,
                      lda=D, ldb=D, ldc=D, epilogue=EPI_BIAS_RESID_F32, bias=f[ln("attn.out.bias"):], aux=a.h[i],
                      ldaux=D)
             ops.layernorm_fwd(a.hm[i], D, f[ln("norm2.weight"):], f[ln("norm2.bias"):], a.ln2[i], D, a.mu2[i],
@@ -422,15 +436,15 @@ class ViTEngine:
             release("dhb", wb)
             dg = a.dg[li]
             acquire("dg", li)
-            kw = dict(a_layout=K_CONTIG, b_layout=MN_CONTIG, lda=D, ldb=M, ldc=M, epilogue=EPI_GELU_BWD, aux=a.u[i],
+            kw = dict(a_layout=K_CONTIG, b_layout=K_CONTIG, lda=D, ldb=D, ldc=M, epilogue=EPI_GELU_BWD, aux=a.u[i],
                       ldaux=M, col_partial=a.gelu_part)
-            ops.gemm(dhb, mv[ln("mlp.fc2.weight"):], dg, T, M, D, **kw)
-            tiles_m = -(-T // ops.gemm_tile_rows(dhb, mv, dg, T, M, D, **kw))
+            ops.gemm(dhb, self.w2t[i], dg, T, M, D, **kw)
+            tiles_m = -(-T // ops.gemm_tile_rows(dhb, self.w2t[i], dg, T, M, D, **kw))
             ops.colsum(a.gelu_part, tiles_m, M, M, a.colpart, gv(self.lname(i, "mlp.fc1.bias")))
             on_side(lambda: self._wgrad(dg, M, a.ln2[i], D, M, D, a.Tp, gv(self.lname(i, "mlp.fc1.weight")), D))
             release("dg", li)
-            ops.gemm(dg, mv[ln("mlp.fc1.weight"):], a.dyln, T, D, M, a_layout=K_CONTIG, b_layout=MN_CONTIG, lda=M,
-                     ldb=D, ldc=D, epilogue=EPI_BF16)
+            ops.gemm(dg, self.w1t[i], a.dyln, T, D, M, a_layout=K_CONTIG, b_layout=K_CONTIG, lda=M,
+                     ldb=M, ldc=D, epilogue=EPI_BF16)
             wb ^= 1
             acquire("dhb", wb)
             dhb = a.dhb[wb]

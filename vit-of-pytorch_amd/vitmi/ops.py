@@ -157,3 +157,9 @@ def axpby(x, y, n, a, b):
 def pack_cols(inp, zstride, ldi, rows, cols, Z, out, ldo):
     check(lib().vit_pack_cols(_p(inp), zstride, ldi, rows, cols, Z, _p(out), ldo, int(out.dtype == BF16), _stream()),
           "vit_pack_cols")
+
+
+def transpose_bf16(inp, rows, cols, ldi, out, ldo):
+    """out[c*ldo + r] = bf16(inp[r*ldi + c]) (K-contiguous weight copies)."""
+    _chk(out, BF16, "out")
+    check(lib().vit_transpose_f32_bf16(_p(inp), rows, cols, ldi, _p(out), ldo, _stream()), "vit_transpose_f32_bf16")
