@@ -184,7 +184,7 @@ def main():
                    "model": f"ViT-{args.arch.upper()}", "image_size": args.image_size, "per_gpu_batch": b,
                    "global_batch": b * world, "seq_len": cfg.tokens, "num_classes": args.num_classes,
                    "parallelism": f"dp{world}"},
-        "roofline": {"bound": "mfma", "kernel": "gemm_bf16 fc1 fwd (bias+GELU epilogue), "
+        "roofline": {"bound": "mfma", "kernel": "gemm fc1 fwd (bias + GELU + GELU' epilogue), "
                                                 f"M={T} N={cfg.mlp_dim} K={cfg.emb_dim}",
                      "achieved": round(fc1_tflops, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                      "frac": round(fc1_tflops / PEAK_BF16_TFLOPS, 4), "traffic": None,

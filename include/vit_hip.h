@@ -64,6 +64,9 @@ enum vit_epilogue {
                                             : acc + bias[n] + pos[m % tokens][n],
                                  pos = aux_f32 with row stride ldaux                          */
   VIT_EPI_SPLITK = 7,         /* split-K partial: C(f32)[(z*split_k + s)*M*N + m*N + n] = acc  */
+  VIT_EPI_BIAS_GELU_DGELU = 8,/* u = acc + bias[n]; C(bf16) = gelu_erf'(u); C2(bf16) = gelu_erf(u)
+                                 (the backward then needs no transcendental: VIT_EPI_MUL_BF16)   */
+  VIT_EPI_MUL_BF16 = 9,       /* C(bf16) = acc * aux_bf16[m*ldaux + n]                         */
 };
 
 typedef struct vit_gemm_args {
@@ -159,6 +162,10 @@ int vit_embed_grad(const float* dh0, int64_t B, int64_t N, int64_t D, float* dpo
 int64_t vit_colsum_partial_rows(int64_t rows);
 int vit_colsum(const void* in, int32_t in_bf16, int64_t rows, int64_t cols, int64_t ld,
                float* partial, float* out, int32_t accumulate, vit_stream_t stream);
+/* the same over 3*seg columns, segment k (columns [k*seg, (k+1)*seg)) written to out_k (NULL = dropped):
+ * q|k|v bias gradients, LayerNorm [dgamma | dbeta | dx column sum] in one reduction. Needs seg % 8 == 0. */
+int vit_colsum3(const void* in, int32_t in_bf16, int64_t rows, int64_t seg, int64_t ld, float* partial,
+                float* out0, float* out1, float* out2, int32_t accumulate, vit_stream_t stream);
 
 /* ------------------------------------------------------------------------------------------
  * Classifier head helpers (tiny, f32): C = op(A) op(B) (+ bias) (+ C if accumulate).
@@ -188,11 +195,12 @@ int vit_cast_pad_rows(const float* in, int64_t rows, int64_t cols, void* out, in
  * Packs q/k/v LinearGeneral weights [D][H,hd] (src/model.py:73-75) into one [D][3D] operand. */
 int vit_pack_cols(const float* in, int64_t zstride, int64_t ldi, int64_t rows, int64_t cols, int64_t Z,
                   void* out, int64_t ldo, int32_t out_bf16, vit_stream_t stream);
-/* out bf16 [cols][ldo] <- transpose of in f32 [rows][ldi]: out[c*ldo + r] = bf16(in[r*ldi + c]).
+/* out bf16 [cols][ldo] <- transpose of in f32 [rows][ldi]: out[c*ldo + r] = bf16(in[r*ldi + c]), for
+ * batch matrices z at in + z*in_batch_stride, out + z*out_batch_stride (strides may be negative).
  * K-contiguous weight copies for the dgrad / projection GEMMs (fc1/fc2 weights src/model.py:31-32,
  * LinearGeneral q/k/v/out src/model.py:73-76). */
 int vit_transpose_f32_bf16(const float* in, int64_t rows, int64_t cols, int64_t ldi, void* out, int64_t ldo,
-                           vit_stream_t stream);
+                           int64_t batch, int64_t in_batch_stride, int64_t out_batch_stride, vit_stream_t stream);
 /* y = a*x + b*y (f32), used for gradient scaling / accumulation. */
 int vit_axpby(const float* x, float* y, int64_t n, float a, float b, vit_stream_t stream);
 

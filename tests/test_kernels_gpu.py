@@ -7,8 +7,8 @@ import torch
 pytestmark = pytest.mark.gpu
 
 from vitmi import ops
-from vitmi._lib import (EPI_BF16, EPI_BIAS_BF16, EPI_BIAS_GELU, EPI_BIAS_RESID_F32, EPI_F32, EPI_GELU_BWD,
-                        EPI_PATCH, EPI_SPLITK, K_CONTIG, MN_CONTIG)
+from vitmi._lib import (EPI_BF16, EPI_BIAS_BF16, EPI_BIAS_GELU, EPI_BIAS_GELU_DGELU, EPI_BIAS_RESID_F32, EPI_F32,
+                        EPI_GELU_BWD, EPI_MUL_BF16, EPI_PATCH, EPI_SPLITK, K_CONTIG, MN_CONTIG)
 
 DEV = "cuda"
 
@@ -324,3 +324,24 @@ def test_transpose_bf16(rows, cols):
     out = torch.full((cols, rows + 3), float("nan"), device=DEV).bfloat16()
     ops.transpose_bf16(x, rows, cols, cols + 5, out, rows + 3)
     assert torch.equal(out[:, :rows], x[:, :cols].t().bfloat16())
+
+
+@pytest.mark.parametrize("tile", [0, 3, 9])
+def test_gemm_gelu_dgelu_and_mul(tile):
+    """fc1 forward epilogue writing GELU(u) and GELU'(u); backward multiply by the saved GELU'."""
+    M, N, K = 700, 512, 256
+    A, B, Am, Bm, lda, ldb = _mats(M, N, K, K_CONTIG, K_CONTIG)
+    bias = torch.randn(N, device=DEV)
+    u = (A.float() @ B.float() + bias).requires_grad_(True)
+    g = torch.nn.functional.gelu(u)
+    gp, = torch.autograd.grad(g.sum(), u)
+    C = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    C2 = torch.empty_like(C)
+    ops.gemm(Am, Bm, C, M, N, K, a_layout=K_CONTIG, b_layout=K_CONTIG, lda=lda, ldb=ldb, ldc=N,
+             epilogue=EPI_BIAS_GELU_DGELU, bias=bias, C2=C2, ldc2=N, tile=tile)
+    assert rel(C.float(), gp) < 5e-3
+    assert rel(C2.float(), g.detach()) < 5e-3
+    D = torch.empty_like(C)
+    ops.gemm(Am, Bm, D, M, N, K, a_layout=K_CONTIG, b_layout=K_CONTIG, lda=lda, ldb=ldb, ldc=N,
+             epilogue=EPI_MUL_BF16, aux=C, ldaux=N, tile=tile)
+    assert rel(D.float(), (A.float() @ B.float()) * C.float()) < 5e-3

@@ -18,8 +18,8 @@ sys.path.insert(0, os.path.join(REPO, "vit-of-pytorch_amd"))
 import torch  # noqa: E402
 
 from vitmi import ops  # noqa: E402
-from vitmi._lib import (EPI_BF16, EPI_BIAS_BF16, EPI_BIAS_GELU, EPI_BIAS_RESID_F32, EPI_GELU_BWD, EPI_SPLITK,  # noqa: E402
-                        K_CONTIG, MN_CONTIG)
+from vitmi._lib import (EPI_BF16, EPI_BIAS_BF16, EPI_BIAS_GELU, EPI_BIAS_GELU_DGELU, EPI_BIAS_RESID_F32,  # noqa
+                        EPI_GELU_BWD, EPI_MUL_BF16, EPI_SPLITK, K_CONTIG, MN_CONTIG)
 
 
 def bench(fn, iters=20):
@@ -87,9 +87,9 @@ def main():
                 elif epi == EPI_BIAS_RESID_F32:
                     extra = dict(bias=bias, aux=Cf, ldaux=N)
                     out = Cf
-                elif epi == EPI_BIAS_GELU:
+                elif epi in (EPI_BIAS_GELU, EPI_BIAS_GELU_DGELU):
                     extra = dict(bias=bias, C2=C2, ldc2=N)
-                elif epi == EPI_GELU_BWD:
+                elif epi in (EPI_GELU_BWD, EPI_MUL_BF16):
                     extra = dict(aux=U, ldaux=N)
                 fn = (lambda tile=tile, epi=epi, extra=extra, out=out:
                       ops.gemm(A, B, out, M, N, K, a_layout=al, b_layout=bl, lda=K, ldb=ldb, ldc=N, epilogue=epi,

@@ -14,7 +14,7 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/ktr
     python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline > $O/bench_ktrace.log 2>&1
 S=$(find $O/ktrace -name "*kernel_stats.csv" | head -1)
 python3 tools/prof_summary.py $S 13 > $O/summary.txt
-RX=${ROOF_RX:-'gemm_(bf16|pp)_kernel<.*, 3>'}
+RX=${ROOF_RX:-'gemm_\w+_kernel<.*, 8>'}
 timeout -k 10 -s KILL 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$RX" --output-format csv -d $O/fetch -o run -- \
     python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > $O/bench_fetch.log 2>&1
 timeout -k 10 -s KILL 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$RX" --output-format csv -d $O/write -o run -- \

@@ -54,9 +54,19 @@ __global__ void cls_bias_grad_kernel(const float* __restrict__ dpos, int N, int 
 constexpr int COLSUM_MAX_CHUNKS = 256;
 constexpr int COLSUM_MIN_ROWS_PER_CHUNK = 64;
 
+// Final destination of column `col`: with seg > 0 the columns are split into segments of `seg`
+// columns written to out / out1 / out2 (segment k -> its own array, NULL = dropped).
+__device__ __forceinline__ float* seg_dst(float* out, float* out1, float* out2, long seg, long ch, int cols, int col) {
+  if (seg <= 0) return out + ch * cols + col;
+  const int k = (int)(col / seg);
+  float* base = k == 0 ? out : (k == 1 ? out1 : out2);
+  return base ? base + (col - k * seg) : nullptr;
+}
+
 template <bool BF16>
 __global__ void __launch_bounds__(256) colsum8_kernel(const void* __restrict__ in, long rows, int cols, long ld,
-                                                      int chunks, float* __restrict__ out, int accumulate) {
+                                                      int chunks, float* __restrict__ out, int accumulate,
+                                                      long seg = 0, float* out1 = nullptr, float* out2 = nullptr) {
   __shared__ float red[8][32][9];
   const int cgl = threadIdx.x & 31, rl = threadIdx.x >> 5;
   const int cg = blockIdx.x * 32 + cgl;
@@ -87,8 +97,8 @@ __global__ void __launch_bounds__(256) colsum8_kernel(const void* __restrict__ i
     float s = 0.f;
 #pragma unroll
     for (int q = 0; q < 8; ++q) s += red[q][ocg][k];
-    float* dst = out + (long)ch * cols + col;
-    *dst = accumulate ? *dst + s : s;
+    float* dst = seg_dst(out, out1, out2, seg, ch, cols, col);
+    if (dst) *dst = accumulate ? *dst + s : s;
   }
 }
 
@@ -274,6 +284,35 @@ extern "C" int64_t vit_colsum_partial_rows(int64_t rows) {
   return c < 1 ? 1 : c;
 }
 
+extern "C" int vit_colsum3(const void* in, int32_t in_bf16, int64_t rows, int64_t seg, int64_t ld, float* partial,
+                           float* out0, float* out1, float* out2, int32_t accumulate, vit_stream_t stream) {
+  const int64_t cols = 3 * seg;
+  VIT_CHECK_ARG(in && partial && seg > 0 && ld >= cols, "vit_colsum3: bad args");
+  const int chunks = (int)vit_colsum_partial_rows(rows);
+  const bool vec = cols % 8 == 0 && ld % 8 == 0 && ((uintptr_t)in % 32) == 0 && ((uintptr_t)partial % 16) == 0;
+  VIT_CHECK_ARG(vec, "vit_colsum3: needs 8-column aligned rows");
+  hipStream_t s = (hipStream_t)stream;
+  const unsigned gx = (unsigned)((cols / 8 + 31) / 32);
+  if (chunks == 1) {
+    if (in_bf16)
+      hipLaunchKernelGGL(colsum8_kernel<true>, dim3(gx, 1), dim3(256), 0, s, in, (long)rows, (int)cols, (long)ld, 1,
+                         out0, (int)accumulate, (long)seg, out1, out2);
+    else
+      hipLaunchKernelGGL(colsum8_kernel<false>, dim3(gx, 1), dim3(256), 0, s, in, (long)rows, (int)cols, (long)ld, 1,
+                         out0, (int)accumulate, (long)seg, out1, out2);
+    VIT_LAUNCH_CHECK("vit_colsum3");
+  }
+  if (in_bf16)
+    hipLaunchKernelGGL(colsum8_kernel<true>, dim3(gx, chunks), dim3(256), 0, s, in, (long)rows, (int)cols, (long)ld,
+                       chunks, partial, 0, 0L, (float*)nullptr, (float*)nullptr);
+  else
+    hipLaunchKernelGGL(colsum8_kernel<false>, dim3(gx, chunks), dim3(256), 0, s, in, (long)rows, (int)cols, (long)ld,
+                       chunks, partial, 0, 0L, (float*)nullptr, (float*)nullptr);
+  hipLaunchKernelGGL(colsum8_kernel<false>, dim3(gx, 1), dim3(256), 0, s, (const void*)partial, (long)chunks,
+                     (int)cols, (long)cols, 1, out0, (int)accumulate, (long)seg, out1, out2);
+  VIT_LAUNCH_CHECK("vit_colsum3");
+}
+
 extern "C" int vit_colsum(const void* in, int32_t in_bf16, int64_t rows, int64_t cols, int64_t ld, float* partial,
                           float* out, int32_t accumulate, vit_stream_t stream) {
   VIT_CHECK_ARG(in && partial && out && cols > 0 && ld >= cols, "vit_colsum: bad args");
@@ -396,10 +435,13 @@ extern "C" int vit_pack_cols(const float* in, int64_t zstride, int64_t ldi, int6
 // runs on the both-K-contiguous ping-pong kernel. 64 x 64 tiles through LDS, coalesced both ways.
 namespace {
 __global__ void __launch_bounds__(256) transpose_f32_bf16_kernel(const float* __restrict__ in, long ldi, int rows,
-                                                                 int cols, bf16_t* __restrict__ out, long ldo) {
+                                                                 int cols, bf16_t* __restrict__ out, long ldo,
+                                                                 long in_bs, long out_bs) {
   __shared__ float tile[64][65];
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
   const int c0 = blockIdx.x * 64, r0 = blockIdx.y * 64;
+  in += blockIdx.z * in_bs;
+  out += blockIdx.z * out_bs;
 #pragma unroll
   for (int k = 0; k < 16; ++k) {
     const int r = r0 + ty + 4 * k, c = c0 + tx;
@@ -415,11 +457,13 @@ __global__ void __launch_bounds__(256) transpose_f32_bf16_kernel(const float* __
 }  // namespace
 
 extern "C" int vit_transpose_f32_bf16(const float* in, int64_t rows, int64_t cols, int64_t ldi, void* out,
-                                      int64_t ldo, vit_stream_t stream) {
-  VIT_CHECK_ARG(in && out && rows >= 0 && cols >= 0 && ldi >= cols && ldo >= rows, "vit_transpose_f32_bf16: bad args");
+                                      int64_t ldo, int64_t batch, int64_t in_batch_stride, int64_t out_batch_stride,
+                                      vit_stream_t stream) {
+  VIT_CHECK_ARG(in && out && rows >= 0 && cols >= 0 && ldi >= cols && ldo >= rows && batch >= 1,
+                "vit_transpose_f32_bf16: bad args");
   if (rows == 0 || cols == 0) return VIT_OK;
-  dim3 grid((unsigned)((cols + 63) / 64), (unsigned)((rows + 63) / 64));
+  dim3 grid((unsigned)((cols + 63) / 64), (unsigned)((rows + 63) / 64), (unsigned)batch);
   hipLaunchKernelGGL(transpose_f32_bf16_kernel, grid, dim3(256), 0, (hipStream_t)stream, in, (long)ldi, (int)rows,
-                     (int)cols, (bf16_t*)out, (long)ldo);
+                     (int)cols, (bf16_t*)out, (long)ldo, (long)in_batch_stride, (long)out_batch_stride);
   VIT_LAUNCH_CHECK("vit_transpose_f32_bf16");
 }

@@ -169,6 +169,18 @@ __device__ __forceinline__ void epi_store(const GemmDev& p, int z, int split_idx
     bf16_t* C = (bf16_t*)p.C + z * p.c_bs;
     const bf16_t* U = (const bf16_t*)p.aux;
     C[(long)m * p.ldc + n] = f2bf(v * gelu_grad_f(bf2f(U[(long)m * p.ldaux + n])));
+  } else if constexpr (EPI == VIT_EPI_BIAS_GELU_DGELU) {
+    bf16_t* C = (bf16_t*)p.C + z * p.c_bs;
+    bf16_t* C2 = (bf16_t*)p.C2 + z * p.c_bs;
+    const float u = v + (p.bias ? p.bias[z * p.bias_bs + n] : 0.f);
+    float pdf;
+    const float cdf = phi_and_pdf(u, &pdf);
+    C[(long)m * p.ldc + n] = f2bf(cdf + u * pdf);
+    C2[(long)m * p.ldc2 + n] = f2bf(u * cdf);
+  } else if constexpr (EPI == VIT_EPI_MUL_BF16) {
+    bf16_t* C = (bf16_t*)p.C + z * p.c_bs;
+    const bf16_t* U = (const bf16_t*)p.aux;
+    C[(long)m * p.ldc + n] = f2bf(v * bf2f(U[(long)m * p.ldaux + n]));
   } else if constexpr (EPI == VIT_EPI_PATCH) {
     float* C = (float*)p.C;
     const float* pos = (const float*)p.aux;
@@ -219,7 +231,8 @@ __device__ __forceinline__ void ld8bf(const bf16_t* p, float* v) {
 template <int EPI>
 __device__ __forceinline__ void epi_store8(const GemmDev& p, int z, int split_idx, int m, int n, float* v) {
   float b[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  if constexpr (EPI == VIT_EPI_BIAS_BF16 || EPI == VIT_EPI_BIAS_GELU || EPI == VIT_EPI_BIAS_RESID_F32) {
+  if constexpr (EPI == VIT_EPI_BIAS_BF16 || EPI == VIT_EPI_BIAS_GELU || EPI == VIT_EPI_BIAS_RESID_F32 ||
+                EPI == VIT_EPI_BIAS_GELU_DGELU) {
     if (p.bias) ld8f(p.bias + z * p.bias_bs + n, b);
   }
   if constexpr (EPI == VIT_EPI_F32) {
@@ -250,6 +263,24 @@ __device__ __forceinline__ void epi_store8(const GemmDev& p, int z, int split_id
     ld8bf((const bf16_t*)p.aux + (long)m * p.ldaux + n, u);
 #pragma unroll
     for (int k = 0; k < 8; ++k) v[k] *= gelu_grad_f(u[k]);
+    st8bf((bf16_t*)p.C + z * p.c_bs + (long)m * p.ldc + n, v, p.nt);
+  } else if constexpr (EPI == VIT_EPI_BIAS_GELU_DGELU) {
+    float gl[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const float u = v[k] + b[k];
+      float pdf;
+      const float cdf = phi_and_pdf(u, &pdf);
+      gl[k] = u * cdf;
+      v[k] = cdf + u * pdf;
+    }
+    st8bf((bf16_t*)p.C + z * p.c_bs + (long)m * p.ldc + n, v, p.nt);
+    st8bf((bf16_t*)p.C2 + z * p.c_bs + (long)m * p.ldc2 + n, gl, p.nt);
+  } else if constexpr (EPI == VIT_EPI_MUL_BF16) {
+    float u[8];
+    ld8bf((const bf16_t*)p.aux + (long)m * p.ldaux + n, u);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] *= u[k];
     st8bf((bf16_t*)p.C + z * p.c_bs + (long)m * p.ldc + n, v, p.nt);
   } else if constexpr (EPI == VIT_EPI_PATCH) {
     const int t = m % p.tokens;
@@ -753,9 +784,10 @@ int pick_tile(const vit_gemm_args* a) {
   if (a->epilogue == VIT_EPI_SPLITK && a->M >= 256 && a->N >= 256) return 5;
   if (a->M >= 1024 && a->N >= 256) {
     // (the GELU-backward epilogue and short-K f32 residual outputs keep 2 workgroups per CU)
-    if (ak && bk && a->epilogue != VIT_EPI_GELU_BWD && !(a->epilogue == VIT_EPI_BIAS_RESID_F32 && a->K < 2048))
+    if (ak && bk && a->epilogue != VIT_EPI_GELU_BWD && a->epilogue != VIT_EPI_MUL_BF16 &&
+        !(a->epilogue == VIT_EPI_BIAS_RESID_F32 && a->K < 2048))
       return 9;
-    if (a->N >= 2048 && a->epilogue != VIT_EPI_GELU_BWD) return 5;
+    if (a->N >= 2048 && a->epilogue != VIT_EPI_GELU_BWD && a->epilogue != VIT_EPI_MUL_BF16) return 5;
     if (!bk && a->K >= 3072) return 5;
     return 3;
   }
@@ -800,6 +832,8 @@ extern "C" int vit_gemm_bf16(const vit_gemm_args* a, vit_stream_t stream) {
     case VIT_EPI_BIAS_GELU: VIT_CHECK_ARG(a->C2 != nullptr, "GELU epilogue needs C2"); break;
     case VIT_EPI_BIAS_RESID_F32: VIT_CHECK_ARG(a->aux != nullptr, "RESID epilogue needs aux"); break;
     case VIT_EPI_GELU_BWD: VIT_CHECK_ARG(a->aux != nullptr, "GELU_BWD epilogue needs aux"); break;
+    case VIT_EPI_MUL_BF16: VIT_CHECK_ARG(a->aux != nullptr, "MUL epilogue needs aux"); break;
+    case VIT_EPI_BIAS_GELU_DGELU: VIT_CHECK_ARG(a->C2 != nullptr, "GELU_DGELU epilogue needs C2"); break;
     case VIT_EPI_PATCH:
       VIT_CHECK_ARG(a->aux && a->aux2 && a->bias && a->tokens > 0 && a->batch == 1, "PATCH epilogue args");
       break;
@@ -841,6 +875,7 @@ extern "C" int vit_gemm_bf16(const vit_gemm_args* a, vit_stream_t stream) {
   if (a->col_partial) {
     VIT_CHECK_ARG(a->batch == 1 && a->split_k == 1 && d.vec && a->N % 8 == 0 &&
                       (a->epilogue == VIT_EPI_F32 || a->epilogue == VIT_EPI_BF16 || a->epilogue == VIT_EPI_GELU_BWD ||
+                       a->epilogue == VIT_EPI_MUL_BF16 ||
                        a->epilogue == VIT_EPI_BIAS_BF16 || a->epilogue == VIT_EPI_BIAS_RESID_F32),
                   "vit_gemm_bf16: col_partial needs batch 1, split_k 1, aligned N%%8==0 operands and a plain epilogue");
   }
@@ -857,6 +892,10 @@ extern "C" int vit_gemm_bf16(const vit_gemm_args* a, vit_stream_t stream) {
     case VIT_EPI_BIAS_GELU: e = launch_layout<VIT_EPI_BIAS_GELU>(cfg, d, ak, bk, batch, split, s); break;
     case VIT_EPI_BIAS_RESID_F32: e = launch_layout<VIT_EPI_BIAS_RESID_F32>(cfg, d, ak, bk, batch, split, s); break;
     case VIT_EPI_GELU_BWD: e = launch_layout<VIT_EPI_GELU_BWD>(cfg, d, ak, bk, batch, split, s); break;
+    case VIT_EPI_BIAS_GELU_DGELU:
+      e = launch_layout<VIT_EPI_BIAS_GELU_DGELU>(cfg, d, ak, bk, batch, split, s);
+      break;
+    case VIT_EPI_MUL_BF16: e = launch_layout<VIT_EPI_MUL_BF16>(cfg, d, ak, bk, batch, split, s); break;
     case VIT_EPI_PATCH: e = launch_layout<VIT_EPI_PATCH>(cfg, d, ak, bk, batch, split, s); break;
     case VIT_EPI_SPLITK: e = launch_layout<VIT_EPI_SPLITK>(cfg, d, ak, bk, batch, split, s); break;
     default: vit::set_error("vit_gemm_bf16: unknown epilogue %d", a->epilogue); return VIT_ERR_INVALID_ARG;
@@ -880,15 +919,54 @@ __global__ void splitk_reduce_kernel(const float* __restrict__ ws, int split, lo
     *dst = accumulate ? *dst + s : s;
   }
 }
+// 4 columns per thread, the slabs read 4 at a time with independent 16-B loads (memory-level
+// parallelism: the scalar loop above issued one dependent load per slab); N, ldo multiples of 4.
+__global__ void splitk_reduce4_kernel(const float* __restrict__ ws, int split, long M, long N, float* __restrict__ out,
+                                      long ldo, long obs, int accumulate) {
+  const int z = blockIdx.y;
+  const long total = M * N, total4 = total / 4;
+  const float4* w = reinterpret_cast<const float4*>(ws + (long)z * split * total);
+  float* o = out + z * obs;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total4; i += (long)gridDim.x * blockDim.x) {
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+    int k = 0;
+    for (; k + 4 <= split; k += 4) {
+      const float4 a = w[(long)k * total4 + i], b = w[(long)(k + 1) * total4 + i];
+      const float4 c = w[(long)(k + 2) * total4 + i], d = w[(long)(k + 3) * total4 + i];
+      s.x += (a.x + b.x) + (c.x + d.x);
+      s.y += (a.y + b.y) + (c.y + d.y);
+      s.z += (a.z + b.z) + (c.z + d.z);
+      s.w += (a.w + b.w) + (c.w + d.w);
+    }
+    for (; k < split; ++k) {
+      const float4 a = w[(long)k * total4 + i];
+      s.x += a.x; s.y += a.y; s.z += a.z; s.w += a.w;
+    }
+    const long e = i * 4, m = e / N, n = e - m * N;
+    float4* dst = reinterpret_cast<float4*>(o + m * ldo + n);
+    if (accumulate) {
+      const float4 p = *dst;
+      s.x += p.x; s.y += p.y; s.z += p.z; s.w += p.w;
+    }
+    *dst = s;
+  }
+}
 }  // namespace
 
 extern "C" int vit_splitk_reduce(const float* ws, int64_t batch, int64_t split, int64_t M, int64_t N, float* out,
                                  int64_t ldo, int64_t out_batch_stride, int32_t accumulate, vit_stream_t stream) {
   VIT_CHECK_ARG(ws && out && batch >= 1 && split >= 1 && ldo >= N, "vit_splitk_reduce: bad args");
   if (M * N == 0) return VIT_OK;
-  long blocks = (M * N + 255) / 256;
+  const bool vec = N % 4 == 0 && ldo % 4 == 0 && out_batch_stride % 4 == 0 && ((uintptr_t)ws % 16) == 0 &&
+                   ((uintptr_t)out % 16) == 0;
+  long blocks = (M * N / (vec ? 4 : 1) + 255) / 256;
   if (blocks > 4096) blocks = 4096;
-  hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)blocks, (unsigned)batch), dim3(256), 0, (hipStream_t)stream, ws,
-                     (int)split, (long)M, (long)N, out, (long)ldo, (long)out_batch_stride, (int)accumulate);
+  if (vec)
+    hipLaunchKernelGGL(splitk_reduce4_kernel, dim3((unsigned)blocks, (unsigned)batch), dim3(256), 0,
+                       (hipStream_t)stream, ws, (int)split, (long)M, (long)N, out, (long)ldo, (long)out_batch_stride,
+                       (int)accumulate);
+  else
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)blocks, (unsigned)batch), dim3(256), 0, (hipStream_t)stream,
+                       ws, (int)split, (long)M, (long)N, out, (long)ldo, (long)out_batch_stride, (int)accumulate);
   VIT_LAUNCH_CHECK("vit_splitk_reduce");
 }

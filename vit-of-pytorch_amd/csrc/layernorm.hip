@@ -212,6 +212,10 @@ extern "C" int vit_layernorm_bwd(const void* dy, int64_t lddy, int32_t dy_f32, c
   int st = vit::check_hip(hipGetLastError(), "vit_layernorm_bwd");
   if (st) return st;
   float* ws = partial + nblk * 3 * D;
+  if (!dgamma_dbeta && !dx_colsum) return VIT_OK;
+  if (D % 8 == 0)  // one reduction for [dgamma | dbeta | dx colsum]
+    return vit_colsum3(partial, 0, nblk, D, 3 * D, ws, dgamma_dbeta, dgamma_dbeta ? dgamma_dbeta + D : nullptr,
+                       dx_colsum, accumulate_params, stream);
   if (dgamma_dbeta) st = vit_colsum(partial, 0, nblk, 2 * D, 3 * D, ws, dgamma_dbeta, accumulate_params, stream);
   if (st) return st;
   if (dx_colsum) st = vit_colsum(partial + 2 * D, 0, nblk, D, 3 * D, ws, dx_colsum, accumulate_params, stream);

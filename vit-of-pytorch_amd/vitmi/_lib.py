@@ -18,7 +18,8 @@ c_vp = ctypes.c_void_p
 
 # enum vit_layout / vit_epilogue (include/vit_hip.h)
 K_CONTIG, MN_CONTIG = 0, 1
-EPI_F32, EPI_BF16, EPI_BIAS_BF16, EPI_BIAS_GELU, EPI_BIAS_RESID_F32, EPI_GELU_BWD, EPI_PATCH, EPI_SPLITK = range(8)
+(EPI_F32, EPI_BF16, EPI_BIAS_BF16, EPI_BIAS_GELU, EPI_BIAS_RESID_F32, EPI_GELU_BWD, EPI_PATCH, EPI_SPLITK,
+ EPI_BIAS_GELU_DGELU, EPI_MUL_BF16) = range(10)
 
 
 class GemmArgs(ctypes.Structure):
@@ -61,7 +62,8 @@ _SIGS = {
     "vit_cast_pad_rows": (c_i32, [c_vp, c_i64, c_i64, c_vp, c_i64, c_vp]),
     "vit_axpby": (c_i32, [c_vp, c_vp, c_i64, c_f32, c_f32, c_vp]),
     "vit_pack_cols": (c_i32, [c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp, c_i64, c_i32, c_vp]),
-    "vit_transpose_f32_bf16": (c_i32, [c_vp, c_i64, c_i64, c_i64, c_vp, c_i64, c_vp]),
+    "vit_transpose_f32_bf16": (c_i32, [c_vp, c_i64, c_i64, c_i64, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp]),
+    "vit_colsum3": (c_i32, [c_vp, c_i32, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_i32, c_vp]),
 }
 
 EXPORTED = tuple(_SIGS)

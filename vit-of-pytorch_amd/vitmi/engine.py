@@ -22,8 +22,8 @@ from dataclasses import dataclass
 import torch
 
 from . import ops
-from ._lib import (EPI_BF16, EPI_BIAS_BF16, EPI_BIAS_GELU, EPI_BIAS_RESID_F32, EPI_GELU_BWD, EPI_PATCH, EPI_SPLITK,
-                   K_CONTIG, MN_CONTIG)
+from ._lib import (EPI_BF16, EPI_BIAS_BF16, EPI_BIAS_GELU_DGELU, EPI_BIAS_RESID_F32, EPI_MUL_BF16, EPI_PATCH,
+                   EPI_SPLITK, K_CONTIG, MN_CONTIG)
 
 ALIGN = 64  # elements; every parameter starts 256-B aligned in the flat buffers
 
@@ -142,7 +142,7 @@ class _Acts:
         self.qkv = [z(Tp, 3 * D) for _ in range(L)]
         self.o = [z(Tp, D) for _ in range(L)]
         self.lse = [z(b, H, N, dt=f) for _ in range(L)]
-        self.u = [z(Tp, M) for _ in range(L)]
+        self.gp = [z(Tp, M) for _ in range(L)]      # GELU'(fc1 pre-activation), for the backward
         self.g = [z(Tp, M) for _ in range(L)]
         self.lncls = z(b, D, dt=f)
         self.muf = z(b, dt=f)
@@ -201,6 +201,10 @@ class ViTEngine:
         self.wconv = torch.zeros(D, kp, device=self.dev, dtype=torch.bfloat16) if kp != cfg.patch_k else None
         self._acts = {}
         self._mirror_sig = None
+        # flat-buffer distance between consecutive encoder layers (constant: same specs, same alignment)
+        o = [self.off(self.lname(i, "norm1.weight")) for i in range(L)]
+        self.layer_stride = o[0] - o[1] if L > 1 else 0
+        assert all(o[i] == o[0] - i * self.layer_stride for i in range(L))
         self._ws = None
         self.step_id = 0
         self.grad_ready_hook = None  # callable(grad_buf, bucket_name, start, end, events) during backward
@@ -241,12 +245,21 @@ class ViTEngine:
             ops.pack_cols(self.flat[qo:], zs, D, D, D, 3, self.wqkv[i], 3 * D)
             bo = self.off(self.lname(i, "attn.query.bias"))
             ops.pack_cols(self.flat[bo:], zs, D, 1, D, 3, self.bqkv[i], 3 * D)
-            M = cfg.mlp_dim
-            for z in range(3):
-                ops.transpose_bf16(self.flat[qo + z * zs:], D, D, D, self.wqkvt[i, z * D:], D)
-            ops.transpose_bf16(self.flat[self.off(self.lname(i, "attn.out.weight")):], D, D, D, self.woutt[i], D)
-            ops.transpose_bf16(self.flat[self.off(self.lname(i, "mlp.fc1.weight")):], M, D, D, self.w1t[i], M)
-            ops.transpose_bf16(self.flat[self.off(self.lname(i, "mlp.fc2.weight")):], D, M, M, self.w2t[i], D)
+        # K-contiguous copies, one launch per weight kind over all layers (layers sit at a constant
+        # stride in the flat buffer, layer L-1 first)
+        M, L = cfg.mlp_dim, cfg.num_layers
+        lst = self.layer_stride
+        o0 = lambda s: self.off(self.lname(0, s))
+        zs = self.off(self.lname(0, "attn.key.weight")) - o0("attn.query.weight")
+        for z in range(3):
+            ops.transpose_bf16(self.flat[o0("attn.query.weight") + z * zs:], D, D, D, self.wqkvt[0, z * D:], D,
+                               batch=L, in_bs=-lst, out_bs=3 * D * D)
+        ops.transpose_bf16(self.flat[o0("attn.out.weight"):], D, D, D, self.woutt[0], D, batch=L, in_bs=-lst,
+                           out_bs=D * D)
+        ops.transpose_bf16(self.flat[o0("mlp.fc1.weight"):], M, D, D, self.w1t[0], M, batch=L, in_bs=-lst,
+                           out_bs=D * M)
+        ops.transpose_bf16(self.flat[o0("mlp.fc2.weight"):], D, M, M, self.w2t[0], D, batch=L, in_bs=-lst,
+                           out_bs=M * D)
         if self.wconv is not None:
             w = self.off("embedding.weight")
             ops.cast_pad_rows(self.flat[w:], D, cfg.patch_k, self.wconv, self.wconv.shape[1])
@@ -322,8 +335,9 @@ class ViTEngine:
             if self.probe is not None:
                 ev0 = torch.cuda.Event(enable_timing=True)
                 ev0.record()
-            ops.gemm(a.ln2[i], mv[ln("mlp.fc1.weight"):], a.u[i], T, M, D, a_layout=K_CONTIG, b_layout=K_CONTIG,
-                     lda=D, ldb=D, ldc=M, epilogue=EPI_BIAS_GELU, bias=f[ln("mlp.fc1.bias"):], C2=a.g[i], ldc2=M)
+            ops.gemm(a.ln2[i], mv[ln("mlp.fc1.weight"):], a.gp[i], T, M, D, a_layout=K_CONTIG, b_layout=K_CONTIG,
+                     lda=D, ldb=D, ldc=M, epilogue=EPI_BIAS_GELU_DGELU, bias=f[ln("mlp.fc1.bias"):], C2=a.g[i],
+                     ldc2=M)
             if self.probe is not None:
                 ev1 = torch.cuda.Event(enable_timing=True)
                 ev1.record()
@@ -436,7 +450,7 @@ class ViTEngine:
             release("dhb", wb)
             dg = a.dg[li]
             acquire("dg", li)
-            kw = dict(a_layout=K_CONTIG, b_layout=K_CONTIG, lda=D, ldb=D, ldc=M, epilogue=EPI_GELU_BWD, aux=a.u[i],
+            kw = dict(a_layout=K_CONTIG, b_layout=K_CONTIG, lda=D, ldb=D, ldc=M, epilogue=EPI_MUL_BF16, aux=a.gp[i],
                       ldaux=M, col_partial=a.gelu_part)
             ops.gemm(dhb, self.w2t[i], dg, T, M, D, **kw)
             tiles_m = -(-T // ops.gemm_tile_rows(dhb, self.w2t[i], dg, T, M, D, **kw))
@@ -462,8 +476,8 @@ class ViTEngine:
             ops.attention_bwd(a.qkv[i], a.o[i], a.dO, a.lse[i], dqkv, b, N, H, hd, scale, bias_partial=a.qkv_bpart)
             qo = ln("attn.query.weight")
             zs = ln("attn.key.weight") - qo
-            for z in range(3):
-                ops.colsum(a.qkv_bpart[:, z * D:], b, D, 3 * D, a.colpart, g[ln("attn.query.bias") + z * zs:])
+            qb = ln("attn.query.bias")
+            ops.colsum3(a.qkv_bpart, b, D, 3 * D, a.colpart, g[qb:], g[qb + zs:], g[qb + 2 * zs:])
             on_side(lambda: self._wgrad(a.ln1[i], D, dqkv, 3 * D, D, D, a.Tp, g[qo:], D, batch=3, b_bs=D,
                                         out_bs=zs))
             release("dqkv", li)

@@ -159,7 +159,14 @@ def pack_cols(inp, zstride, ldi, rows, cols, Z, out, ldo):
           "vit_pack_cols")
 
 
-def transpose_bf16(inp, rows, cols, ldi, out, ldo):
-    """out[c*ldo + r] = bf16(inp[r*ldi + c]) (K-contiguous weight copies)."""
+def transpose_bf16(inp, rows, cols, ldi, out, ldo, batch=1, in_bs=0, out_bs=0):
+    """out[z][c*ldo + r] = bf16(inp[z][r*ldi + c]) (K-contiguous weight copies; z strides may be negative)."""
     _chk(out, BF16, "out")
-    check(lib().vit_transpose_f32_bf16(_p(inp), rows, cols, ldi, _p(out), ldo, _stream()), "vit_transpose_f32_bf16")
+    check(lib().vit_transpose_f32_bf16(_p(inp), rows, cols, ldi, _p(out), ldo, batch, in_bs, out_bs, _stream()),
+          "vit_transpose_f32_bf16")
+
+
+def colsum3(inp, rows, seg, ld, partial, out0, out1, out2, accumulate=False):
+    """column sums of a [rows][3*seg] matrix, segment k -> out_k (q|k|v bias gradients)."""
+    check(lib().vit_colsum3(_p(inp), int(inp.dtype == BF16), rows, seg, ld, _p(partial), _p(out0), _p(out1), _p(out2),
+                            int(accumulate), _stream()), "vit_colsum3")
