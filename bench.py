@@ -43,6 +43,23 @@ def train_flops_per_image(a, image_size, num_classes):
     return 3 * fwd - patch
 
 
+def pmc_traffic(kernel_tag="gemm_pp2_kernel<true, true, 8>"):
+    """HBM bytes per launch of the roofline kernel from the newest committed rocprofv3 PMC passes
+    (tools/prof.sh: FETCH_SIZE and WRITE_SIZE in separate passes, FETCH_SIZE doubled per the gfx950
+    correction of MI355X_MICROARCH.md). None when no pass of that kernel is committed."""
+    import glob
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*", "fc1_traffic*.json")), key=os.path.getmtime)
+    for path in reversed(files):
+        try:
+            d = json.load(open(path))
+        except (OSError, ValueError):
+            continue
+        if kernel_tag in d.get("kernel", ""):
+            return {"bytes": round(d["traffic_bytes"]), "fetch": round(d["fetch_bytes_corrected"]),
+                    "write": round(d["write_bytes"]), "source": os.path.relpath(path, REPO)}
+    return None
+
+
 def cpu_baseline(arch, image_size, num_classes, seconds_budget=20.0):
     """Time the CPU oracle (restatement of reference src/train.py:train_epoch's step) on the host."""
     from oracle.vit_oracle import OneCycle, ViTConfig, init_params, loss_and_grads, sgd_step, tame_params
@@ -164,6 +181,7 @@ def main():
     imgs = args.steps * b * world
     value = imgs / dt
     fpi = train_flops_per_image(arch, args.image_size, args.num_classes)
+    traffic = pmc_traffic() if args.arch == "b16" and b == 256 else None
     step_tflops_per_gpu = value / world * fpi / 1e12
     out = {
         "metric": "images/sec training step, ViT-B/16 224px bf16, 1/2/4/8 MI355X" if args.arch == "b16" and
@@ -187,7 +205,9 @@ def main():
         "roofline": {"bound": "mfma", "kernel": "gemm fc1 fwd (bias + GELU + GELU' epilogue), "
                                                 f"M={T} N={cfg.mlp_dim} K={cfg.emb_dim}",
                      "achieved": round(fc1_tflops, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-                     "frac": round(fc1_tflops / PEAK_BF16_TFLOPS, 4), "traffic": None,
+                     "frac": round(fc1_tflops / PEAK_BF16_TFLOPS, 4), "traffic": (traffic or {}).get("bytes"),
+                     "traffic_detail": traffic,
+                     "algorithmic_bytes": T * cfg.emb_dim * 2 + cfg.mlp_dim * cfg.emb_dim * 2 + 2 * T * cfg.mlp_dim * 2,
                      "avg_launch_ms": round(fc1_ms, 4), "launches": len(probe)},
         "step_mfma_frac": round(step_tflops_per_gpu / PEAK_BF16_TFLOPS, 4),
         "train_gflop_per_image": round(fpi / 1e9, 3),
