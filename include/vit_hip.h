@@ -204,6 +204,24 @@ int vit_transpose_f32_bf16(const float* in, int64_t rows, int64_t cols, int64_t 
 /* y = a*x + b*y (f32), used for gradient scaling / accumulation. */
 int vit_axpby(const float* x, float* y, int64_t n, float a, float b, vit_stream_t stream);
 
+/* ------------------------------------------------------------------------------------------
+ * fp32 ("exact") forward: the reference's arithmetic (f32 operands, f32 accumulation) for the
+ * logits-parity gate and fp32 evaluation. Projections use vit_gemm_f32; LayerNorm
+ * vit_layernorm_fwd with y_f32 = 1.
+ * ---------------------------------------------------------------------------------------- */
+/* out f32 [B*N, Kpad]: as vit_im2col (src/model.py:179,197-200) without the bf16 rounding */
+int vit_im2col_f32(const float* x, float* out, int64_t B, int64_t img, int64_t P, int64_t Kpad,
+                   vit_stream_t stream);
+/* h[b*N+t] = (t == 0 ? cls : h[b*N+t]) + pos[t]   (src/model.py:203-204, :16-17) */
+int vit_embed_fwd_f32(float* h, int64_t B, int64_t N, int64_t D, const float* pos, const float* cls,
+                      vit_stream_t stream);
+/* out = 0.5 u (1 + erf(u / sqrt 2))   nn.GELU() src/model.py:33 */
+int vit_gelu_f32(const float* in, float* out, int64_t n, vit_stream_t stream);
+/* o = softmax((q k^T) * inv_sqrt_hd) v per (image, head), f32: qkv [B*N, 3, H, hd], o [B*N, H, hd]
+ * (SelfAttention.forward src/model.py:90-97) */
+int vit_attention_fwd_f32(const float* qkv, float* o, int64_t B, int64_t N, int64_t H, int64_t hd,
+                          float inv_sqrt_hd, vit_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

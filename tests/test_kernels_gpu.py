@@ -345,3 +345,27 @@ def test_gemm_gelu_dgelu_and_mul(tile):
     ops.gemm(Am, Bm, D, M, N, K, a_layout=K_CONTIG, b_layout=K_CONTIG, lda=lda, ldb=ldb, ldc=N,
              epilogue=EPI_MUL_BF16, aux=C, ldaux=N, tile=tile)
     assert rel(D.float(), (A.float() @ B.float()) * C.float()) < 5e-3
+
+
+@pytest.mark.parametrize("at,bt", [(False, False), (False, True), (True, False), (True, True)])
+def test_gemm_f32_layouts(at, bt):
+    M, N, K = 300, 200, 150
+    A = torch.randn(M, K, device=DEV)
+    B = torch.randn(K, N, device=DEV)
+    Am = A.t().contiguous() if at else A
+    Bm = B.t().contiguous() if bt else B
+    bias = torch.randn(N, device=DEV)
+    C = torch.randn(M, N, device=DEV)
+    C0 = C.clone()
+    ops.gemm_f32(M, N, K, Am, M if at else K, at, Bm, K if bt else N, bt, C, N, bias=bias, accumulate=True)
+    assert rel(C, C0 + A @ B + bias) < 1e-5
+
+
+def test_attention_fwd_f32():
+    B, N, H, hd = 2, 197, 3, 80
+    D = H * hd
+    qkv = torch.randn(B * N, 3 * D, device=DEV) * 1.5
+    o = torch.empty(B * N, D, device=DEV)
+    ops.attention_fwd_f32(qkv, o, B, N, H, hd, 1.0 / math.sqrt(hd))
+    ref, _ = _attn_ref(qkv, B, N, H, hd)
+    assert rel(o, ref) < 1e-5

@@ -178,3 +178,56 @@ def test_b16_full_gradients_match_oracle():
     assert rel(logits, ref_logits) < 1e-2
     assert abs(float(loss.detach()) - float(ref_loss)) <= 1e-3 * abs(float(ref_loss))
     check_grads(m, ref_grads)
+
+
+# ---- fp32 ("exact") forward: the north-star logits gate (<= 1e-3 relative) -----------------------
+H80 = ViTConfig(image_size=28, patch_size=14, emb_dim=320, mlp_dim=640, num_heads=4, num_layers=2, num_classes=10)
+
+
+@pytest.mark.parametrize("cfg,bs", [(TINY, 4), (SMALL, 3), (H80, 5)])
+def test_exact_forward_logits_within_1e3(cfg, bs):
+    params = tame_params(init_params(cfg, seed=42))
+    g = torch.Generator().manual_seed(7)
+    x = torch.randn(bs, 3, cfg.image_size, cfg.image_size, generator=g)
+    y = torch.randint(0, cfg.num_classes, (bs,), generator=g)
+    ref_logits, ref_loss, _ = loss_and_grads(params, x, y, cfg)
+    m = make_model(cfg, params)
+    m.precision = "fp32"
+    with torch.no_grad():
+        logits = m(x.cuda())
+    loss = torch.nn.functional.cross_entropy(logits, y.cuda())
+    assert rel(logits, ref_logits) < 1e-3, rel(logits, ref_logits)
+    assert abs(float(loss) - float(ref_loss)) <= 1e-3 * abs(float(ref_loss))
+
+
+def test_b16_exact_logits_match_reference_golden(golden_dir):
+    """ViT-B/16 @224 (tamed init, bs 2): fp32 forward vs the reference's own logits, gate 1e-3."""
+    z = np.load(os.path.join(golden_dir, "b16_tamed.npz"))
+    params = tame_params(init_params(B16, seed=42))
+    g = torch.Generator().manual_seed(int(z["input_seed"]))
+    x = torch.randn(2, 3, 224, 224, generator=g)
+    m = make_model(B16, params)
+    m.precision = "fp32"
+    with torch.no_grad():
+        logits = m(x.cuda())
+    loss = torch.nn.functional.cross_entropy(logits, torch.from_numpy(z["labels"]).cuda())
+    assert rel(logits, z["logits"]) < 1e-3, rel(logits, z["logits"])
+    assert abs(float(loss) - float(z["loss"])) <= 1e-3 * float(z["loss"])
+
+
+def test_bf16_step_head_dim_80():
+    """hd 80 (ViT-H/14's head size) through the bf16 training step vs the oracle."""
+    cfg, bs = H80, 4
+    params = tame_params(init_params(cfg, seed=42))
+    g = torch.Generator().manual_seed(8)
+    x = torch.randn(bs, 3, cfg.image_size, cfg.image_size, generator=g)
+    y = torch.randint(0, cfg.num_classes, (bs,), generator=g)
+    ref_logits, ref_loss, ref_grads = loss_and_grads(params, x, y, cfg)
+    m = make_model(cfg, params)
+    from vitmi.model import CrossEntropyLoss
+    logits = m(x.cuda())
+    loss = CrossEntropyLoss()(logits, y.cuda())
+    loss.backward()
+    assert rel(logits, ref_logits) < 1e-2
+    assert abs(float(loss.detach()) - float(ref_loss)) <= 1e-3 * abs(float(ref_loss))
+    check_grads(m, ref_grads)

@@ -580,3 +580,84 @@ extern "C" int vit_attention_bwd(const void* qkv, const void* o, const void* dou
   }
   return vit::check_hip(e, "vit_attention_bwd launch");
 }
+
+// ---- fp32 (exact) attention forward -------------------------------------------------------------
+// The reference's SelfAttention core (src/model.py:90-97) in f32 operands and f32 accumulation, for
+// the exact-parity forward (no bf16 anywhere): one query row per thread, keys streamed through LDS in
+// chunks of 32 with an online softmax; S = (q . k) / sqrt(hd), as the reference divides after the
+// matmul. qkv f32 [B*N, 3, H, hd] -> o f32 [B*N, H, hd].
+namespace {
+template <int HD>
+__global__ void __launch_bounds__(256) attn_fwd_f32_kernel(const float* __restrict__ qkv, float* __restrict__ o, int N,
+                                                           int H, int hd, float inv_sqrt) {
+  constexpr int KC = 32;
+  __shared__ float Ks[KC][HD + 1], Vs[KC][HD + 1];
+  const int bh = blockIdx.x, b = bh / H, h = bh % H;
+  const int D = H * hd;
+  const long rs = 3L * D;
+  const float* base = qkv + (long)b * N * rs + (long)h * hd;
+  const int qi = blockIdx.y * 256 + threadIdx.x;
+  const bool valid = qi < N;
+  float q[HD], acc[HD];
+#pragma unroll
+  for (int d = 0; d < HD; ++d) {
+    q[d] = (valid && d < hd) ? base[(long)qi * rs + d] : 0.f;
+    acc[d] = 0.f;
+  }
+  float m = -INFINITY, l = 0.f;
+  for (int k0 = 0; k0 < N; k0 += KC) {
+    __syncthreads();
+    for (int e = threadIdx.x; e < KC * HD; e += 256) {
+      const int j = e / HD, d = e % HD;
+      const bool ok = k0 + j < N && d < hd;
+      Ks[j][d] = ok ? base[(long)(k0 + j) * rs + D + d] : 0.f;
+      Vs[j][d] = ok ? base[(long)(k0 + j) * rs + 2 * D + d] : 0.f;
+    }
+    __syncthreads();
+    float s[KC];
+    float cm = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < KC; ++j) {
+      float dot = 0.f;
+#pragma unroll
+      for (int d = 0; d < HD; ++d) dot = fmaf(q[d], Ks[j][d], dot);
+      s[j] = k0 + j < N ? dot * inv_sqrt : -INFINITY;
+      cm = fmaxf(cm, s[j]);
+    }
+    const float mn = fmaxf(m, cm);
+    const float corr = expf(m - mn);
+    l *= corr;
+#pragma unroll
+    for (int d = 0; d < HD; ++d) acc[d] *= corr;
+#pragma unroll
+    for (int j = 0; j < KC; ++j) {
+      const float p = expf(s[j] - mn);
+      l += p;
+#pragma unroll
+      for (int d = 0; d < HD; ++d) acc[d] = fmaf(p, Vs[j][d], acc[d]);
+    }
+    m = mn;
+  }
+  if (valid) {
+    const float inv = 1.0f / l;
+    float* dst = o + ((long)b * N + qi) * D + (long)h * hd;
+#pragma unroll
+    for (int d = 0; d < HD; ++d)
+      if (d < hd) dst[d] = acc[d] * inv;
+  }
+}
+}  // namespace
+
+extern "C" int vit_attention_fwd_f32(const float* qkv, float* o, int64_t B, int64_t N, int64_t H, int64_t hd,
+                                     float inv_sqrt_hd, vit_stream_t stream) {
+  VIT_CHECK_ARG(qkv && o && B >= 1 && N >= 1 && H >= 1 && hd >= 1 && hd <= 96, "vit_attention_fwd_f32: bad args");
+  dim3 grid((unsigned)(B * H), (unsigned)((N + 255) / 256));
+  hipStream_t s = (hipStream_t)stream;
+  if (hd <= 32)
+    hipLaunchKernelGGL(attn_fwd_f32_kernel<32>, grid, dim3(256), 0, s, qkv, o, (int)N, (int)H, (int)hd, inv_sqrt_hd);
+  else if (hd <= 64)
+    hipLaunchKernelGGL(attn_fwd_f32_kernel<64>, grid, dim3(256), 0, s, qkv, o, (int)N, (int)H, (int)hd, inv_sqrt_hd);
+  else
+    hipLaunchKernelGGL(attn_fwd_f32_kernel<96>, grid, dim3(256), 0, s, qkv, o, (int)N, (int)H, (int)hd, inv_sqrt_hd);
+  return vit::check_hip(hipGetLastError(), "vit_attention_fwd_f32");
+}

@@ -7,7 +7,8 @@ namespace {
 
 // ---- im2col for Conv2d(3, D, k=P, s=P) (reference src/model.py:179,197-200) ----------------------
 // out[b*N + 1 + py*g + px][c*P*P + ky*P + kx] = x[b][c][py*P+ky][px*P+kx]; cls rows and pad cols = 0.
-__global__ void im2col_kernel(const float* __restrict__ x, bf16_t* __restrict__ out, int B, int img, int P, int Kpad) {
+template <typename OUT>
+__global__ void im2col_kernel(const float* __restrict__ x, OUT* __restrict__ out, int B, int img, int P, int Kpad) {
   const int g = img / P;
   const int N = g * g + 1;
   const long total = (long)B * N * Kpad;
@@ -23,7 +24,10 @@ __global__ void im2col_kernel(const float* __restrict__ x, bf16_t* __restrict__ 
       const int c = col / (P * P), rem = col % (P * P), ky = rem / P, kx = rem % P;
       v = x[(((long)b * 3 + c) * img + (py * P + ky)) * img + (px * P + kx)];
     }
-    out[i] = f2bf(v);
+    if constexpr (sizeof(OUT) == 2)
+      out[i] = f2bf(v);
+    else
+      out[i] = v;
   }
 }
 
@@ -126,32 +130,59 @@ __global__ void colsum_final_kernel(const float* __restrict__ partial, int chunk
   out[c] = accumulate ? out[c] + s : s;
 }
 
-// ---- small f32 GEMM (classifier head) -----------------------------------------------------------
-__global__ void gemm_f32_kernel(int M, int N, int K, const float* __restrict__ A, long lda, int at,
-                                const float* __restrict__ B, long ldb, int bt, float* __restrict__ C, long ldc,
-                                const float* __restrict__ bias, int accumulate) {
-  __shared__ float As[16][17], Bs[16][17];
-  const int tx = threadIdx.x, ty = threadIdx.y;
-  const int m = blockIdx.y * 16 + ty, n = blockIdx.x * 16 + tx;
-  float acc = 0.f;
+// ---- f32 GEMM: classifier head of the bf16 step, and every projection of the fp32 (exact) forward.
+// 64 x 64 tile per 256-thread workgroup, 4 x 4 outputs per thread, k-tiles of 16 staged in LDS
+// (f32 operands, f32 accumulation: the reference's fp32 arithmetic, no bf16 rounding anywhere).
+__global__ void __launch_bounds__(256) gemm_f32_kernel(int M, int N, int K, const float* __restrict__ A, long lda,
+                                                       int at, const float* __restrict__ B, long ldb, int bt,
+                                                       float* __restrict__ C, long ldc, const float* __restrict__ bias,
+                                                       int accumulate) {
+  __shared__ float As[16][68], Bs[16][68];  // [k][m], [k][n]
+  const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
+  const int m0 = blockIdx.y * 64, n0 = blockIdx.x * 64;
+  float acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = 0.f;
   for (int k0 = 0; k0 < K; k0 += 16) {
-    {  // A tile: As[ty][tx] = A(m0+ty, k0+tx)
-      const int mm = blockIdx.y * 16 + ty, kk = k0 + tx;
-      As[ty][tx] = (mm < M && kk < K) ? (at ? A[(long)kk * lda + mm] : A[(long)mm * lda + kk]) : 0.f;
-    }
-    {  // B tile: Bs[ty][tx] = B(k0+ty, n0+tx)
-      const int kk = k0 + ty, nn = blockIdx.x * 16 + tx;
-      Bs[ty][tx] = (kk < K && nn < N) ? (bt ? B[(long)nn * ldb + kk] : B[(long)kk * ldb + nn]) : 0.f;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int idx = tid + e * 256;
+      int m, k;
+      if (at) { k = idx >> 6; m = idx & 63; } else { m = idx >> 4; k = idx & 15; }
+      const int gm = m0 + m, gk = k0 + k;
+      As[k][m] = (gm < M && gk < K) ? (at ? A[(long)gk * lda + gm] : A[(long)gm * lda + gk]) : 0.f;
+      int n, kb;
+      if (bt) { n = idx >> 4; kb = idx & 15; } else { kb = idx >> 6; n = idx & 63; }
+      const int gn = n0 + n, gkb = k0 + kb;
+      Bs[kb][n] = (gn < N && gkb < K) ? (bt ? B[(long)gn * ldb + gkb] : B[(long)gkb * ldb + gn]) : 0.f;
     }
     __syncthreads();
 #pragma unroll
-    for (int k = 0; k < 16; ++k) acc += As[ty][k] * Bs[k][tx];
+    for (int k = 0; k < 16; ++k) {
+      const float4 a = *reinterpret_cast<const float4*>(&As[k][ty * 4]);
+      const float4 b = *reinterpret_cast<const float4*>(&Bs[k][tx * 4]);
+      const float av[4] = {a.x, a.y, a.z, a.w}, bv[4] = {b.x, b.y, b.z, b.w};
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = fmaf(av[i], bv[j], acc[i][j]);
+    }
     __syncthreads();
   }
-  if (m < M && n < N) {
-    float v = acc + (bias ? bias[n] : 0.f);
-    float* dst = C + (long)m * ldc + n;
-    *dst = accumulate ? *dst + v : v;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int m = m0 + ty * 4 + i;
+    if (m >= M) continue;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int n = n0 + tx * 4 + j;
+      if (n >= N) continue;
+      const float v = acc[i][j] + (bias ? bias[n] : 0.f);
+      float* dst = C + (long)m * ldc + n;
+      *dst = accumulate ? *dst + v : v;
+    }
   }
 }
 
@@ -262,7 +293,7 @@ extern "C" int vit_im2col(const float* x, void* out, int64_t B, int64_t img, int
                           vit_stream_t stream) {
   VIT_CHECK_ARG(x && out && B > 0 && P > 0 && img >= P && Kpad >= 3 * P * P, "vit_im2col: bad args");
   const int64_t g = img / P, N = g * g + 1;
-  hipLaunchKernelGGL(im2col_kernel, dim3(grid_for(B * N * Kpad)), dim3(256), 0, (hipStream_t)stream, x, (bf16_t*)out,
+  hipLaunchKernelGGL(im2col_kernel<bf16_t>, dim3(grid_for(B * N * Kpad)), dim3(256), 0, (hipStream_t)stream, x, (bf16_t*)out,
                      (int)B, (int)img, (int)P, (int)Kpad);
   VIT_LAUNCH_CHECK("vit_im2col");
 }
@@ -346,7 +377,7 @@ extern "C" int vit_gemm_f32(int64_t M, int64_t N, int64_t K, const float* A, int
                             int32_t accumulate, vit_stream_t stream) {
   VIT_CHECK_ARG(A && B && C && M >= 0 && N >= 0 && K >= 0, "vit_gemm_f32: bad args");
   if (M == 0 || N == 0) return VIT_OK;
-  dim3 grid((unsigned)((N + 15) / 16), (unsigned)((M + 15) / 16)), block(16, 16);
+  dim3 grid((unsigned)((N + 63) / 64), (unsigned)((M + 63) / 64)), block(256);
   hipLaunchKernelGGL(gemm_f32_kernel, grid, block, 0, (hipStream_t)stream, (int)M, (int)N, (int)K, A, (long)lda,
                      (int)a_trans, B, (long)ldb, (int)b_trans, C, (long)ldc, bias, (int)accumulate);
   VIT_LAUNCH_CHECK("vit_gemm_f32");
@@ -466,4 +497,50 @@ extern "C" int vit_transpose_f32_bf16(const float* in, int64_t rows, int64_t col
   hipLaunchKernelGGL(transpose_f32_bf16_kernel, grid, dim3(256), 0, (hipStream_t)stream, in, (long)ldi, (int)rows,
                      (int)cols, (bf16_t*)out, (long)ldo, (long)in_batch_stride, (long)out_batch_stride);
   VIT_LAUNCH_CHECK("vit_transpose_f32_bf16");
+}
+
+
+// ---- fp32 (exact) forward helpers -----------------------------------------------------------------
+namespace {
+// h[b*N + t] = (t == 0 ? cls : h[b*N + t]) + pos[t]  (src/model.py:203-204, PositionEmbs :16-17)
+__global__ void embed_fwd_kernel(float* __restrict__ h, int B, int N, int D, const float* __restrict__ pos,
+                                 const float* __restrict__ cls) {
+  const long total = (long)B * N * D;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int d = (int)(i % D);
+    const int t = (int)((i / D) % N);
+    h[i] = (t == 0 ? cls[d] : h[i]) + pos[(long)t * D + d];
+  }
+}
+// exact-erf GELU, nn.GELU() (src/model.py:33)
+__global__ void gelu_f32_kernel(const float* __restrict__ in, float* __restrict__ out, long n) {
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const float u = in[i];
+    out[i] = 0.5f * u * (1.0f + erff(u * 0.70710678118654752f));
+  }
+}
+}  // namespace
+
+extern "C" int vit_im2col_f32(const float* x, float* out, int64_t B, int64_t img, int64_t P, int64_t Kpad,
+                              vit_stream_t stream) {
+  VIT_CHECK_ARG(x && out && B > 0 && P > 0 && img >= P && Kpad >= 3 * P * P, "vit_im2col_f32: bad args");
+  const int64_t g = img / P, N = g * g + 1;
+  hipLaunchKernelGGL(im2col_kernel<float>, dim3(grid_for(B * N * Kpad)), dim3(256), 0, (hipStream_t)stream, x, out,
+                     (int)B, (int)img, (int)P, (int)Kpad);
+  VIT_LAUNCH_CHECK("vit_im2col_f32");
+}
+
+extern "C" int vit_embed_fwd_f32(float* h, int64_t B, int64_t N, int64_t D, const float* pos, const float* cls,
+                                 vit_stream_t stream) {
+  VIT_CHECK_ARG(h && pos && cls && B > 0 && N > 0 && D > 0, "vit_embed_fwd_f32: bad args");
+  hipLaunchKernelGGL(embed_fwd_kernel, dim3(grid_for(B * N * D)), dim3(256), 0, (hipStream_t)stream, h, (int)B,
+                     (int)N, (int)D, pos, cls);
+  VIT_LAUNCH_CHECK("vit_embed_fwd_f32");
+}
+
+extern "C" int vit_gelu_f32(const float* in, float* out, int64_t n, vit_stream_t stream) {
+  VIT_CHECK_ARG(in && out && n >= 0, "vit_gelu_f32: bad args");
+  if (n == 0) return VIT_OK;
+  hipLaunchKernelGGL(gelu_f32_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, in, out, (long)n);
+  VIT_LAUNCH_CHECK("vit_gelu_f32");
 }

@@ -64,6 +64,10 @@ _SIGS = {
     "vit_pack_cols": (c_i32, [c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp, c_i64, c_i32, c_vp]),
     "vit_transpose_f32_bf16": (c_i32, [c_vp, c_i64, c_i64, c_i64, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp]),
     "vit_colsum3": (c_i32, [c_vp, c_i32, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_i32, c_vp]),
+    "vit_im2col_f32": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp]),
+    "vit_embed_fwd_f32": (c_i32, [c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp]),
+    "vit_gelu_f32": (c_i32, [c_vp, c_vp, c_i64, c_vp]),
+    "vit_attention_fwd_f32": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_f32, c_vp]),
 }
 
 EXPORTED = tuple(_SIGS)

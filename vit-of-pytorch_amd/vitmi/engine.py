@@ -355,6 +355,51 @@ class ViTEngine:
         self._last_b = b
         return a.logits
 
+    # ---- fp32 ("exact") forward -------------------------------------------------------------------
+    def forward_exact(self, x: torch.Tensor):
+        """The forward in the reference's own arithmetic: f32 operands and f32 accumulation in every
+        projection (vit_gemm_f32), f32 attention and exact-erf GELU, f32 LayerNorm outputs; no bf16
+        rounding anywhere. Forward only (logits-parity gate, fp32 evaluation); keeps no activations.
+        x: [b, 3, img, img] -> logits [b, C] f32 (a fresh tensor)."""
+        cfg = self.cfg
+        if x.dim() != 4 or x.shape[1] != 3 or x.shape[2] != cfg.image_size or x.shape[3] != cfg.image_size:
+            raise ValueError(f"expected input [b, 3, {cfg.image_size}, {cfg.image_size}], got {tuple(x.shape)}")
+        x = x.to(self.dev, torch.float32).contiguous()
+        b = x.shape[0]
+        D, M, H, N, L, C = cfg.emb_dim, cfg.mlp_dim, cfg.num_heads, cfg.tokens, cfg.num_layers, cfg.num_classes
+        hd = D // H
+        T, kp = b * N, cfg.patch_k
+        f = self.flat
+        e = lambda *shape: torch.empty(*shape, device=self.dev)
+        fv = lambda name: f[self.off(name):]
+        patches = e(T, kp)
+        ops.im2col_f32(x, patches, b, cfg.image_size, cfg.patch_size, kp)
+        h = e(T, D)
+        # Conv2d(k = s = P) as patches x W^T (W [D][3 P^2]), then cls row and position embedding
+        ops.gemm_f32(T, D, kp, patches, kp, False, fv("embedding.weight"), kp, True, h, D, bias=fv("embedding.bias"))
+        ops.embed_fwd_f32(h, b, N, D, fv("transformer.pos_embedding.pos_embedding"), fv("cls_token"))
+        y, qkv, o, u = e(T, D), e(T, 3 * D), e(T, D), e(T, M)
+        mu, rs = e(T), e(T)
+        for i in range(L):
+            ln = lambda s: fv(self.lname(i, s))
+            ops.layernorm_fwd(h, D, ln("norm1.weight"), ln("norm1.bias"), y, D, mu, rs, T, D)
+            for z, w in enumerate(("query", "key", "value")):   # LinearGeneral: W [D][H,hd] (in x out)
+                ops.gemm_f32(T, D, D, y, D, False, ln(f"attn.{w}.weight"), D, False, qkv[:, z * D:], 3 * D,
+                             bias=ln(f"attn.{w}.bias"))
+            ops.attention_fwd_f32(qkv, o, b, N, H, hd, 1.0 / math.sqrt(hd))
+            ops.gemm_f32(T, D, D, o, D, False, ln("attn.out.weight"), D, False, h, D, bias=ln("attn.out.bias"),
+                         accumulate=True)                        # h += out(attn) (src/model.py:124)
+            ops.layernorm_fwd(h, D, ln("norm2.weight"), ln("norm2.bias"), y, D, mu, rs, T, D)
+            ops.gemm_f32(T, M, D, y, D, False, ln("mlp.fc1.weight"), D, True, u, M, bias=ln("mlp.fc1.bias"))
+            ops.gelu_f32(u, u, T * M)
+            ops.gemm_f32(T, D, M, u, M, False, ln("mlp.fc2.weight"), M, True, h, D, bias=ln("mlp.fc2.bias"),
+                         accumulate=True)                        # h += mlp(ln2(h)) (src/model.py:129)
+        lncls = e(b, D)
+        ops.layernorm_fwd(h, N * D, fv("transformer.norm.weight"), fv("transformer.norm.bias"), lncls, D, mu, rs, b, D)
+        logits = e(b, C)
+        ops.gemm_f32(b, C, D, lncls, D, False, fv("classifier.weight"), D, True, logits, C, bias=fv("classifier.bias"))
+        return logits
+
     # ---- loss ------------------------------------------------------------------------------------
     def cross_entropy(self, labels: torch.Tensor, grad_scale: float | None = None):
         """Fused CE on the last logits: fills dlogits (scaled by grad_scale, default 1/b) and

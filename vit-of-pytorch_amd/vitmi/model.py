@@ -172,6 +172,10 @@ class VisionTransformer(nn.Module):
                                num_layers=num_layers, num_classes=num_classes)
         self.dropout_rate = dropout_rate
         self.attn_dropout_rate = attn_dropout_rate
+        # "bf16": the training path (bf16 MFMA operands, fp32 accumulation, autograd through the HIP
+        # engine). "fp32": forward-only in the reference's own arithmetic (f32 operands everywhere),
+        # for the logits-parity gate and fp32 evaluation; its output carries no autograd graph.
+        self.precision = "bf16"
         self._engine = None
         self._flat_names = None
         self._flat_params = None
@@ -226,6 +230,13 @@ class VisionTransformer(nn.Module):
             raise NotImplementedError("dropout > 0 is not implemented on the MI355X path yet (presets use 0.0, "
                                       "reference src/config.py:64-65)")
         eng = self.engine()
+        if self.precision == "fp32":
+            if torch.is_grad_enabled() and any(p.requires_grad for p in self._flat_params):
+                raise RuntimeError("precision='fp32' is the forward-only exact path; run it under torch.no_grad() "
+                                   "(training uses precision='bf16')")
+            return eng.forward_exact(x)
+        if self.precision != "bf16":
+            raise ValueError(f"unknown precision {self.precision!r} (bf16 | fp32)")
         sig = self._version_sig()
         if eng._mirror_sig != sig:
             eng.refresh_mirror()

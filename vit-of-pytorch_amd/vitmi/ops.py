@@ -170,3 +170,24 @@ def colsum3(inp, rows, seg, ld, partial, out0, out1, out2, accumulate=False):
     """column sums of a [rows][3*seg] matrix, segment k -> out_k (q|k|v bias gradients)."""
     check(lib().vit_colsum3(_p(inp), int(inp.dtype == BF16), rows, seg, ld, _p(partial), _p(out0), _p(out1), _p(out2),
                             int(accumulate), _stream()), "vit_colsum3")
+
+
+# ---- fp32 (exact) forward ---------------------------------------------------------------------
+def im2col_f32(x, out, B, img, P, Kpad):
+    _chk(x, F32, "x")
+    _chk(out, F32, "out")
+    check(lib().vit_im2col_f32(_p(x), _p(out), B, img, P, Kpad, _stream()), "vit_im2col_f32")
+
+
+def embed_fwd_f32(h, B, N, D, pos, cls):
+    check(lib().vit_embed_fwd_f32(_p(h), B, N, D, _p(pos), _p(cls), _stream()), "vit_embed_fwd_f32")
+
+
+def gelu_f32(inp, out, n):
+    check(lib().vit_gelu_f32(_p(inp), _p(out), n, _stream()), "vit_gelu_f32")
+
+
+def attention_fwd_f32(qkv, o, B, N, H, hd, inv_sqrt_hd):
+    _chk(qkv, F32, "qkv")
+    _chk(o, F32, "o")
+    check(lib().vit_attention_fwd_f32(_p(qkv), _p(o), B, N, H, hd, inv_sqrt_hd, _stream()), "vit_attention_fwd_f32")
