@@ -369,3 +369,23 @@ def test_attention_fwd_f32():
     ops.attention_fwd_f32(qkv, o, B, N, H, hd, 1.0 / math.sqrt(hd))
     ref, _ = _attn_ref(qkv, B, N, H, hd)
     assert rel(o, ref) < 1e-5
+
+
+@pytest.mark.parametrize("epi,K", [(EPI_BF16, 64), (EPI_BIAS_RESID_F32, 2048)])
+def test_gemm_wave_split_rows(epi, K):
+    """M = 50 432, N = 768 (591 tiles of 256x256 = 2.3 waves): the auto path splits the rows between the
+    256x256 kernel (whole waves) and 128x128 tiles; every row must come out right."""
+    M, N = 50432, 768
+    A, B, Am, Bm, lda, ldb = _mats(M, N, K, K_CONTIG, K_CONTIG, ints=True)
+    ref = A.double() @ B.double()
+    if epi == EPI_BF16:
+        C = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+        ops.gemm(Am, Bm, C, M, N, K, a_layout=K_CONTIG, b_layout=K_CONTIG, lda=lda, ldb=ldb, ldc=N, epilogue=epi)
+        assert torch.equal(C.double(), ref.bfloat16().double())
+    else:
+        bias = torch.randint(-3, 4, (N,), device=DEV).float()
+        R = torch.randint(-9, 10, (M, N), device=DEV).float()
+        C = R.clone()
+        ops.gemm(Am, Bm, C, M, N, K, a_layout=K_CONTIG, b_layout=K_CONTIG, lda=lda, ldb=ldb, ldc=N, epilogue=epi,
+                 bias=bias, aux=C, ldaux=N)
+        assert torch.equal(C.double(), ref + bias.double() + R.double())

@@ -1,3 +1,3 @@
 set -e
-timeout -k 10 400 python -u tools/gemm_bench.py --tiles 3,5,9 --shapes fc2dgk:9/5,fc1:8/3 --rounds 3 > gpurun_out/gemm_epi89.log 2>&1
-cat gpurun_out/gemm_epi89.log
+timeout -k 10 400 python -u tools/gemm_bench.py --tiles 0,9 --shapes fc1dgk:1,outk:1,qkvdg:1,fc2:4,fc1:8 --rounds 3 > gpurun_out/gemm_split.log 2>&1
+cat gpurun_out/gemm_split.log

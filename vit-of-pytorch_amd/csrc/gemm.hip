@@ -881,26 +881,64 @@ extern "C" int vit_gemm_bf16(const vit_gemm_args* a, vit_stream_t stream) {
   }
   hipStream_t s = (hipStream_t)stream;
   const int batch = (int)a->batch, split = (int)a->split_k;
-  hipError_t e;
   const int cfg = pick_tile(a);
   VIT_CHECK_ARG(cfg >= 0 && cfg <= 9, "vit_gemm_bf16: bad tile config %d", cfg);
   VIT_CHECK_ARG(cfg != 1 || a->K % 32 == 0, "vit_gemm_bf16: K");
-  switch (a->epilogue) {
-    case VIT_EPI_F32: e = launch_layout<VIT_EPI_F32>(cfg, d, ak, bk, batch, split, s); break;
-    case VIT_EPI_BF16: e = launch_layout<VIT_EPI_BF16>(cfg, d, ak, bk, batch, split, s); break;
-    case VIT_EPI_BIAS_BF16: e = launch_layout<VIT_EPI_BIAS_BF16>(cfg, d, ak, bk, batch, split, s); break;
-    case VIT_EPI_BIAS_GELU: e = launch_layout<VIT_EPI_BIAS_GELU>(cfg, d, ak, bk, batch, split, s); break;
-    case VIT_EPI_BIAS_RESID_F32: e = launch_layout<VIT_EPI_BIAS_RESID_F32>(cfg, d, ak, bk, batch, split, s); break;
-    case VIT_EPI_GELU_BWD: e = launch_layout<VIT_EPI_GELU_BWD>(cfg, d, ak, bk, batch, split, s); break;
-    case VIT_EPI_BIAS_GELU_DGELU:
-      e = launch_layout<VIT_EPI_BIAS_GELU_DGELU>(cfg, d, ak, bk, batch, split, s);
-      break;
-    case VIT_EPI_MUL_BF16: e = launch_layout<VIT_EPI_MUL_BF16>(cfg, d, ak, bk, batch, split, s); break;
-    case VIT_EPI_PATCH: e = launch_layout<VIT_EPI_PATCH>(cfg, d, ak, bk, batch, split, s); break;
-    case VIT_EPI_SPLITK: e = launch_layout<VIT_EPI_SPLITK>(cfg, d, ak, bk, batch, split, s); break;
-    default: vit::set_error("vit_gemm_bf16: unknown epilogue %d", a->epilogue); return VIT_ERR_INVALID_ARG;
+  auto run = [&](int c, const GemmDev& g) -> hipError_t {
+    switch (a->epilogue) {
+      case VIT_EPI_F32: return launch_layout<VIT_EPI_F32>(c, g, ak, bk, batch, split, s);
+      case VIT_EPI_BF16: return launch_layout<VIT_EPI_BF16>(c, g, ak, bk, batch, split, s);
+      case VIT_EPI_BIAS_BF16: return launch_layout<VIT_EPI_BIAS_BF16>(c, g, ak, bk, batch, split, s);
+      case VIT_EPI_BIAS_GELU: return launch_layout<VIT_EPI_BIAS_GELU>(c, g, ak, bk, batch, split, s);
+      case VIT_EPI_BIAS_RESID_F32: return launch_layout<VIT_EPI_BIAS_RESID_F32>(c, g, ak, bk, batch, split, s);
+      case VIT_EPI_GELU_BWD: return launch_layout<VIT_EPI_GELU_BWD>(c, g, ak, bk, batch, split, s);
+      case VIT_EPI_BIAS_GELU_DGELU: return launch_layout<VIT_EPI_BIAS_GELU_DGELU>(c, g, ak, bk, batch, split, s);
+      case VIT_EPI_MUL_BF16: return launch_layout<VIT_EPI_MUL_BF16>(c, g, ak, bk, batch, split, s);
+      case VIT_EPI_PATCH: return launch_layout<VIT_EPI_PATCH>(c, g, ak, bk, batch, split, s);
+      case VIT_EPI_SPLITK: return launch_layout<VIT_EPI_SPLITK>(c, g, ak, bk, batch, split, s);
+      default: return hipErrorInvalidValue;
+    }
+  };
+  if (a->epilogue < 0 || a->epilogue > VIT_EPI_MUL_BF16) {
+    vit::set_error("vit_gemm_bf16: unknown epilogue %d", a->epilogue);
+    return VIT_ERR_INVALID_ARG;
   }
-  return vit::check_hip(e, "vit_gemm_bf16 launch");
+  // Wave quantisation of the one-workgroup-per-CU 256 x 256 kernels: when the last wave of tiles
+  // would run less than half full (M = 50 432, N = 768: 591 tiles = 2.3 waves on 256 CUs), the
+  // rows that fill whole waves run on them and the remaining rows on 128 x 128 tiles (several
+  // workgroups per CU), ~2.4 instead of 3 wave-times. Row-local epilogues only.
+  if ((cfg == 5 || cfg == 9) && batch == 1 && split == 1 && !a->col_partial && a->epilogue != VIT_EPI_PATCH &&
+      a->tile == 0) {
+    static const int ncu = [] {
+      int dev = 0, n = 0;
+      if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                                 hipSuccess)
+        return 0;
+      return n;
+    }();
+    const long tiles_n = (a->N + 255) / 256, tiles = ((a->M + 255) / 256) * tiles_n;
+    if (ncu > 0) {
+      const long full = tiles / ncu, rem = tiles - full * ncu;
+      const long main_rows = (full * ncu / tiles_n) * 256;
+      if (full >= 1 && rem > 0 && 2 * rem <= ncu && main_rows > 0 && main_rows < a->M) {
+        GemmDev g1 = d, g2 = d;
+        g1.M = (int)main_rows;
+        g2.M = (int)(a->M - main_rows);
+        const long r0 = main_rows;
+        const long a_off = ak ? r0 * a->lda * 2 : r0 * 2;
+        g2.A = d.A + a_off;
+        g2.a_bytes = d.a_bytes > a_off ? (uint32_t)(d.a_bytes - a_off) : 0u;
+        const int csz = (a->epilogue == VIT_EPI_F32 || a->epilogue == VIT_EPI_BIAS_RESID_F32) ? 4 : 2;
+        g2.C = (char*)d.C + r0 * a->ldc * csz;
+        if (d.C2) g2.C2 = (char*)d.C2 + r0 * a->ldc2 * 2;
+        if (d.aux) g2.aux = (const char*)d.aux + r0 * a->ldaux * (a->epilogue == VIT_EPI_BIAS_RESID_F32 ? 4 : 2);
+        hipError_t e = run(cfg, g1);
+        if (e == hipSuccess) e = run(0, g2);
+        return vit::check_hip(e, "vit_gemm_bf16 launch");
+      }
+    }
+  }
+  return vit::check_hip(run(cfg, d), "vit_gemm_bf16 launch");
 }
 
 // ---- split-K reduction -------------------------------------------------------------------------
