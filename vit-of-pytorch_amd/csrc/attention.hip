@@ -97,6 +97,10 @@ __device__ __forceinline__ v8bf pack8(const v4f& a, const v4f& b) {
   return __builtin_bit_cast(v8bf, r);
 }
 
+// 2^x on the transcendental unit (bare v_exp_f32). Arguments are s*log2e - lse <= ~0, so results
+// only underflow (to 0) for keys whose softmax weight is below f32 resolution anyway.
+__device__ __forceinline__ float ex2(float x) { return __builtin_amdgcn_exp2f(x); }
+
 __device__ __forceinline__ v4f mfma(const v8bf& a, const v8bf& b, const v4f& c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
@@ -106,6 +110,17 @@ __device__ __forceinline__ void store4(bf16_t* dst, const v4f& v, float s) {
   u.x = pack2bf(v[0] * s, v[1] * s);
   u.y = pack2bf(v[2] * s, v[3] * s);
   *reinterpret_cast<uint2*>(dst) = u;
+}
+
+// Global row fragment (16 rows x 32 k, MFMA operand layout) straight to registers: lane (g, i) gets
+// row r0 + i, columns kk*32 + 8g .. +7; rows >= N and columns >= hd read as zero.
+template <int HD>
+__device__ __forceinline__ v8bf gl_row(const bf16_t* __restrict__ src, long row_stride, int r0, int kk, int N, int hd,
+                                       int lane) {
+  const int row = r0 + (lane & 15), col = kk * 32 + 8 * (lane >> 4);
+  v8s v = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (row < N && col < hd) v = *reinterpret_cast<const v8s*>(src + (long)row * row_stride + col);
+  return __builtin_bit_cast(v8bf, v);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -128,15 +143,17 @@ __global__ void __launch_bounds__(NW * 64) attn_fwd_kernel(const bf16_t* __restr
   const int g = lane >> 4, i = lane & 15;
   const float c = scale * LOG2E;
   const int nqt = (N + 15) / 16;
+  // Q fragments come straight from HBM; the next strip's are requested before this strip's math
+  v8bf qn[HD / 32];
+#pragma unroll
+  for (int kk = 0; kk < HD / 32; ++kk) qn[kk] = gl_row<HD>(base, rs, wave * 16, kk, N, hd, lane);
   for (int qt = wave; qt < nqt; qt += NW) {
     const int q = qt * 16 + i;
     v8bf qf[HD / 32];
 #pragma unroll
     for (int kk = 0; kk < HD / 32; ++kk) {
-      v8s v = {0, 0, 0, 0, 0, 0, 0, 0};
-      const int d = kk * 32 + 8 * g;
-      if (q < N && d < hd) v = *reinterpret_cast<const v8s*>(base + (long)q * rs + d);
-      qf[kk] = __builtin_bit_cast(v8bf, v);
+      qf[kk] = qn[kk];
+      qn[kk] = gl_row<HD>(base, rs, (qt + NW) * 16, kk, N, hd, lane);  // rows >= N read as zero
     }
     v4f s[NKT];
 #pragma unroll
@@ -163,7 +180,7 @@ __global__ void __launch_bounds__(NW * 64) attn_fwd_kernel(const bf16_t* __restr
     for (int kt = 0; kt < NKT; ++kt)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float p = exp2f(s[kt][r] * c - mc);
+        const float p = ex2(s[kt][r] * c - mc);
         s[kt][r] = p;
         l += p;
       }
@@ -192,17 +209,6 @@ __device__ __forceinline__ float sum16(float v) {
   return v;
 }
 
-// Global row fragment (16 rows x 32 k, MFMA operand layout) straight to registers: lane (g, i) gets
-// row r0 + i, columns kk*32 + 8g .. +7; rows >= N and columns >= hd read as zero.
-template <int HD>
-__device__ __forceinline__ v8bf gl_row(const bf16_t* __restrict__ src, long row_stride, int r0, int kk, int N, int hd,
-                                       int lane) {
-  const int row = r0 + (lane & 15), col = kk * 32 + 8 * (lane >> 4);
-  v8s v = {0, 0, 0, 0, 0, 0, 0, 0};
-  if (row < N && col < hd) v = *reinterpret_cast<const v8s*>(src + (long)row * row_stride + col);
-  return __builtin_bit_cast(v8bf, v);
-}
-
 // ------------------------------------------------------------------------------------------------
 // Backward, two LDS images at a time (56 KB at N = 197, hd = 64: two workgroups per CU, so one
 // workgroup's image loads overlap the other's MFMA work).
@@ -220,7 +226,7 @@ __global__ void __launch_bounds__(NW * 64, 2) attn_bwd_kernel(const bf16_t* __re
                                                               const bf16_t* __restrict__ dout,
                                                               const float* __restrict__ lse, bf16_t* __restrict__ dqkv,
                                                               float* __restrict__ bias_partial, int N, int H, int hd,
-                                                              float scale) {
+                                                              float scale, int stages) {
   constexpr int NP = NKT * 16;
   constexpr int IMG = NP * HD * 2;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -238,7 +244,10 @@ __global__ void __launch_bounds__(NW * 64, 2) attn_bwd_kernel(const bf16_t* __re
   bf16_t* dq_base = dqkv + (long)b * N * rs + (long)h * hd;
 
   load_images<HD, NP, NW * 64>(ImA, base + D, rs, ImB, base + 2 * D, rs, N, hd);
-  for (int r = threadIdx.x; r < NP; r += blockDim.x) lse_s[r] = r < N ? lse[(long)bh * N + r] * LOG2E : INFINITY;
+  for (int r = threadIdx.x; r < NP; r += blockDim.x) {
+    lse_s[r] = r < N ? lse[(long)bh * N + r] * LOG2E : INFINITY;  // padded queries: P = 2^-inf = 0
+    dlt_s[r] = 0.f;
+  }
   __syncthreads();
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -251,122 +260,227 @@ __global__ void __launch_bounds__(NW * 64, 2) attn_bwd_kernel(const bf16_t* __re
 #pragma unroll
     for (int r = 0; r < 4; ++r) bq[dt][r] = bk[dt][r] = bv[dt][r] = 0.f;
 
-  // ---- stage 1: delta and dQ, query-tile pairs ----
-  for (int qp = wave; qp < npair; qp += NW) {
-    v8bf qf[2][HD / 32], df[2][HD / 32];
-    float ls[2], dl[2] = {0.f, 0.f};
+  // ---- stage 1: delta and dQ ----
+  if (!(stages & 1)) {
+  } else if constexpr (HD <= 64) {
+    // one 16-query strip at a time with P and dP of ALL keys kept in registers (2 x NKT x 4 f32):
+    // delta = sum_j P dP comes out of the same pass, so dS and dQ need no recompute of S / dP
+    const int nqt = (N + 15) / 16;
+    v8bf qn[HD / 32], dn[HD / 32];  // next strip's Q / dO rows, requested one strip ahead
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-#pragma unroll
-      for (int kk = 0; kk < HD / 32; ++kk) {
-        qf[u][kk] = gl_row<HD>(base, rs, (2 * qp + u) * 16, kk, N, hd, lane);
-        df[u][kk] = gl_row<HD>(dob, D, (2 * qp + u) * 16, kk, N, hd, lane);
-      }
-      ls[u] = lse_s[(2 * qp + u) * 16 + i];
+    for (int kk = 0; kk < HD / 32; ++kk) {
+      qn[kk] = gl_row<HD>(base, rs, wave * 16, kk, N, hd, lane);
+      dn[kk] = gl_row<HD>(dob, D, wave * 16, kk, N, hd, lane);
     }
-    // pass A: delta
-    for (int kt = 0; kt < 2 * npair; ++kt) {
-      v8bf kr[HD / 32], vr[HD / 32];
+    for (int qt = wave; qt < nqt; qt += NW) {
+      v8bf qf[HD / 32], df[HD / 32];
 #pragma unroll
       for (int kk = 0; kk < HD / 32; ++kk) {
-        kr[kk] = rd_row<HD>(ImA, kt * 16, kk, lane);
-        vr[kk] = rd_row<HD>(ImB, kt * 16, kk, lane);
+        qf[kk] = qn[kk];
+        df[kk] = dn[kk];
+        qn[kk] = gl_row<HD>(base, rs, (qt + NW) * 16, kk, N, hd, lane);
+        dn[kk] = gl_row<HD>(dob, D, (qt + NW) * 16, kk, N, hd, lane);
       }
+      const float ls = lse_s[qt * 16 + i];
+      v4f P[NKT], DP[NKT];
+      float dl = 0.f;
 #pragma unroll
-      for (int u = 0; u < 2; ++u) {
+      for (int kt = 0; kt < NKT; ++kt) {
+        if (kt == NKT - 1 && kt * 16 >= N) {  // a wholly padded last key tile (N % 32 in 1..16)
+          P[kt] = DP[kt] = v4f{0.f, 0.f, 0.f, 0.f};
+          continue;
+        }
         v4f st = {0.f, 0.f, 0.f, 0.f}, dpt = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int kk = 0; kk < HD / 32; ++kk) {
-          st = mfma(kr[kk], qf[u][kk], st);
-          dpt = mfma(vr[kk], df[u][kk], dpt);
+          st = mfma(rd_row<HD>(ImA, kt * 16, kk, lane), qf[kk], st);
+          dpt = mfma(rd_row<HD>(ImB, kt * 16, kk, lane), df[kk], dpt);
         }
+        const bool full = (kt + 1) * 16 <= N;  // wave-uniform: only the last tiles hold padded keys
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int key = kt * 16 + 4 * g + r;
-          if (key < N) dl[u] += exp2f(st[r] * c - ls[u]) * dpt[r];
+          float pv = ex2(st[r] * c - ls);
+          if (!full && kt * 16 + 4 * g + r >= N) pv = 0.f;
+          P[kt][r] = pv;
+          dl += pv * dpt[r];
         }
+        DP[kt] = dpt;
       }
-    }
+      dl += __shfl_xor(dl, 16, 64);
+      dl += __shfl_xor(dl, 32, 64);
+      const int q = qt * 16 + i;
+      if (q >= N) dl = 0.f;
+      if (g == 0) dlt_s[q] = dl;
+      v4f dq[HD / 16];
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      dl[u] += __shfl_xor(dl[u], 16, 64);
-      dl[u] += __shfl_xor(dl[u], 32, 64);
-      const int q = (2 * qp + u) * 16 + i;
-      if (q >= N) dl[u] = 0.f;
-      if (g == 0) dlt_s[q] = dl[u];
-    }
-    // pass B: dQ
-    v4f dq[2][HD / 16];
+      for (int dt = 0; dt < HD / 16; ++dt) dq[dt] = v4f{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int u = 0; u < 2; ++u)
+      for (int ks = 0; ks < NKT / 2; ++ks) {
+        v4f d0, d1;
 #pragma unroll
-      for (int dt = 0; dt < HD / 16; ++dt) dq[u][dt] = v4f{0.f, 0.f, 0.f, 0.f};
-    for (int ks = 0; ks < npair; ++ks) {
-      v4f DS[2][2];  // [query tile][key tile]
-#pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        const int kt = 2 * ks + t;
-        v8bf kr[HD / 32], vr[HD / 32];
-#pragma unroll
-        for (int kk = 0; kk < HD / 32; ++kk) {
-          kr[kk] = rd_row<HD>(ImA, kt * 16, kk, lane);
-          vr[kk] = rd_row<HD>(ImB, kt * 16, kk, lane);
+        for (int r = 0; r < 4; ++r) {
+          d0[r] = P[2 * ks][r] * (DP[2 * ks][r] - dl);
+          d1[r] = P[2 * ks + 1][r] * (DP[2 * ks + 1][r] - dl);
         }
+        const v8bf bD = pack8(d0, d1);
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          v4f st = {0.f, 0.f, 0.f, 0.f}, dpt = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-          for (int kk = 0; kk < HD / 32; ++kk) {
-            st = mfma(kr[kk], qf[u][kk], st);
-            dpt = mfma(vr[kk], df[u][kk], dpt);
-          }
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int key = kt * 16 + 4 * g + r;
-            const float p = key < N ? exp2f(st[r] * c - ls[u]) : 0.f;
-            DS[u][t][r] = p * (dpt[r] - dl[u]);
-          }
-        }
+        for (int dt = 0; dt < HD / 16; ++dt) dq[dt] = mfma(rd_tr<HD>(ImA, 2 * ks, 2 * ks + 1, dt * 16, lane), bD, dq[dt]);
       }
-      const v8bf bD0 = pack8(DS[0][0], DS[0][1]), bD1 = pack8(DS[1][0], DS[1][1]);
-#pragma unroll
-      for (int dt = 0; dt < HD / 16; ++dt) {
-        const v8bf kt_ = rd_tr<HD>(ImA, 2 * ks, 2 * ks + 1, dt * 16, lane);
-        dq[0][dt] = mfma(kt_, bD0, dq[0][dt]);
-        dq[1][dt] = mfma(kt_, bD1, dq[1][dt]);
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int q = (2 * qp + u) * 16 + i;
       if (q < N) {
 #pragma unroll
         for (int dt = 0; dt < HD / 16; ++dt) {
           const int d = dt * 16 + 4 * g;
-          if (d < hd) store4(dq_base + (long)q * rs + d, dq[u][dt], scale);
+          if (d < hd) store4(dq_base + (long)q * rs + d, dq[dt], scale);
         }
       }
       if (bias_partial) {
 #pragma unroll
         for (int dt = 0; dt < HD / 16; ++dt)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) bq[dt][r] += sum16(dq[u][dt][r]);  // padded queries: dS = 0
+          for (int r = 0; r < 4; ++r) bq[dt][r] += dq[dt][r];  // padded queries: dS = 0; lanes summed at the end
       }
     }
+  } else {
+    for (int qp = wave; qp < npair; qp += NW) {
+      v8bf qf[2][HD / 32], df[2][HD / 32];
+      float ls[2], dl[2] = {0.f, 0.f};
+  #pragma unroll
+      for (int u = 0; u < 2; ++u) {
+  #pragma unroll
+        for (int kk = 0; kk < HD / 32; ++kk) {
+          qf[u][kk] = gl_row<HD>(base, rs, (2 * qp + u) * 16, kk, N, hd, lane);
+          df[u][kk] = gl_row<HD>(dob, D, (2 * qp + u) * 16, kk, N, hd, lane);
+        }
+        ls[u] = lse_s[(2 * qp + u) * 16 + i];
+      }
+      // pass A: delta
+      for (int kt = 0; kt < 2 * npair; ++kt) {
+        v8bf kr[HD / 32], vr[HD / 32];
+  #pragma unroll
+        for (int kk = 0; kk < HD / 32; ++kk) {
+          kr[kk] = rd_row<HD>(ImA, kt * 16, kk, lane);
+          vr[kk] = rd_row<HD>(ImB, kt * 16, kk, lane);
+        }
+  #pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          v4f st = {0.f, 0.f, 0.f, 0.f}, dpt = {0.f, 0.f, 0.f, 0.f};
+  #pragma unroll
+          for (int kk = 0; kk < HD / 32; ++kk) {
+            st = mfma(kr[kk], qf[u][kk], st);
+            dpt = mfma(vr[kk], df[u][kk], dpt);
+          }
+  #pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int key = kt * 16 + 4 * g + r;
+            if (key < N) dl[u] += ex2(st[r] * c - ls[u]) * dpt[r];
+          }
+        }
+      }
+  #pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        dl[u] += __shfl_xor(dl[u], 16, 64);
+        dl[u] += __shfl_xor(dl[u], 32, 64);
+        const int q = (2 * qp + u) * 16 + i;
+        if (q >= N) dl[u] = 0.f;
+        if (g == 0) dlt_s[q] = dl[u];
+      }
+      // pass B: dQ
+      v4f dq[2][HD / 16];
+  #pragma unroll
+      for (int u = 0; u < 2; ++u)
+  #pragma unroll
+        for (int dt = 0; dt < HD / 16; ++dt) dq[u][dt] = v4f{0.f, 0.f, 0.f, 0.f};
+      for (int ks = 0; ks < npair; ++ks) {
+        v4f DS[2][2];  // [query tile][key tile]
+  #pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          const int kt = 2 * ks + t;
+          v8bf kr[HD / 32], vr[HD / 32];
+  #pragma unroll
+          for (int kk = 0; kk < HD / 32; ++kk) {
+            kr[kk] = rd_row<HD>(ImA, kt * 16, kk, lane);
+            vr[kk] = rd_row<HD>(ImB, kt * 16, kk, lane);
+          }
+  #pragma unroll
+          for (int u = 0; u < 2; ++u) {
+            v4f st = {0.f, 0.f, 0.f, 0.f}, dpt = {0.f, 0.f, 0.f, 0.f};
+  #pragma unroll
+            for (int kk = 0; kk < HD / 32; ++kk) {
+              st = mfma(kr[kk], qf[u][kk], st);
+              dpt = mfma(vr[kk], df[u][kk], dpt);
+            }
+  #pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int key = kt * 16 + 4 * g + r;
+              const float p = key < N ? ex2(st[r] * c - ls[u]) : 0.f;
+              DS[u][t][r] = p * (dpt[r] - dl[u]);
+            }
+          }
+        }
+        const v8bf bD0 = pack8(DS[0][0], DS[0][1]), bD1 = pack8(DS[1][0], DS[1][1]);
+  #pragma unroll
+        for (int dt = 0; dt < HD / 16; ++dt) {
+          const v8bf kt_ = rd_tr<HD>(ImA, 2 * ks, 2 * ks + 1, dt * 16, lane);
+          dq[0][dt] = mfma(kt_, bD0, dq[0][dt]);
+          dq[1][dt] = mfma(kt_, bD1, dq[1][dt]);
+        }
+      }
+  #pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int q = (2 * qp + u) * 16 + i;
+        if (q < N) {
+  #pragma unroll
+          for (int dt = 0; dt < HD / 16; ++dt) {
+            const int d = dt * 16 + 4 * g;
+            if (d < hd) store4(dq_base + (long)q * rs + d, dq[u][dt], scale);
+          }
+        }
+        if (bias_partial) {
+  #pragma unroll
+          for (int dt = 0; dt < HD / 16; ++dt)
+  #pragma unroll
+            for (int r = 0; r < 4; ++r) bq[dt][r] += dq[u][dt][r];  // padded queries: dS = 0
+        }
+      }
+    }
+
+  }
+  if (bias_partial) {  // the wave's dQ column sums leave registers before stage 2
+#pragma unroll
+    for (int dt = 0; dt < HD / 16; ++dt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float v = sum16(bq[dt][r]);
+        if (i == 0) bsum[(wave * 3 + 0) * HD + dt * 16 + 4 * g + r] = v * scale;
+      }
   }
   __syncthreads();  // K / V images no longer read; delta complete
 
   // ---- stage 2: dK and dV, key-tile pairs ----
+  if (!(stages & 2)) return;  // diagnostic timing of stage 1 alone (VIT_ATTN_BWD_STAGES)
   load_images<HD, NP, NW * 64>(ImA, base, rs, ImB, dob, D, N, hd);  // Q, dO
   __syncthreads();
+  // the last query pair may hold one wholly padded 16-row tile (N % 32 in 1..16): its S / dP
+  // products are skipped (P = dS = 0 there)
+  const bool last_half = (2 * npair - 1) * 16 >= N;
+  v8bf kn[2][HD / 32], vn[2][HD / 32];  // next pair's K / V rows, requested one pair ahead
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int kk = 0; kk < HD / 32; ++kk) {
+      kn[t][kk] = gl_row<HD>(base + D, rs, (2 * wave + t) * 16, kk, N, hd, lane);
+      vn[t][kk] = gl_row<HD>(base + 2 * D, rs, (2 * wave + t) * 16, kk, N, hd, lane);
+    }
   for (int kp = wave; kp < npair; kp += NW) {
     v8bf kf[2][HD / 32], vf[2][HD / 32];
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
       for (int kk = 0; kk < HD / 32; ++kk) {
-        kf[t][kk] = gl_row<HD>(base + D, rs, (2 * kp + t) * 16, kk, N, hd, lane);
-        vf[t][kk] = gl_row<HD>(base + 2 * D, rs, (2 * kp + t) * 16, kk, N, hd, lane);
+        kf[t][kk] = kn[t][kk];
+        vf[t][kk] = vn[t][kk];
+        kn[t][kk] = gl_row<HD>(base + D, rs, (2 * (kp + NW) + t) * 16, kk, N, hd, lane);
+        vn[t][kk] = gl_row<HD>(base + 2 * D, rs, (2 * (kp + NW) + t) * 16, kk, N, hd, lane);
       }
     v4f dv[2][HD / 16], dk[2][HD / 16];
 #pragma unroll
@@ -381,12 +495,19 @@ __global__ void __launch_bounds__(NW * 64, 2) attn_bwd_kernel(const bf16_t* __re
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         const int qt = 2 * qs + u;
+        if (u == 1 && last_half && qs == npair - 1) {
+          P[0][1] = P[1][1] = DS[0][1] = DS[1][1] = v4f{0.f, 0.f, 0.f, 0.f};
+          continue;
+        }
         v8bf qr[HD / 32], orow[HD / 32];
 #pragma unroll
         for (int kk = 0; kk < HD / 32; ++kk) {
           qr[kk] = rd_row<HD>(ImA, qt * 16, kk, lane);
           orow[kk] = rd_row<HD>(ImB, qt * 16, kk, lane);
         }
+        // queries 16qt + 4g + r, r = 0..3: one 16-B read each of lse and delta
+        const v4f lq = *reinterpret_cast<const v4f*>(lse_s + qt * 16 + 4 * g);
+        const v4f dq4 = *reinterpret_cast<const v4f*>(dlt_s + qt * 16 + 4 * g);
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
           v4f sv = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
@@ -398,10 +519,9 @@ __global__ void __launch_bounds__(NW * 64, 2) attn_bwd_kernel(const bf16_t* __re
           const bool kvalid = (2 * kp + t) * 16 + i < N;
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const int q = qt * 16 + 4 * g + r;
-            const float p = kvalid ? exp2f(sv[r] * c - lse_s[q]) : 0.f;
+            const float p = kvalid ? ex2(sv[r] * c - lq[r]) : 0.f;
             P[t][u][r] = p;
-            DS[t][u][r] = p * (dp[r] - dlt_s[q]);
+            DS[t][u][r] = p * (dp[r] - dq4[r]);
           }
         }
       }
@@ -435,22 +555,29 @@ __global__ void __launch_bounds__(NW * 64, 2) attn_bwd_kernel(const bf16_t* __re
         for (int dt = 0; dt < HD / 16; ++dt)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {  // invalid keys hold exact zeros (P = 0)
-            bk[dt][r] += sum16(dk[t][dt][r]);
-            bv[dt][r] += sum16(dv[t][dt][r]);
+            bk[dt][r] += dk[t][dt][r];
+            bv[dt][r] += dv[t][dt][r];
           }
       }
     }
   }
 
   if (bias_partial) {
-    // lanes i == 0 hold the wave's column sums for d = 16dt + 4g + r; fixed-order sum over waves
-    if (i == 0) {
+    // per-lane partials -> the wave's column sums for d = 16dt + 4g + r (sum over the 16 lanes i),
+    // then a fixed-order sum over waves
+#pragma unroll
+    for (int dt = 0; dt < HD / 16; ++dt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        bk[dt][r] = sum16(bk[dt][r]);
+        bv[dt][r] = sum16(bv[dt][r]);
+      }
+    if (i == 0) {  // the dQ sums were stored after stage 1
 #pragma unroll
       for (int dt = 0; dt < HD / 16; ++dt)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int d = dt * 16 + 4 * g + r;
-          bsum[(wave * 3 + 0) * HD + d] = bq[dt][r] * scale;
           bsum[(wave * 3 + 1) * HD + d] = bk[dt][r] * scale;
           bsum[(wave * 3 + 2) * HD + d] = bv[dt][r];
         }
@@ -484,7 +611,12 @@ hipError_t launch_bwd_nw(const bf16_t* qkv, const bf16_t* dout, const float* lse
   const size_t lds = (size_t)2 * NKT * 16 * HD * 2 + 2 * NKT * 16 * 4 + (size_t)NW * 3 * HD * 4;
   auto kern = attn_bwd_kernel<HD, NKT, NW>;
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL(kern, dim3(B * H), dim3(NW * 64), lds, s, qkv, dout, lse, dqkv, bias_partial, N, H, hd, scale);
+  static const int stages = [] {
+    const char* e = getenv("VIT_ATTN_BWD_STAGES");
+    return e ? atoi(e) : 3;
+  }();
+  hipLaunchKernelGGL(kern, dim3(B * H), dim3(NW * 64), lds, s, qkv, dout, lse, dqkv, bias_partial, N, H, hd, scale,
+                     stages);
   return hipGetLastError();
 }
 

@@ -23,6 +23,7 @@ import numpy as np
 import torch
 import torch.distributed as dist
 
+from . import checkpoint as _ckpt
 from .config import get_train_config
 from .dist import GradAllReducer
 from .model import CrossEntropyLoss, VisionTransformer
@@ -153,10 +154,8 @@ def save_model(save_dir, epoch, model, optimizer, lr_scheduler, device_ids=(), b
 
 
 def load_checkpoint(path):
-    """Weights of a reference .pth checkpoint (src/checkpoint.py:7-17, pth branch)."""
-    if not path.endswith("pth"):
-        raise NotImplementedError("only .pth checkpoints are supported (JAX .npz import is a later round)")
-    return torch.load(path, map_location="cpu", weights_only=True)["state_dict"]
+    """Weights of a reference .pth or JAX .npz checkpoint (src/checkpoint.py:7-17)."""
+    return _ckpt.load_checkpoint(path)
 
 
 def build_model(config, device):
