@@ -53,6 +53,7 @@ def main():
     ap.add_argument("--wgrad", action="store_true")
     ap.add_argument("--splits", default="8,16")
     ap.add_argument("--blas", action="store_true")
+    ap.add_argument("--colpart", action="store_true", help="also write per-tile column partial sums")
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--T", type=int, default=50432)
     ap.add_argument("--D", type=int, default=768)
@@ -91,6 +92,10 @@ def main():
                     extra = dict(bias=bias, C2=C2, ldc2=N)
                 elif epi in (EPI_GELU_BWD, EPI_MUL_BF16):
                     extra = dict(aux=U, ldaux=N)
+                if args.colpart and epi in (EPI_BF16, EPI_GELU_BWD, EPI_MUL_BF16):
+                    rows = ops.gemm_tile_rows(A, B, out, M, N, K, a_layout=al, b_layout=bl, lda=K, ldb=ldb, ldc=N,
+                                              epilogue=epi, tile=tile, **extra)
+                    extra = dict(extra, col_partial=torch.empty((M + rows - 1) // rows, N, device=dev))
                 fn = (lambda tile=tile, epi=epi, extra=extra, out=out:
                       ops.gemm(A, B, out, M, N, K, a_layout=al, b_layout=bl, lda=K, ldb=ldb, ldc=N, epilogue=epi,
                                tile=tile, **extra))

@@ -1,5 +1,9 @@
 #!/usr/bin/env python3
-"""Per-launch HBM traffic of one kernel from rocprofv3 --pmc counter_collection.csv files.
+"""Per-launch HBM traffic of one GEMM call from rocprofv3 --pmc counter_collection.csv files.
+
+A call may launch more than one kernel (the wave split runs the whole-wave rows on a 256x256 kernel
+and the remainder on 128x128 tiles): every kernel matching NAME_REGEX is averaged over its own
+dispatches and the per-call traffic is the sum over the matched kernels.
 
 Usage: pmc_traffic.py NAME_REGEX fetch.csv write.csv [out.json]
 FETCH_SIZE / WRITE_SIZE are in KB. gfx950 correction (MI355X_MICROARCH.md, HBM section): FETCH_SIZE reports
@@ -27,13 +31,20 @@ def per_dispatch(path, counter, rx):
 def main():
     rx = re.compile(sys.argv[1])
     f, fn = per_dispatch(sys.argv[2], "FETCH_SIZE", rx)
-    w, _ = per_dispatch(sys.argv[3], "WRITE_SIZE", rx)
+    w, wn = per_dispatch(sys.argv[3], "WRITE_SIZE", rx)
     assert f and w, "no matching dispatches"
-    fetch_b = 2.0 * 1024 * sum(f.values()) / len(f)
-    write_b = 1024 * sum(w.values()) / len(w)
-    out = {"kernel": next(iter(fn.values())), "dispatches_fetch": len(f), "dispatches_write": len(w),
+    parts = {}
+    for name in sorted(set(fn.values())):
+        fd = [v for k, v in f.items() if fn[k] == name]
+        wd = [v for k, v in w.items() if wn[k] == name]
+        fb = 2.0 * 1024 * sum(fd) / len(fd)
+        wb = 1024 * sum(wd) / max(1, len(wd))
+        parts[name] = {"dispatches": len(fd), "fetch_bytes_corrected": fb, "write_bytes": wb}
+    fetch_b = sum(p["fetch_bytes_corrected"] for p in parts.values())
+    write_b = sum(p["write_bytes"] for p in parts.values())
+    out = {"kernel": " + ".join(parts), "dispatches_fetch": len(f), "dispatches_write": len(w),
            "fetch_bytes_raw": fetch_b / 2, "fetch_bytes_corrected": fetch_b, "write_bytes": write_b,
-           "traffic_bytes": fetch_b + write_b,
+           "traffic_bytes": fetch_b + write_b, "per_kernel": parts,
            "correction": "FETCH_SIZE x2 (gfx950 wide-read undercount), WRITE_SIZE as reported; KB=1024 B"}
     print(json.dumps(out, indent=1))
     if len(sys.argv) > 4:

@@ -228,8 +228,10 @@ __device__ __forceinline__ void ld8bf(const bf16_t* p, float* v) {
 }
 
 // 8 consecutive columns n..n+7 of row m (all in range, aligned: p.vec).
+// pre: the 8 aux values of (m, n..n+7) already loaded by the caller (GELU_BWD / MUL / RESID), or null.
 template <int EPI>
-__device__ __forceinline__ void epi_store8(const GemmDev& p, int z, int split_idx, int m, int n, float* v) {
+__device__ __forceinline__ void epi_store8(const GemmDev& p, int z, int split_idx, int m, int n, float* v,
+                                           const float* pre = nullptr) {
   float b[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   if constexpr (EPI == VIT_EPI_BIAS_BF16 || EPI == VIT_EPI_BIAS_GELU || EPI == VIT_EPI_BIAS_RESID_F32 ||
                 EPI == VIT_EPI_BIAS_GELU_DGELU) {
@@ -254,13 +256,23 @@ __device__ __forceinline__ void epi_store8(const GemmDev& p, int z, int split_id
     st8bf((bf16_t*)p.C2 + z * p.c_bs + (long)m * p.ldc2 + n, gl, p.nt);
   } else if constexpr (EPI == VIT_EPI_BIAS_RESID_F32) {
     float r[8];
-    ld8f((const float*)p.aux + (long)m * p.ldaux + n, r);
+    if (pre) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) r[k] = pre[k];
+    } else {
+      ld8f((const float*)p.aux + (long)m * p.ldaux + n, r);
+    }
 #pragma unroll
     for (int k = 0; k < 8; ++k) v[k] += b[k] + r[k];
     st8f((float*)p.C + z * p.c_bs + (long)m * p.ldc + n, v, p.nt);
   } else if constexpr (EPI == VIT_EPI_GELU_BWD) {
     float u[8];
-    ld8bf((const bf16_t*)p.aux + (long)m * p.ldaux + n, u);
+    if (pre) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) u[k] = pre[k];
+    } else {
+      ld8bf((const bf16_t*)p.aux + (long)m * p.ldaux + n, u);
+    }
 #pragma unroll
     for (int k = 0; k < 8; ++k) v[k] *= gelu_grad_f(u[k]);
     st8bf((bf16_t*)p.C + z * p.c_bs + (long)m * p.ldc + n, v, p.nt);
@@ -278,7 +290,12 @@ __device__ __forceinline__ void epi_store8(const GemmDev& p, int z, int split_id
     st8bf((bf16_t*)p.C2 + z * p.c_bs + (long)m * p.ldc2 + n, gl, p.nt);
   } else if constexpr (EPI == VIT_EPI_MUL_BF16) {
     float u[8];
-    ld8bf((const bf16_t*)p.aux + (long)m * p.ldaux + n, u);
+    if (pre) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) u[k] = pre[k];
+    } else {
+      ld8bf((const bf16_t*)p.aux + (long)m * p.ldaux + n, u);
+    }
 #pragma unroll
     for (int k = 0; k < 8; ++k) v[k] *= u[k];
     st8bf((bf16_t*)p.C + z * p.c_bs + (long)m * p.ldc + n, v, p.nt);
@@ -300,6 +317,36 @@ __device__ __forceinline__ void epi_store8(const GemmDev& p, int z, int split_id
     st8f((float*)p.C + ((long)z * p.split_k + split_idx) * (long)p.M * p.N + (long)m * p.N + n, v, p.nt);
   }
 }
+
+// Epilogue operand prefetch: the aux values (bf16 GELU input / multiplier, f32 residual) of 8-column
+// chunks are requested a whole staging pass ahead, so the HBM latency of the lock-step epilogue is
+// paid once per tile instead of once per chunk. AuxPre<EPI>::W uint4 per chunk (0: no aux).
+template <int EPI>
+struct AuxPre {
+  static constexpr int W = (EPI == VIT_EPI_GELU_BWD || EPI == VIT_EPI_MUL_BF16) ? 1
+                           : EPI == VIT_EPI_BIAS_RESID_F32                      ? 2
+                                                                                : 0;
+  __device__ __forceinline__ static void fetch(const GemmDev& p, int m, int n, uint4* d) {
+    if constexpr (W == 1) {
+      d[0] = *reinterpret_cast<const uint4*>((const bf16_t*)p.aux + (long)m * p.ldaux + n);
+    } else if constexpr (W == 2) {
+      const float* a = (const float*)p.aux + (long)m * p.ldaux + n;
+      d[0] = *reinterpret_cast<const uint4*>(a);
+      d[1] = *reinterpret_cast<const uint4*>(a + 4);
+    }
+  }
+  __device__ __forceinline__ static void unpack(const uint4* d, float* u) {
+    if constexpr (W == 1) {
+      const uint4 x = d[0];
+      u[0] = bf2f(x.x & 0xffff); u[1] = bf2f(x.x >> 16); u[2] = bf2f(x.y & 0xffff); u[3] = bf2f(x.y >> 16);
+      u[4] = bf2f(x.z & 0xffff); u[5] = bf2f(x.z >> 16); u[6] = bf2f(x.w & 0xffff); u[7] = bf2f(x.w >> 16);
+    } else if constexpr (W == 2) {
+      u[0] = __uint_as_float(d[0].x); u[1] = __uint_as_float(d[0].y); u[2] = __uint_as_float(d[0].z);
+      u[3] = __uint_as_float(d[0].w); u[4] = __uint_as_float(d[1].x); u[5] = __uint_as_float(d[1].y);
+      u[6] = __uint_as_float(d[1].z); u[7] = __uint_as_float(d[1].w);
+    }
+  }
+};
 
 // Multi-stage LDS-DMA pipeline: STAGES k-tile buffers; at step t the DMA of step t+STAGES-1 is
 // issued into the buffer read at step t-1, so STAGES-2 k-tiles stay in flight across every
@@ -783,10 +830,10 @@ int pick_tile(const vit_gemm_args* a) {
   const bool ak = a->a_layout == VIT_K_CONTIG, bk = a->b_layout == VIT_K_CONTIG;
   if (a->epilogue == VIT_EPI_SPLITK && a->M >= 256 && a->N >= 256) return 5;
   if (a->M >= 1024 && a->N >= 256) {
-    // (the GELU-backward epilogue and short-K f32 residual outputs keep 2 workgroups per CU)
-    if (ak && bk && a->epilogue != VIT_EPI_GELU_BWD && a->epilogue != VIT_EPI_MUL_BF16 &&
-        !(a->epilogue == VIT_EPI_BIAS_RESID_F32 && a->K < 2048))
-      return 9;
+    // (short-K f32 residual outputs keep 2 workgroups per CU; the aux-reading epilogues run on the
+    // half-tile kernel since their operand is prefetched a staging pass ahead: fc2 dgrad x GELU'
+    // 286 us vs 356 us on 256x128)
+    if (ak && bk && !(a->epilogue == VIT_EPI_BIAS_RESID_F32 && a->K < 2048)) return 9;
     if (a->N >= 2048 && a->epilogue != VIT_EPI_GELU_BWD && a->epilogue != VIT_EPI_MUL_BF16) return 5;
     if (!bk && a->K >= 3072) return 5;
     return 3;
