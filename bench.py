@@ -48,7 +48,12 @@ def pmc_traffic(kernel_tag="gemm_pp2_kernel<true, true, 8>"):
     (tools/prof.sh: FETCH_SIZE and WRITE_SIZE in separate passes, FETCH_SIZE doubled per the gfx950
     correction of MI355X_MICROARCH.md). None when no pass of that kernel is committed."""
     import glob
-    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*", "fc1_traffic*.json")), key=os.path.getmtime)
+    import re
+
+    def version(path):  # profiles/rNN/fc1_traffic_vK.json: newest round, then newest pass
+        m = re.search(r"r(\d+)[/\\]fc1_traffic_v(\d+)", path)
+        return (int(m.group(1)), int(m.group(2))) if m else (-1, -1)
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*", "fc1_traffic*.json")), key=version)
     for path in reversed(files):
         try:
             d = json.load(open(path))
