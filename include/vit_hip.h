@@ -53,6 +53,26 @@ int vit_abi_version(void);
  * ---------------------------------------------------------------------------------------- */
 enum vit_layout { VIT_K_CONTIG = 0, VIT_MN_CONTIG = 1 };
 
+/* Dropout descriptor. nn.Dropout(p) of PositionEmbs (src/model.py:19-20), EncoderBlock
+ * (:124-125) and MlpBlock (:46-49) as a counter-based mask that forward and backward regenerate:
+ * element (row, col) of dropout site `site` is kept iff the 16-bit half (col % 8) of
+ * Philox4x32-10(counter = {col / 8, row, site, offset_lo}, key = {seed_lo, seed_hi ^ offset_hi})
+ * is >= round(p * 65536); kept elements are scaled by 1 / (1 - p). A NULL descriptor or p == 0
+ * disables it. Sites used by the engine: 0 = position embedding, 1 + 3i / 2 + 3i / 3 + 3i =
+ * attention output / MLP dropout1 / MLP dropout2 of encoder layer i. */
+typedef struct vit_dropout {
+  float p;
+  uint32_t site;
+  uint64_t seed;
+  uint64_t offset;
+  int64_t row_stride; /* mask row of a call's row r = r * row_stride (0 is taken as 1); the final
+                         LayerNorm backward runs on the cls rows only (row stride N tokens) */
+} vit_dropout;
+
+/* mult[r*ld + c] = dropout multiplier (0 or 1/(1-p)) of element (row0 + r, c), c < cols (tests) */
+int vit_dropout_mask(const vit_dropout* d, int64_t row0, int64_t rows, int64_t cols, float* mult,
+                     int64_t ld, vit_stream_t stream);
+
 enum vit_epilogue {
   VIT_EPI_F32 = 0,            /* C(f32)  = acc                                                */
   VIT_EPI_BF16 = 1,           /* C(bf16) = acc                                                */
@@ -97,6 +117,10 @@ typedef struct vit_gemm_args {
                          ceil(M / tile_rows) rows with vit_colsum. tile_rows: vit_gemm_tile_rows() */
   int32_t epilogue;
   int32_t tile;    /* 0 = auto */
+  const vit_dropout* dropout; /* optional, on the epilogue's output (row m, col n):
+                                 PATCH: C = drop(embedding + pos);  BIAS_RESID_F32: C = drop(acc + bias) + aux;
+                                 BIAS_GELU_DGELU: C2 = drop(gelu(u)), C = gelu'(u) * mult (the dropout
+                                 backward folded into the saved derivative) */
 } vit_gemm_args;
 
 int vit_gemm_bf16(const vit_gemm_args* args, vit_stream_t stream);
@@ -116,6 +140,8 @@ int vit_splitk_reduce(const float* ws, int64_t batch, int64_t split, int64_t M, 
  *      (dy*xhat, dy, dx_out) go to `partial` (>= vit_layernorm_bwd_partial_rows(rows) rows of 3*D);
  *      when non-NULL, dgamma_dbeta[0:D] = dgamma, [D:2D] = dbeta, and dx_colsum[0:D] = column sums of
  *      dx_out (= the bias gradient of the linear layer feeding this residual stream).
+ *      dx_dropout (optional): the bf16 copy and dx_colsum carry dx_out * mult (the gradient of the
+ *      dropout-ed branch that fed the residual stream); dx itself stays unmasked.
  * ---------------------------------------------------------------------------------------- */
 int vit_layernorm_fwd(const float* x, int64_t ldx, const float* gamma, const float* beta,
                       void* y, int64_t ldy, int32_t y_f32, float* mean, float* rstd,
@@ -126,7 +152,7 @@ int vit_layernorm_bwd(const void* dy, int64_t lddy, int32_t dy_f32, const float*
                       const float* dres, int64_t lddres, float* dx, int64_t lddx,
                       void* dx_bf16, int64_t lddxb, float* partial, float* dgamma_dbeta,
                       float* dx_colsum, int32_t accumulate_params, int64_t rows, int64_t D,
-                      vit_stream_t stream);
+                      const vit_dropout* dx_dropout, vit_stream_t stream);
 
 /* ------------------------------------------------------------------------------------------
  * Fused multi-head self-attention, one (image, head) per workgroup, all keys in LDS.
@@ -153,9 +179,10 @@ int vit_im2col(const float* x, void* out, int64_t B, int64_t img, int64_t P, int
                vit_stream_t stream);
 
 /* token-level grads of the embedding (src/model.py:17,203-204): from dh0 f32 [B*N, D]:
- * dpos[n][d] = sum_b dh0[b*N+n][d]; dcls = dpos[0]; dconv_bias = sum_{n>=1} dpos[n]. */
+ * dpos[n][d] = sum_b dh0[b*N+n][d]; dcls = dpos[0]; dconv_bias = sum_{n>=1} dpos[n].
+ * dropout (optional): dh0 is taken through the position-embedding dropout's multipliers first. */
 int vit_embed_grad(const float* dh0, int64_t B, int64_t N, int64_t D, float* dpos, float* dcls,
-                   float* dconv_bias, vit_stream_t stream);
+                   float* dconv_bias, const vit_dropout* dropout, vit_stream_t stream);
 
 /* column sums: out[n] (+)= sum_r in[r*ld + n], in bf16 (in_bf16=1) or f32. `partial` needs
  * vit_colsum_partial_rows(rows) * cols floats. (bias grads, src/train.py:23 autograd) */

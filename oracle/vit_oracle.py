@@ -153,8 +153,14 @@ def tame_params(params: "OrderedDict[str, torch.Tensor]", seed: int = 1) -> "Ord
     return out
 
 
-def forward(params, x: torch.Tensor, cfg: ViTConfig) -> torch.Tensor:
-    """Functional ViT forward (reference src/model.py:196-211 and the modules it calls)."""
+def forward(params, x: torch.Tensor, cfg: ViTConfig, drop=None) -> torch.Tensor:
+    """Functional ViT forward (reference src/model.py:196-211 and the modules it calls).
+
+    drop: optional train-mode dropout multipliers (0 or 1/(1-p)), applied where nn.Dropout sits in
+    the reference: drop["pos"] [b, n, D] after the position embedding (:19-20); per layer i
+    drop[("attn", i)] [b, n, D] on the attention output (:124-125), drop[("d1", i)] [b, n, M] after
+    GELU (:46-47) and drop[("d2", i)] [b, n, D] after fc2 (:50-51)."""
+    dm = (lambda key, t: t * drop[key].to(t.dtype)) if drop else (lambda key, t: t)
     D, H = cfg.emb_dim, cfg.num_heads
     hd = D // H
     p = params
@@ -164,7 +170,7 @@ def forward(params, x: torch.Tensor, cfg: ViTConfig) -> torch.Tensor:
     emb = emb.permute(0, 2, 3, 1).reshape(b, -1, D)
     # prepend cls (:203-204), + pos-emb (PositionEmbs.forward :16-22)
     h = torch.cat([p["cls_token"].expand(b, 1, D), emb], dim=1)
-    h = h + p["transformer.pos_embedding.pos_embedding"]
+    h = dm("pos", h + p["transformer.pos_embedding.pos_embedding"])
     n = h.shape[1]
     for i in range(cfg.num_layers):
         q_ = f"transformer.encoder_layers.{i}."
@@ -183,12 +189,12 @@ def forward(params, x: torch.Tensor, cfg: ViTConfig) -> torch.Tensor:
         a = a.transpose(1, 2).reshape(b, n, D)
         # out LinearGeneral W[H,hd,D] contracted over (H,hd) (:97-99)
         o = a @ p[q_ + "attn.out.weight"].reshape(D, D) + p[q_ + "attn.out.bias"]
-        h = h + o
+        h = h + dm(("attn", i), o)
         y = F.layer_norm(h, (D,), p[q_ + "norm2.weight"], p[q_ + "norm2.bias"], 1e-5)
         # MlpBlock: fc1 -> exact-erf GELU -> fc2 (:41-51)
         u = F.linear(y, p[q_ + "mlp.fc1.weight"], p[q_ + "mlp.fc1.bias"])
-        g = F.gelu(u)
-        h = h + F.linear(g, p[q_ + "mlp.fc2.weight"], p[q_ + "mlp.fc2.bias"])
+        g = dm(("d1", i), F.gelu(u))
+        h = h + dm(("d2", i), F.linear(g, p[q_ + "mlp.fc2.weight"], p[q_ + "mlp.fc2.bias"]))
     # final LayerNorm over all tokens (:155), classifier on the cls row (:210)
     h = F.layer_norm(h, (D,), p["transformer.norm.weight"], p["transformer.norm.bias"], 1e-5)
     return F.linear(h[:, 0], p["classifier.weight"], p["classifier.bias"])
@@ -200,10 +206,10 @@ def cross_entropy(logits: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
     return (lse - logits.gather(1, labels.view(-1, 1)).squeeze(1)).mean()
 
 
-def loss_and_grads(params, x, labels, cfg: ViTConfig, dtype=torch.float32):
+def loss_and_grads(params, x, labels, cfg: ViTConfig, dtype=torch.float32, drop=None):
     """Forward + CE + backward on CPU. Returns (logits, loss, grads OrderedDict)."""
     leaves = OrderedDict((k, v.detach().to(dtype).clone().requires_grad_(True)) for k, v in params.items())
-    logits = forward(leaves, x.to(dtype), cfg)
+    logits = forward(leaves, x.to(dtype), cfg, drop=drop)
     loss = cross_entropy(logits, labels)
     loss.backward()
     grads = OrderedDict((k, v.grad.detach().clone()) for k, v in leaves.items())

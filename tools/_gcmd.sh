@@ -1,3 +1,4 @@
 set -e
-timeout -k 10 400 python -u tools/gemm_bench.py --tiles 0,9 --shapes fc1dgk:1,outk:1,qkvdg:1,fc2:4,fc1:8 --rounds 3 > gpurun_out/gemm_split.log 2>&1
-cat gpurun_out/gemm_split.log
+export TMPDIR=/tmp
+timeout -k 10 300 python -u -m pytest tests/test_dropout_gpu.py tests/test_kernels_gpu.py -x -q --timeout 120 --timeout-method thread 2>&1 | tail -2
+timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline > gpurun_out/bench.log 2>&1; tail -1 gpurun_out/bench.log | cut -c1-300

@@ -67,6 +67,58 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, ui
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
 }
 
+// ---- dropout: Philox4x32-10 counter-based masks (see vit_dropout in vit_hip.h) ----
+struct DropDev {
+  uint32_t thr;    // keep iff the 16-bit draw >= thr; 0 = dropout off
+  uint32_t site, k0, k1, off;
+  float scale;     // 1 / (1 - p)
+  int row0;        // added to the launch's row index (a GEMM launched on a row sub-range)
+  int row_mul;     // mask row = row * row_mul + row0
+};
+static inline DropDev make_drop(const vit_dropout* d) {
+  DropDev r = {0u, 0u, 0u, 0u, 0u, 1.0f, 0, 1};
+  if (!d || !(d->p > 0.0f)) return r;
+  const double t = (double)d->p * 65536.0 + 0.5;
+  r.thr = t >= 65536.0 ? 65536u : (uint32_t)t;
+  if (r.thr == 0) return r;
+  r.site = d->site;
+  r.k0 = (uint32_t)d->seed;
+  r.k1 = (uint32_t)(d->seed >> 32) ^ (uint32_t)(d->offset >> 32);
+  r.off = (uint32_t)d->offset;
+  r.scale = d->p < 1.0f ? 1.0f / (1.0f - d->p) : 0.0f;
+  r.row_mul = d->row_stride > 1 ? (int)d->row_stride : 1;
+  return r;
+}
+// Random123 Philox4x32 with 10 rounds
+__device__ __forceinline__ void philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0,
+                                              uint32_t k1, uint32_t* r) {
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    const uint32_t hi0 = __umulhi(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
+    const uint32_t hi1 = __umulhi(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
+    c0 = hi1 ^ c1 ^ k0;
+    c1 = lo1;
+    c2 = hi0 ^ c3 ^ k1;
+    c3 = lo0;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  r[0] = c0; r[1] = c1; r[2] = c2; r[3] = c3;
+}
+// multipliers (0 or 1/(1-p)) of columns 8*col8 .. 8*col8+7 of `row`
+__device__ __forceinline__ void drop_mult8(const DropDev& d, long row, int col8, float* m) {
+  uint32_t r[4];
+  philox4x32_10((uint32_t)col8, (uint32_t)(row * d.row_mul + d.row0), d.site, d.off, d.k0, d.k1, r);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) m[k] = ((r[k >> 1] >> (16 * (k & 1))) & 0xffffu) >= d.thr ? d.scale : 0.0f;
+}
+__device__ __forceinline__ float drop_mult1(const DropDev& d, long row, int col) {
+  uint32_t r[4];
+  philox4x32_10((uint32_t)(col >> 3), (uint32_t)(row * d.row_mul + d.row0), d.site, d.off, d.k0, d.k1, r);
+  const int k = col & 7;
+  return ((r[k >> 1] >> (16 * (k & 1))) & 0xffffu) >= d.thr ? d.scale : 0.0f;
+}
+
 // ---- host-side error plumbing (thread-local last error, int status returns) ----
 namespace vit {
 void set_error(const char* fmt, ...);

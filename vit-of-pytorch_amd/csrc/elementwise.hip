@@ -32,13 +32,25 @@ __global__ void im2col_kernel(const float* __restrict__ x, OUT* __restrict__ out
 }
 
 // dpos[n][d] = sum_b dh0[(b*N+n)*D + d]
-__global__ void pos_grad_kernel(const float* __restrict__ dh0, int B, int N, int D, float* __restrict__ dpos) {
+__global__ void pos_grad_kernel(const float* __restrict__ dh0, int B, int N, int D, float* __restrict__ dpos,
+                                DropDev drop) {
   const int n = blockIdx.y;
   const int d = blockIdx.x * blockDim.x + threadIdx.x;
   if (d >= D) return;
   float s = 0.f;
-  for (int b = 0; b < B; ++b) s += dh0[((long)b * N + n) * D + d];
+  if (drop.thr) {  // gradient through the position-embedding dropout
+    for (int b = 0; b < B; ++b) s += dh0[((long)b * N + n) * D + d] * drop_mult1(drop, (long)b * N + n, d);
+  } else {
+    for (int b = 0; b < B; ++b) s += dh0[((long)b * N + n) * D + d];
+  }
   dpos[(long)n * D + d] = s;
+}
+
+__global__ void dropout_mask_kernel(DropDev drop, long row0, long rows, int cols, float* __restrict__ out, long ld) {
+  const long r = blockIdx.y;
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= rows || c >= cols) return;
+  out[r * ld + c] = drop.thr ? drop_mult1(drop, row0 + r, c) : 1.0f;
 }
 // dcls = dpos[0]; dconv_bias = sum_{n>=1} dpos[n]
 __global__ void cls_bias_grad_kernel(const float* __restrict__ dpos, int N, int D, float* __restrict__ dcls,
@@ -299,11 +311,11 @@ extern "C" int vit_im2col(const float* x, void* out, int64_t B, int64_t img, int
 }
 
 extern "C" int vit_embed_grad(const float* dh0, int64_t B, int64_t N, int64_t D, float* dpos, float* dcls,
-                              float* dconv_bias, vit_stream_t stream) {
+                              float* dconv_bias, const vit_dropout* dropout, vit_stream_t stream) {
   VIT_CHECK_ARG(dh0 && dpos && dcls && dconv_bias && B > 0 && N > 0 && D > 0, "vit_embed_grad: bad args");
   hipStream_t s = (hipStream_t)stream;
   hipLaunchKernelGGL(pos_grad_kernel, dim3((unsigned)((D + 255) / 256), (unsigned)N), dim3(256), 0, s, dh0, (int)B,
-                     (int)N, (int)D, dpos);
+                     (int)N, (int)D, dpos, make_drop(dropout));
   hipLaunchKernelGGL(cls_bias_grad_kernel, dim3((unsigned)((D + 255) / 256)), dim3(256), 0, s, dpos, (int)N, (int)D,
                      dcls, dconv_bias);
   VIT_LAUNCH_CHECK("vit_embed_grad");
@@ -543,4 +555,13 @@ extern "C" int vit_gelu_f32(const float* in, float* out, int64_t n, vit_stream_t
   if (n == 0) return VIT_OK;
   hipLaunchKernelGGL(gelu_f32_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, in, out, (long)n);
   VIT_LAUNCH_CHECK("vit_gelu_f32");
+}
+
+extern "C" int vit_dropout_mask(const vit_dropout* d, int64_t row0, int64_t rows, int64_t cols, float* mult,
+                                int64_t ld, vit_stream_t stream) {
+  VIT_CHECK_ARG(mult && rows >= 0 && rows <= 65535 && cols > 0 && ld >= cols, "vit_dropout_mask: bad args");
+  if (rows == 0) return VIT_OK;
+  hipLaunchKernelGGL(dropout_mask_kernel, dim3((unsigned)((cols + 255) / 256), (unsigned)rows), dim3(256), 0,
+                     (hipStream_t)stream, make_drop(d), (long)row0, (long)rows, (int)cols, mult, (long)ld);
+  VIT_LAUNCH_CHECK("vit_dropout_mask");
 }

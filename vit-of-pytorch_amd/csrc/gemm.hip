@@ -46,6 +46,7 @@ struct GemmDev {
   float* col_partial;  // optional per-M-tile column sums of the output
   int group_m;         // tile order: groups of group_m tile rows, column-major inside (0: row-major)
   int nt;              // non-temporal output stores (keep the operands resident in L2)
+  DropDev drop;        // dropout on the PATCH / BIAS_RESID_F32 / BIAS_GELU_DGELU output (thr 0 = off)
 };
 
 // blockIdx (after the XCD remap) -> output tile. Grouping tile rows keeps the weight panels a
@@ -141,47 +142,55 @@ __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
+// Internal epilogue flag: the dropout variant of PATCH / BIAS_RESID_F32 / BIAS_GELU_DGELU (its own
+// instantiation, so the dropout-free kernels carry none of the Philox code)
+constexpr int EPI_DROP = 16;
+
 template <int EPI>
 __device__ __forceinline__ void epi_store(const GemmDev& p, int z, int split_idx, int m, int n, float v) {
+  constexpr int E = EPI & 15;                  // base epilogue
+  constexpr bool DROP = (EPI & EPI_DROP) != 0;  // dropout variant
   if (m >= p.M || n >= p.N) return;
-  if constexpr (EPI == VIT_EPI_F32) {
+  if constexpr (E == VIT_EPI_F32) {
     float* C = (float*)p.C + z * p.c_bs;
     C[(long)m * p.ldc + n] = v;
-  } else if constexpr (EPI == VIT_EPI_BF16) {
+  } else if constexpr (E == VIT_EPI_BF16) {
     bf16_t* C = (bf16_t*)p.C + z * p.c_bs;
     C[(long)m * p.ldc + n] = f2bf(v);
-  } else if constexpr (EPI == VIT_EPI_BIAS_BF16) {
+  } else if constexpr (E == VIT_EPI_BIAS_BF16) {
     bf16_t* C = (bf16_t*)p.C + z * p.c_bs;
     const float b = p.bias ? p.bias[z * p.bias_bs + n] : 0.f;
     C[(long)m * p.ldc + n] = f2bf(v + b);
-  } else if constexpr (EPI == VIT_EPI_BIAS_GELU) {
+  } else if constexpr (E == VIT_EPI_BIAS_GELU) {
     bf16_t* C = (bf16_t*)p.C + z * p.c_bs;
     bf16_t* C2 = (bf16_t*)p.C2 + z * p.c_bs;
     const float u = v + (p.bias ? p.bias[z * p.bias_bs + n] : 0.f);
     C[(long)m * p.ldc + n] = f2bf(u);
     C2[(long)m * p.ldc2 + n] = f2bf(gelu_f(u));
-  } else if constexpr (EPI == VIT_EPI_BIAS_RESID_F32) {
+  } else if constexpr (E == VIT_EPI_BIAS_RESID_F32) {
     float* C = (float*)p.C + z * p.c_bs;
     const float* R = (const float*)p.aux;
     const float b = p.bias ? p.bias[z * p.bias_bs + n] : 0.f;
-    C[(long)m * p.ldc + n] = v + b + R[(long)m * p.ldaux + n];
-  } else if constexpr (EPI == VIT_EPI_GELU_BWD) {
+    const float dm = DROP ? drop_mult1(p.drop, m, n) : 1.0f;
+    C[(long)m * p.ldc + n] = (v + b) * dm + R[(long)m * p.ldaux + n];
+  } else if constexpr (E == VIT_EPI_GELU_BWD) {
     bf16_t* C = (bf16_t*)p.C + z * p.c_bs;
     const bf16_t* U = (const bf16_t*)p.aux;
     C[(long)m * p.ldc + n] = f2bf(v * gelu_grad_f(bf2f(U[(long)m * p.ldaux + n])));
-  } else if constexpr (EPI == VIT_EPI_BIAS_GELU_DGELU) {
+  } else if constexpr (E == VIT_EPI_BIAS_GELU_DGELU) {
     bf16_t* C = (bf16_t*)p.C + z * p.c_bs;
     bf16_t* C2 = (bf16_t*)p.C2 + z * p.c_bs;
     const float u = v + (p.bias ? p.bias[z * p.bias_bs + n] : 0.f);
     float pdf;
     const float cdf = phi_and_pdf(u, &pdf);
-    C[(long)m * p.ldc + n] = f2bf(cdf + u * pdf);
-    C2[(long)m * p.ldc2 + n] = f2bf(u * cdf);
-  } else if constexpr (EPI == VIT_EPI_MUL_BF16) {
+    const float dm = DROP ? drop_mult1(p.drop, m, n) : 1.0f;
+    C[(long)m * p.ldc + n] = f2bf((cdf + u * pdf) * dm);
+    C2[(long)m * p.ldc2 + n] = f2bf(u * cdf * dm);
+  } else if constexpr (E == VIT_EPI_MUL_BF16) {
     bf16_t* C = (bf16_t*)p.C + z * p.c_bs;
     const bf16_t* U = (const bf16_t*)p.aux;
     C[(long)m * p.ldc + n] = f2bf(v * bf2f(U[(long)m * p.ldaux + n]));
-  } else if constexpr (EPI == VIT_EPI_PATCH) {
+  } else if constexpr (E == VIT_EPI_PATCH) {
     float* C = (float*)p.C;
     const float* pos = (const float*)p.aux;
     const int t = m % p.tokens;
@@ -190,8 +199,9 @@ __device__ __forceinline__ void epi_store(const GemmDev& p, int z, int split_idx
       o = p.aux2[n] + pos[n];
     else
       o = v + p.bias[n] + pos[(long)t * p.ldaux + n];
+    if constexpr (DROP) o *= drop_mult1(p.drop, m, n);
     C[(long)m * p.ldc + n] = o;
-  } else if constexpr (EPI == VIT_EPI_SPLITK) {
+  } else if constexpr (E == VIT_EPI_SPLITK) {
     float* C = (float*)p.C + ((long)z * p.split_k + split_idx) * (long)p.M * p.N;
     C[(long)m * p.N + n] = v;
   }
@@ -232,20 +242,22 @@ __device__ __forceinline__ void ld8bf(const bf16_t* p, float* v) {
 template <int EPI>
 __device__ __forceinline__ void epi_store8(const GemmDev& p, int z, int split_idx, int m, int n, float* v,
                                            const float* pre = nullptr) {
+  constexpr int E = EPI & 15;
+  constexpr bool DROP = (EPI & EPI_DROP) != 0;
   float b[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  if constexpr (EPI == VIT_EPI_BIAS_BF16 || EPI == VIT_EPI_BIAS_GELU || EPI == VIT_EPI_BIAS_RESID_F32 ||
-                EPI == VIT_EPI_BIAS_GELU_DGELU) {
+  if constexpr (E == VIT_EPI_BIAS_BF16 || E == VIT_EPI_BIAS_GELU || E == VIT_EPI_BIAS_RESID_F32 ||
+                E == VIT_EPI_BIAS_GELU_DGELU) {
     if (p.bias) ld8f(p.bias + z * p.bias_bs + n, b);
   }
-  if constexpr (EPI == VIT_EPI_F32) {
+  if constexpr (E == VIT_EPI_F32) {
     st8f((float*)p.C + z * p.c_bs + (long)m * p.ldc + n, v, p.nt);
-  } else if constexpr (EPI == VIT_EPI_BF16) {
+  } else if constexpr (E == VIT_EPI_BF16) {
     st8bf((bf16_t*)p.C + z * p.c_bs + (long)m * p.ldc + n, v, p.nt);
-  } else if constexpr (EPI == VIT_EPI_BIAS_BF16) {
+  } else if constexpr (E == VIT_EPI_BIAS_BF16) {
 #pragma unroll
     for (int k = 0; k < 8; ++k) v[k] += b[k];
     st8bf((bf16_t*)p.C + z * p.c_bs + (long)m * p.ldc + n, v, p.nt);
-  } else if constexpr (EPI == VIT_EPI_BIAS_GELU) {
+  } else if constexpr (E == VIT_EPI_BIAS_GELU) {
     float gl[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
@@ -254,7 +266,7 @@ __device__ __forceinline__ void epi_store8(const GemmDev& p, int z, int split_id
     }
     st8bf((bf16_t*)p.C + z * p.c_bs + (long)m * p.ldc + n, v, p.nt);
     st8bf((bf16_t*)p.C2 + z * p.c_bs + (long)m * p.ldc2 + n, gl, p.nt);
-  } else if constexpr (EPI == VIT_EPI_BIAS_RESID_F32) {
+  } else if constexpr (E == VIT_EPI_BIAS_RESID_F32) {
     float r[8];
     if (pre) {
 #pragma unroll
@@ -262,10 +274,17 @@ __device__ __forceinline__ void epi_store8(const GemmDev& p, int z, int split_id
     } else {
       ld8f((const float*)p.aux + (long)m * p.ldaux + n, r);
     }
+    if constexpr (DROP) {
+      float dm[8];
+      drop_mult8(p.drop, m, n >> 3, dm);
 #pragma unroll
-    for (int k = 0; k < 8; ++k) v[k] += b[k] + r[k];
+      for (int k = 0; k < 8; ++k) v[k] = (v[k] + b[k]) * dm[k] + r[k];
+    } else {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] += b[k] + r[k];
+    }
     st8f((float*)p.C + z * p.c_bs + (long)m * p.ldc + n, v, p.nt);
-  } else if constexpr (EPI == VIT_EPI_GELU_BWD) {
+  } else if constexpr (E == VIT_EPI_GELU_BWD) {
     float u[8];
     if (pre) {
 #pragma unroll
@@ -276,7 +295,7 @@ __device__ __forceinline__ void epi_store8(const GemmDev& p, int z, int split_id
 #pragma unroll
     for (int k = 0; k < 8; ++k) v[k] *= gelu_grad_f(u[k]);
     st8bf((bf16_t*)p.C + z * p.c_bs + (long)m * p.ldc + n, v, p.nt);
-  } else if constexpr (EPI == VIT_EPI_BIAS_GELU_DGELU) {
+  } else if constexpr (E == VIT_EPI_BIAS_GELU_DGELU) {
     float gl[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
@@ -286,9 +305,18 @@ __device__ __forceinline__ void epi_store8(const GemmDev& p, int z, int split_id
       gl[k] = u * cdf;
       v[k] = cdf + u * pdf;
     }
+    if constexpr (DROP) {
+      float dm[8];
+      drop_mult8(p.drop, m, n >> 3, dm);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        gl[k] *= dm[k];
+        v[k] *= dm[k];
+      }
+    }
     st8bf((bf16_t*)p.C + z * p.c_bs + (long)m * p.ldc + n, v, p.nt);
     st8bf((bf16_t*)p.C2 + z * p.c_bs + (long)m * p.ldc2 + n, gl, p.nt);
-  } else if constexpr (EPI == VIT_EPI_MUL_BF16) {
+  } else if constexpr (E == VIT_EPI_MUL_BF16) {
     float u[8];
     if (pre) {
 #pragma unroll
@@ -299,7 +327,7 @@ __device__ __forceinline__ void epi_store8(const GemmDev& p, int z, int split_id
 #pragma unroll
     for (int k = 0; k < 8; ++k) v[k] *= u[k];
     st8bf((bf16_t*)p.C + z * p.c_bs + (long)m * p.ldc + n, v, p.nt);
-  } else if constexpr (EPI == VIT_EPI_PATCH) {
+  } else if constexpr (E == VIT_EPI_PATCH) {
     const int t = m % p.tokens;
     float ps[8];
     ld8f((const float*)p.aux + (long)t * p.ldaux + n, ps);
@@ -312,8 +340,14 @@ __device__ __forceinline__ void epi_store8(const GemmDev& p, int z, int split_id
 #pragma unroll
       for (int k = 0; k < 8; ++k) v[k] += b[k] + ps[k];
     }
+    if constexpr (DROP) {
+      float dm[8];
+      drop_mult8(p.drop, m, n >> 3, dm);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] *= dm[k];
+    }
     st8f((float*)p.C + (long)m * p.ldc + n, v, p.nt);
-  } else if constexpr (EPI == VIT_EPI_SPLITK) {
+  } else if constexpr (E == VIT_EPI_SPLITK) {
     st8f((float*)p.C + ((long)z * p.split_k + split_idx) * (long)p.M * p.N + (long)m * p.N + n, v, p.nt);
   }
 }
@@ -323,8 +357,9 @@ __device__ __forceinline__ void epi_store8(const GemmDev& p, int z, int split_id
 // paid once per tile instead of once per chunk. AuxPre<EPI>::W uint4 per chunk (0: no aux).
 template <int EPI>
 struct AuxPre {
-  static constexpr int W = (EPI == VIT_EPI_GELU_BWD || EPI == VIT_EPI_MUL_BF16) ? 1
-                           : EPI == VIT_EPI_BIAS_RESID_F32                      ? 2
+  static constexpr int E = EPI & 15;
+  static constexpr int W = (E == VIT_EPI_GELU_BWD || E == VIT_EPI_MUL_BF16) ? 1
+                           : E == VIT_EPI_BIAS_RESID_F32                      ? 2
                                                                                 : 0;
   __device__ __forceinline__ static void fetch(const GemmDev& p, int m, int n, uint4* d) {
     if constexpr (W == 1) {
@@ -907,6 +942,12 @@ extern "C" int vit_gemm_bf16(const vit_gemm_args* a, vit_stream_t stream) {
     d.vec = v ? 1 : 0;
   }
   d.col_partial = a->col_partial;
+  d.drop = make_drop(a->dropout);
+  VIT_CHECK_ARG(!d.drop.thr || a->epilogue == VIT_EPI_PATCH || a->epilogue == VIT_EPI_BIAS_RESID_F32 ||
+                    a->epilogue == VIT_EPI_BIAS_GELU_DGELU,
+                "vit_gemm_bf16: dropout is supported on the PATCH, BIAS_RESID_F32 and BIAS_GELU_DGELU epilogues");
+  VIT_CHECK_ARG(!d.drop.thr || (a->a_layout == VIT_K_CONTIG && a->b_layout == VIT_K_CONTIG),
+                "vit_gemm_bf16: dropout epilogues need K-contiguous A and B");
   {
     static const int env_gm = [] {
       const char* e = getenv("VIT_GEMM_GROUP_M");
@@ -937,11 +978,17 @@ extern "C" int vit_gemm_bf16(const vit_gemm_args* a, vit_stream_t stream) {
       case VIT_EPI_BF16: return launch_layout<VIT_EPI_BF16>(c, g, ak, bk, batch, split, s);
       case VIT_EPI_BIAS_BF16: return launch_layout<VIT_EPI_BIAS_BF16>(c, g, ak, bk, batch, split, s);
       case VIT_EPI_BIAS_GELU: return launch_layout<VIT_EPI_BIAS_GELU>(c, g, ak, bk, batch, split, s);
-      case VIT_EPI_BIAS_RESID_F32: return launch_layout<VIT_EPI_BIAS_RESID_F32>(c, g, ak, bk, batch, split, s);
+      case VIT_EPI_BIAS_RESID_F32:
+        if (g.drop.thr) return launch_cfg<VIT_EPI_BIAS_RESID_F32 | EPI_DROP, true, true>(c, g, batch, split, s);
+        return launch_layout<VIT_EPI_BIAS_RESID_F32>(c, g, ak, bk, batch, split, s);
       case VIT_EPI_GELU_BWD: return launch_layout<VIT_EPI_GELU_BWD>(c, g, ak, bk, batch, split, s);
-      case VIT_EPI_BIAS_GELU_DGELU: return launch_layout<VIT_EPI_BIAS_GELU_DGELU>(c, g, ak, bk, batch, split, s);
+      case VIT_EPI_BIAS_GELU_DGELU:
+        if (g.drop.thr) return launch_cfg<VIT_EPI_BIAS_GELU_DGELU | EPI_DROP, true, true>(c, g, batch, split, s);
+        return launch_layout<VIT_EPI_BIAS_GELU_DGELU>(c, g, ak, bk, batch, split, s);
       case VIT_EPI_MUL_BF16: return launch_layout<VIT_EPI_MUL_BF16>(c, g, ak, bk, batch, split, s);
-      case VIT_EPI_PATCH: return launch_layout<VIT_EPI_PATCH>(c, g, ak, bk, batch, split, s);
+      case VIT_EPI_PATCH:
+        if (g.drop.thr) return launch_cfg<VIT_EPI_PATCH | EPI_DROP, true, true>(c, g, batch, split, s);
+        return launch_layout<VIT_EPI_PATCH>(c, g, ak, bk, batch, split, s);
       case VIT_EPI_SPLITK: return launch_layout<VIT_EPI_SPLITK>(c, g, ak, bk, batch, split, s);
       default: return hipErrorInvalidValue;
     }
@@ -979,6 +1026,7 @@ extern "C" int vit_gemm_bf16(const vit_gemm_args* a, vit_stream_t stream) {
         g2.C = (char*)d.C + r0 * a->ldc * csz;
         if (d.C2) g2.C2 = (char*)d.C2 + r0 * a->ldc2 * 2;
         if (d.aux) g2.aux = (const char*)d.aux + r0 * a->ldaux * (a->epilogue == VIT_EPI_BIAS_RESID_F32 ? 4 : 2);
+        g2.drop.row0 = (int)r0;  // dropout masks are indexed by the absolute row
         hipError_t e = run(cfg, g1);
         if (e == hipSuccess) e = run(0, g2);
         return vit::check_hip(e, "vit_gemm_bf16 launch");

@@ -73,7 +73,7 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const void* __restrict__ dy
                                                      const float* __restrict__ rstd, const float* __restrict__ gamma,
                                                      const float* __restrict__ dres, long lddres, float* __restrict__ dx,
                                                      long lddx, bf16_t* __restrict__ dxb, long lddxb,
-                                                     float* __restrict__ partial, int rows, int D) {
+                                                     float* __restrict__ partial, int rows, int D, DropDev drop) {
   __shared__ float red[4][NV * 256];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   float4 pg[NV], pb[NV], ps[NV];
@@ -129,6 +129,15 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const void* __restrict__ dy
         o.z = rs * (g[k].z - m1 - xh[k].z * m2) + r4[k].z;
         o.w = rs * (g[k].w - m1 - xh[k].w * m2) + r4[k].w;
         *reinterpret_cast<float4*>(dx + (long)row * lddx + c) = o;
+        if (drop.thr) {  // the copy / column sums feed the dropout-ed branch: gradient x mask
+          float m8[8];
+          drop_mult8(drop, row, c >> 3, m8);
+          const bool hi = c & 4;
+          o.x *= hi ? m8[4] : m8[0];
+          o.y *= hi ? m8[5] : m8[1];
+          o.z *= hi ? m8[6] : m8[2];
+          o.w *= hi ? m8[7] : m8[3];
+        }
         ps[k].x += o.x; ps[k].y += o.y; ps[k].z += o.z; ps[k].w += o.w;
         if (dxb) {
           uint2 u;
@@ -193,8 +202,9 @@ extern "C" int vit_layernorm_bwd(const void* dy, int64_t lddy, int32_t dy_f32, c
                                  const float* mean, const float* rstd, const float* gamma, const float* dres,
                                  int64_t lddres, float* dx, int64_t lddx, void* dx_bf16, int64_t lddxb, float* partial,
                                  float* dgamma_dbeta, float* dx_colsum, int32_t accumulate_params, int64_t rows,
-                                 int64_t D, vit_stream_t stream) {
+                                 int64_t D, const vit_dropout* dx_dropout, vit_stream_t stream) {
   VIT_CHECK_ARG(dy && x && mean && rstd && gamma && dx && partial, "vit_layernorm_bwd: null pointer");
+  const DropDev drop = make_drop(dx_dropout);
   VIT_CHECK_ARG(D > 0 && D % 4 == 0 && D <= 2048, "vit_layernorm_bwd: D=%lld unsupported", (long long)D);
   if (rows <= 0) return VIT_OK;
   const int64_t nblk = ln_bwd_blocks(rows);
@@ -204,7 +214,7 @@ extern "C" int vit_layernorm_bwd(const void* dy, int64_t lddy, int32_t dy_f32, c
   case n:                                                                                                           \
     hipLaunchKernelGGL(ln_bwd_kernel<n>, dim3((unsigned)nblk), dim3(256), 0, s, dy, (long)lddy, (int)dy_f32, x,     \
                        (long)ldx, mean, rstd, gamma, dres, (long)lddres, dx, (long)lddx, (bf16_t*)dx_bf16,           \
-                       (long)lddxb, partial, (int)rows, (int)D);                                                    \
+                       (long)lddxb, partial, (int)rows, (int)D, drop);                                              \
     break;
     C(1) C(2) C(3) C(4) C(5) C(6) C(7) C(8)
 #undef C

@@ -22,6 +22,12 @@ K_CONTIG, MN_CONTIG = 0, 1
  EPI_BIAS_GELU_DGELU, EPI_MUL_BF16) = range(10)
 
 
+class Dropout(ctypes.Structure):
+    """struct vit_dropout (include/vit_hip.h)"""
+    _fields_ = [("p", c_f32), ("site", ctypes.c_uint32), ("seed", ctypes.c_uint64), ("offset", ctypes.c_uint64),
+                ("row_stride", c_i64)]
+
+
 class GemmArgs(ctypes.Structure):
     _fields_ = [
         ("M", c_i64), ("N", c_i64), ("K", c_i64),
@@ -33,7 +39,7 @@ class GemmArgs(ctypes.Structure):
         ("bias", c_vp), ("bias_batch_stride", c_i64),
         ("aux", c_vp), ("ldaux", c_i64), ("aux2", c_vp),
         ("batch", c_i64), ("split_k", c_i64), ("tokens", c_i64), ("col_partial", c_vp),
-        ("epilogue", c_i32), ("tile", c_i32),
+        ("epilogue", c_i32), ("tile", c_i32), ("dropout", ctypes.POINTER(Dropout)),
     ]
 
 
@@ -47,11 +53,13 @@ _SIGS = {
     "vit_layernorm_fwd": (c_i32, [c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_i32, c_vp, c_vp, c_i64, c_i64, c_f32, c_vp]),
     "vit_layernorm_bwd_partial_rows": (c_i64, [c_i64]),
     "vit_layernorm_bwd": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_i64,
-                                  c_vp, c_i64, c_vp, c_vp, c_vp, c_i32, c_i64, c_i64, c_vp]),
+                                  c_vp, c_i64, c_vp, c_vp, c_vp, c_i32, c_i64, c_i64, ctypes.POINTER(Dropout),
+                                  c_vp]),
     "vit_attention_fwd": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_f32, c_vp]),
     "vit_attention_bwd": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_f32, c_vp]),
     "vit_im2col": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp]),
-    "vit_embed_grad": (c_i32, [c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp]),
+    "vit_embed_grad": (c_i32, [c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, ctypes.POINTER(Dropout), c_vp]),
+    "vit_dropout_mask": (c_i32, [ctypes.POINTER(Dropout), c_i64, c_i64, c_i64, c_vp, c_i64, c_vp]),
     "vit_colsum_partial_rows": (c_i64, [c_i64]),
     "vit_colsum": (c_i32, [c_vp, c_i32, c_i64, c_i64, c_i64, c_vp, c_vp, c_i32, c_vp]),
     "vit_gemm_f32": (c_i32, [c_i64, c_i64, c_i64, c_vp, c_i64, c_i32, c_vp, c_i64, c_i32, c_vp, c_i64, c_vp, c_i32,

@@ -211,6 +211,12 @@ class ViTEngine:
         self.overlap_wgrad = True    # weight-gradient GEMMs on a side stream, overlapped with the dgrad chain
         self._side = None
         self.probe = None  # list: (start, end) HIP events around every fc1 forward GEMM launch
+        # dropout (nn.Dropout of PositionEmbs / EncoderBlock / MlpBlock, reference src/model.py:19-20,
+        # 46-49, 124-125): counter-based Philox masks keyed by (seed, per-forward offset, site, row,
+        # col), regenerated by the backward instead of stored. Seeded from torch's initial seed.
+        self.drop_seed = (torch.initial_seed() * 0x9E3779B97F4A7C15 + 0x632BE59BD9B4E019) & (2**64 - 1)
+        self._drop_offset = 0
+        self._drop = None  # (p, seed, offset) of the last forward, or None
 
     # ---- parameters --------------------------------------------------------------------------
     def pv(self, name, buf=None):
@@ -299,8 +305,17 @@ class ViTEngine:
         ops.splitk_reduce(ws, batch, s, M, N, out, ldo, out_bs)
 
     # ---- forward -------------------------------------------------------------------------------
-    def forward(self, x: torch.Tensor):
-        """x: [b, 3, img, img] fp32 on the device. Returns logits [b, C] (fp32, engine-owned)."""
+    def _dd(self, site, row_stride=1):
+        """dropout descriptor of `site` for the last forward (None when dropout is off)."""
+        if self._drop is None:
+            return None
+        p, seed, off = self._drop
+        return ops.dropout_desc(p, site, seed, off, row_stride)
+
+    def forward(self, x: torch.Tensor, dropout_p: float = 0.0):
+        """x: [b, 3, img, img] fp32 on the device. Returns logits [b, C] (fp32, engine-owned).
+        dropout_p > 0: training-mode nn.Dropout(p) at the reference's four sites per model
+        (position embedding; per layer the attention output, GELU output and fc2 output)."""
         cfg = self.cfg
         if x.dim() != 4 or x.shape[1] != 3 or x.shape[2] != cfg.image_size or x.shape[3] != cfg.image_size:
             raise ValueError(f"expected input [b, 3, {cfg.image_size}, {cfg.image_size}], got {tuple(x.shape)}")
@@ -312,13 +327,21 @@ class ViTEngine:
         T = a.T
         mv = self.mirror
         f = self.flat
+        if dropout_p and dropout_p > 0.0:
+            if not dropout_p < 1.0:
+                raise ValueError(f"dropout probability has to be in [0, 1), got {dropout_p}")
+            self._drop_offset += 1
+            self._drop = (float(dropout_p), self.drop_seed, self._drop_offset)
+        else:
+            self._drop = None
+        dd = self._dd
         # patch embedding: im2col + GEMM with conv-bias / cls / pos-emb epilogue
         ops.im2col(x, a.patches, b, cfg.image_size, cfg.patch_size, a.kpad)
         wconv = self.wconv if self.wconv is not None else mv[self.off("embedding.weight"):]
         ops.gemm(a.patches, wconv, a.h[0], T, D, a.kpad, a_layout=K_CONTIG, b_layout=K_CONTIG, lda=a.kpad,
                  ldb=a.kpad, ldc=D, epilogue=EPI_PATCH, bias=f[self.off("embedding.bias"):],
                  aux=f[self.off("transformer.pos_embedding.pos_embedding"):], ldaux=D,
-                 aux2=f[self.off("cls_token"):], tokens=N)
+                 aux2=f[self.off("cls_token"):], tokens=N, dropout=dd(0))
         scale = 1.0 / math.sqrt(hd)
         for i in range(L):
             ln = lambda s: self.off(self.lname(i, s))
@@ -329,7 +352,7 @@ class ViTEngine:
             ops.attention_fwd(a.qkv[i], a.o[i], a.lse[i], b, N, H, hd, scale)
             ops.gemm(a.o[i], self.woutt[i], a.hm[i], T, D, D, a_layout=K_CONTIG, b_layout=K_CONTIG,
                      lda=D, ldb=D, ldc=D, epilogue=EPI_BIAS_RESID_F32, bias=f[ln("attn.out.bias"):], aux=a.h[i],
-                     ldaux=D)
+                     ldaux=D, dropout=dd(1 + 3 * i))
             ops.layernorm_fwd(a.hm[i], D, f[ln("norm2.weight"):], f[ln("norm2.bias"):], a.ln2[i], D, a.mu2[i],
                               a.rs2[i], T, D)
             if self.probe is not None:
@@ -337,14 +360,14 @@ class ViTEngine:
                 ev0.record()
             ops.gemm(a.ln2[i], mv[ln("mlp.fc1.weight"):], a.gp[i], T, M, D, a_layout=K_CONTIG, b_layout=K_CONTIG,
                      lda=D, ldb=D, ldc=M, epilogue=EPI_BIAS_GELU_DGELU, bias=f[ln("mlp.fc1.bias"):], C2=a.g[i],
-                     ldc2=M)
+                     ldc2=M, dropout=dd(2 + 3 * i))
             if self.probe is not None:
                 ev1 = torch.cuda.Event(enable_timing=True)
                 ev1.record()
                 self.probe.append((ev0, ev1))
             ops.gemm(a.g[i], mv[ln("mlp.fc2.weight"):], a.h[i + 1], T, D, M, a_layout=K_CONTIG, b_layout=K_CONTIG,
                      lda=M, ldb=M, ldc=D, epilogue=EPI_BIAS_RESID_F32, bias=f[ln("mlp.fc2.bias"):], aux=a.hm[i],
-                     ldaux=D)
+                     ldaux=D, dropout=dd(3 + 3 * i))
         # final LayerNorm on the cls rows only (only row 0 reaches the classifier, src/model.py:210)
         ops.layernorm_fwd(a.h[L], N * D, f[self.off("transformer.norm.weight"):], f[self.off("transformer.norm.bias"):],
                           a.lncls, D, a.muf, a.rsf, b, D)
@@ -430,6 +453,7 @@ class ViTEngine:
         gv = lambda name: g[self.off(name):]
         dl = dlogits.to(self.dev, torch.float32).contiguous()
         hook = self.grad_ready_hook
+        dd = self._dd
         main = torch.cuda.current_stream(self.dev)
         overlap = self.overlap_wgrad
         if overlap and self._side is None:
@@ -482,7 +506,7 @@ class ViTEngine:
         ops.layernorm_bwd(a.dlncls, D, a.h[L], N * D, a.muf, a.rsf, f[self.off("transformer.norm.weight"):], a.dh,
                           N * D, a.lnpart, b, D, dx_bf16=a.dhb[wb], lddxb=N * D,
                           dgamma_dbeta=gv("transformer.norm.weight"),
-                          dx_colsum=gv(self.lname(L - 1, "mlp.fc2.bias")))
+                          dx_colsum=gv(self.lname(L - 1, "mlp.fc2.bias")), dx_dropout=dd(3 + 3 * (L - 1), N))
         fire(self.layout.buckets[0])
         scale = 1.0 / math.sqrt(hd)
         for i in reversed(range(L)):
@@ -510,7 +534,7 @@ class ViTEngine:
             ops.layernorm_bwd(a.dyln, D, a.hm[i], D, a.mu2[i], a.rs2[i], f[ln("norm2.weight"):], a.dh, D, a.lnpart, T,
                               D, dres=a.dh, lddres=D, dx_bf16=dhb, lddxb=D,
                               dgamma_dbeta=gv(self.lname(i, "norm2.weight")),
-                              dx_colsum=gv(self.lname(i, "attn.out.bias")))
+                              dx_colsum=gv(self.lname(i, "attn.out.bias")), dx_dropout=dd(1 + 3 * i))
             # ---- attention: hm = h + out(attn(ln1(h))) ----
             on_side(lambda: self._wgrad(a.o[i], D, dhb, D, D, D, a.Tp, gv(self.lname(i, "attn.out.weight")), D))
             release("dhb", wb)
@@ -533,14 +557,15 @@ class ViTEngine:
             ops.layernorm_bwd(a.dyln, D, a.h[i], D, a.mu1[i], a.rs1[i], f[ln("norm1.weight"):], a.dh, D, a.lnpart, T,
                               D, dres=a.dh, lddres=D, dx_bf16=a.dhb[wb], lddxb=D,
                               dgamma_dbeta=gv(self.lname(i, "norm1.weight")),
-                              dx_colsum=gv(self.lname(i - 1, "mlp.fc2.bias")) if i > 0 else None)
+                              dx_colsum=gv(self.lname(i - 1, "mlp.fc2.bias")) if i > 0 else None,
+                              dx_dropout=dd(3 + 3 * (i - 1)) if i > 0 else dd(0))
             fire(self.layout.buckets[L - i])
         # ---- embedding: conv weight grad (wgrad over patches), bias / pos / cls ----
         dhb = a.dhb[wb]
         on_side(lambda: self._wgrad(dhb, D, a.patches, a.kpad, D, cfg.patch_k, a.Tp, gv("embedding.weight"),
                                     cfg.patch_k))
         ops.embed_grad(a.dh, b, N, D, gv("transformer.pos_embedding.pos_embedding"), gv("cls_token"),
-                       gv("embedding.bias"))
+                       gv("embedding.bias"), dropout=dd(0))
         fire(self.layout.buckets[-1])
         if overlap:
             main.wait_stream(side)

@@ -127,7 +127,7 @@ class _ViTFunction(torch.autograd.Function):
     @staticmethod
     def forward(ctx, model, x, *params):
         eng = model._engine
-        logits = eng.forward(x)
+        logits = eng.forward(x, dropout_p=model.dropout_rate if model.training else 0.0)
         ctx.model = model
         ctx.step = eng.step_id
         return logits.clone()
@@ -226,11 +226,12 @@ class VisionTransformer(nn.Module):
         return self._engine
 
     def forward(self, x):
-        if self.training and (self.dropout_rate > 0 or self.attn_dropout_rate > 0):
-            raise NotImplementedError("dropout > 0 is not implemented on the MI355X path yet (presets use 0.0, "
-                                      "reference src/config.py:64-65)")
+        # (attn_dropout_rate builds SelfAttention.dropout, which the reference never applies: src/model.py:78-99)
         eng = self.engine()
         if self.precision == "fp32":
+            if self.training and self.dropout_rate > 0:
+                raise NotImplementedError("precision='fp32' is the forward-only exact path; train-mode dropout runs on "
+                                          "the bf16 path (use model.eval() for fp32 evaluation)")
             if torch.is_grad_enabled() and any(p.requires_grad for p in self._flat_params):
                 raise RuntimeError("precision='fp32' is the forward-only exact path; run it under torch.no_grad() "
                                    "(training uses precision='bf16')")

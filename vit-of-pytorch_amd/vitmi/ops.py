@@ -11,7 +11,7 @@ import ctypes
 import torch
 
 from . import _lib
-from ._lib import GemmArgs, check
+from ._lib import Dropout, GemmArgs, check
 
 BF16 = torch.bfloat16
 F32 = torch.float32
@@ -41,7 +41,7 @@ def _chk(t, dtype, name):
 # ---------------------------------------------------------------------------------------------
 def _gemm_args(A, B, C, M, N, K, *, a_layout, b_layout, lda, ldb, ldc, epilogue, bias=None, aux=None, ldaux=0,
                C2=None, ldc2=0, aux2=None, batch=1, a_bs=0, b_bs=0, c_bs=0, bias_bs=0, split_k=1, tokens=0, tile=0,
-               col_partial=None):
+               col_partial=None, dropout=None):
     a = GemmArgs()
     a.M, a.N, a.K = M, N, K
     a.A, a.lda, a.a_batch_stride, a.a_layout = A.data_ptr(), lda, a_bs, a_layout
@@ -54,7 +54,25 @@ def _gemm_args(A, B, C, M, N, K, *, a_layout, b_layout, lda, ldb, ldc, epilogue,
     a.batch, a.split_k, a.tokens = batch, split_k, tokens
     a.col_partial = col_partial.data_ptr() if col_partial is not None else None
     a.epilogue, a.tile = epilogue, tile
+    a.dropout = ctypes.pointer(dropout) if dropout is not None else None
     return a
+
+
+def dropout_desc(p, site, seed, offset, row_stride=1):
+    """struct vit_dropout for nn.Dropout(p) at `site` (None when p == 0)."""
+    if not p:
+        return None
+    return Dropout(float(p), int(site), int(seed) & (2**64 - 1), int(offset) & (2**64 - 1), int(row_stride))
+
+
+def _dp(d):
+    return ctypes.pointer(d) if d is not None else None
+
+
+def dropout_mask(d, row0, rows, cols, out, ld):
+    """out[r, c] = multiplier (0 or 1/(1-p)) of element (row0 + r, c) of dropout descriptor d."""
+    _chk(out, F32, "out")
+    check(lib().vit_dropout_mask(_dp(d), row0, rows, cols, _p(out), ld, _stream()), "vit_dropout_mask")
 
 
 def gemm(A, B, C, M, N, K, **kw):
@@ -87,10 +105,11 @@ def layernorm_bwd_partial_rows(rows):
 
 
 def layernorm_bwd(dy, lddy, x, ldx, mean, rstd, gamma, dx, lddx, partial, rows, D, *, dres=None, lddres=0,
-                  dx_bf16=None, lddxb=0, dgamma_dbeta=None, dx_colsum=None, accumulate=False):
+                  dx_bf16=None, lddxb=0, dgamma_dbeta=None, dx_colsum=None, accumulate=False, dx_dropout=None):
     check(lib().vit_layernorm_bwd(_p(dy), lddy, int(dy.dtype == F32), _p(x), ldx, _p(mean), _p(rstd), _p(gamma),
                                   _p(dres), lddres, _p(dx), lddx, _p(dx_bf16), lddxb, _p(partial), _p(dgamma_dbeta),
-                                  _p(dx_colsum), int(accumulate), rows, D, _stream()), "vit_layernorm_bwd")
+                                  _p(dx_colsum), int(accumulate), rows, D, _dp(dx_dropout), _stream()),
+          "vit_layernorm_bwd")
 
 
 def attention_fwd(qkv, o, lse, B, N, H, hd, scale):
@@ -111,8 +130,9 @@ def im2col(x, out, B, img, P, Kpad):
     check(lib().vit_im2col(_p(x), _p(out), B, img, P, Kpad, _stream()), "vit_im2col")
 
 
-def embed_grad(dh0, B, N, D, dpos, dcls, dconv_bias):
-    check(lib().vit_embed_grad(_p(dh0), B, N, D, _p(dpos), _p(dcls), _p(dconv_bias), _stream()), "vit_embed_grad")
+def embed_grad(dh0, B, N, D, dpos, dcls, dconv_bias, dropout=None):
+    check(lib().vit_embed_grad(_p(dh0), B, N, D, _p(dpos), _p(dcls), _p(dconv_bias), _dp(dropout), _stream()),
+          "vit_embed_grad")
 
 
 def colsum_partial_rows(rows):
