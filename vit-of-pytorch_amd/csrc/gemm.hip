@@ -47,6 +47,7 @@ struct GemmDev {
   int group_m;         // tile order: groups of group_m tile rows, column-major inside (0: row-major)
   int nt;              // non-temporal output stores (keep the operands resident in L2)
   DropDev drop;        // dropout on the PATCH / BIAS_RESID_F32 / BIAS_GELU_DGELU output (thr 0 = off)
+  int diag;            // diagnostics (VIT_GEMM_DIAG): 1 = skip the half-tile kernel's global stores, 2 = its epilogue
 };
 
 // blockIdx (after the XCD remap) -> output tile. Grouping tile rows keeps the weight panels a
@@ -959,6 +960,11 @@ extern "C" int vit_gemm_bf16(const vit_gemm_args* a, vit_stream_t stream) {
     }();
     d.group_m = env_gm;
     d.nt = env_nt;
+    static const int env_diag = [] {
+      const char* e = getenv("VIT_GEMM_DIAG");
+      return e ? atoi(e) : 0;
+    }();
+    d.diag = env_diag;
   }
   if (a->col_partial) {
     VIT_CHECK_ARG(a->batch == 1 && a->split_k == 1 && d.vec && a->N % 8 == 0 &&

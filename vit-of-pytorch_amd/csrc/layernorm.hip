@@ -86,10 +86,11 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const void* __restrict__ dy
     const int c = (k * 64 + lane) * 4;
     gm[k] = c < D ? *reinterpret_cast<const float4*>(gamma + c) : make_float4(0.f, 0.f, 0.f, 0.f);
   }
-  for (int row = blockIdx.x * 4 + wave; row < rows; row += gridDim.x * 4) {
-    // issue every load of the row up front (dy, x, residual grad, stats) so their latencies overlap
-    const float mu = mean[row], rs = rstd[row];
-    float4 d4[NV], x4[NV], r4[NV];
+  // rows are software-pipelined: the next row's loads (dy, x, residual grad, stats) are issued
+  // before this row's math and stores, so each wave keeps two rows of HBM reads in flight
+  auto load_row = [&](int row, float4* d4, float4* x4, float4* r4, float& mu, float& rs) {
+    mu = mean[row];
+    rs = rstd[row];
 #pragma unroll
     for (int k = 0; k < NV; ++k) {
       const int c = (k * 64 + lane) * 4;
@@ -106,6 +107,16 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const void* __restrict__ dy
         d4[k] = x4[k] = r4[k] = make_float4(0.f, 0.f, 0.f, 0.f);
       }
     }
+  };
+  const int stride = gridDim.x * 4;
+  float4 d4[NV], x4[NV], r4[NV];
+  float mu = 0.f, rs = 0.f;
+  int row = blockIdx.x * 4 + wave;
+  if (row < rows) load_row(row, d4, x4, r4, mu, rs);
+  for (; row < rows; row += stride) {
+    float4 dn[NV], xn[NV], rn[NV];
+    float mun = 0.f, rsn = 0.f;
+    if (row + stride < rows) load_row(row + stride, dn, xn, rn, mun, rsn);
     float4 xh[NV], g[NV];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
@@ -147,6 +158,14 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const void* __restrict__ dy
         }
       }
     }
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      d4[k] = dn[k];
+      x4[k] = xn[k];
+      r4[k] = rn[k];
+    }
+    mu = mun;
+    rs = rsn;
   }
   // block partials [dgamma | dbeta | dsum]: sum dy*xhat, sum dy, sum of the written dx (the
   // bias gradient of the linear layer that produced this residual stream)

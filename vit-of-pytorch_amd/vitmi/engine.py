@@ -16,6 +16,7 @@ autograd backward at src/train.py:23). Design:
 from __future__ import annotations
 
 import math
+import os
 from collections import OrderedDict
 from dataclasses import dataclass
 
@@ -208,7 +209,8 @@ class ViTEngine:
         self._ws = None
         self.step_id = 0
         self.grad_ready_hook = None  # callable(grad_buf, bucket_name, start, end, events) during backward
-        self.overlap_wgrad = True    # weight-gradient GEMMs on a side stream, overlapped with the dgrad chain
+        # weight-gradient GEMMs on a side stream, overlapped with the dgrad chain (VITMI_OVERLAP=0: serial)
+        self.overlap_wgrad = os.environ.get("VITMI_OVERLAP", "1") != "0"
         self._side = None
         self.probe = None  # list: (start, end) HIP events around every fc1 forward GEMM launch
         # dropout (nn.Dropout of PositionEmbs / EncoderBlock / MlpBlock, reference src/model.py:19-20,
