@@ -9,9 +9,10 @@
 //        registers), masked wavefront softmax, O^T = V^T P^T with V read by ds_read_b64_tr_b16.
 //        The P fragment is the S accumulator itself (keys permuted consistently on both MFMA
 //        operands), so P never touches LDS. Saves LSE (f32) for the backward.
-//   bwd: phase 1, each wave owns 16-key tiles: recompute P (key on the lane), dP, dS and
-//        accumulate dV^T, dK^T in registers over all queries. phase 2, each wave owns 16-query
-//        tiles: recompute S^T, dP^T and accumulate dQ^T. No atomics, deterministic.
+//   bwd: stage 1 (K, V in LDS), each wave owns 16-query strips: P and dP of the strip for all keys
+//        stay in registers, delta = sum P dP, dS = P (dP - delta), dQ = dS K. stage 2 (Q, dO in
+//        LDS), each wave owns pairs of 16-key tiles: recompute P, dS and accumulate dV = P^T dO,
+//        dK = dS^T Q in registers. No atomics, deterministic (details above attn_bwd_kernel).
 // LDS images: [rows][HD] bf16 with a 16-B-chunk XOR swizzle that is conflict-free for both the
 // row read (ds_read_b128) and the transposed read (ds_read_b64_tr_b16) at HD = 64.
 #include "common.h"
@@ -212,11 +213,13 @@ __device__ __forceinline__ float sum16(float v) {
 // ------------------------------------------------------------------------------------------------
 // Backward, two LDS images at a time (56 KB at N = 197, hd = 64: two workgroups per CU, so one
 // workgroup's image loads overlap the other's MFMA work).
-//   stage 1 (K, V images): each wave owns pairs of 16-query tiles, Q / dO rows in registers;
-//     pass A: delta_q = sum_j P_qj dP_qj from the recomputed P and dP themselves (FlashAttention-2's
-//     rowsum(dO * O) differs from it by bf16 O's rounding, and dS = P (dP - delta) is a small
-//     difference: that turned into 10-25% errors on the q/k weight gradients under near-uniform
-//     attention); pass B: dS and dQ = dS K.
+//   stage 1 (K, V images): each wave owns 16-query strips, Q / dO rows in registers (the next
+//     strip's requested one strip ahead). HD <= 64: P and dP of the strip for all keys are kept in
+//     registers, so delta_q = sum_j P_qj dP_qj (from the recomputed P and dP themselves:
+//     FlashAttention-2's rowsum(dO * O) differs from it by bf16 O's rounding, and dS = P (dP - delta)
+//     is a small difference: that turned into 10-25% errors on the q/k weight gradients under
+//     near-uniform attention), dS and dQ = dS K come from one pass. HD = 96 (too many registers):
+//     pairs of strips, pass A for delta, pass B recomputing S / dP for dS and dQ.
 //   stage 2 (Q, dO images): each wave owns pairs of 16-key tiles, K / V rows in registers; dV =
 //     P^T dO, dK = dS^T Q, with delta from stage 1.
 // Deterministic (no atomics). Optionally writes per-image column sums of dQ | dK | dV (q/k/v bias
@@ -594,15 +597,25 @@ __global__ void __launch_bounds__(NW * 64, 2) attn_bwd_kernel(const bf16_t* __re
   }
 }
 
-template <int HD, int NKT>
-hipError_t launch_fwd(const bf16_t* qkv, bf16_t* o, float* lse, int B, int N, int H, int hd, float scale,
-                      hipStream_t s) {
-  constexpr int NW = 4;
+template <int HD, int NKT, int NW>
+hipError_t launch_fwd_nw(const bf16_t* qkv, bf16_t* o, float* lse, int B, int N, int H, int hd, float scale,
+                         hipStream_t s) {
   const size_t lds = (size_t)2 * NKT * 16 * HD * 2;
   auto kern = attn_fwd_kernel<HD, NKT, NW>;
   if (lds > 64 * 1024) (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   hipLaunchKernelGGL(kern, dim3(B * H), dim3(NW * 64), lds, s, qkv, o, lse, N, H, hd, scale);
   return hipGetLastError();
+}
+
+template <int HD, int NKT>
+hipError_t launch_fwd(const bf16_t* qkv, bf16_t* o, float* lse, int B, int N, int H, int hd, float scale,
+                      hipStream_t s) {
+  static const int nw = [] {
+    const char* e = getenv("VIT_ATTN_FWD_NW");
+    return e ? atoi(e) : 4;
+  }();
+  if (nw == 8) return launch_fwd_nw<HD, NKT, 8>(qkv, o, lse, B, N, H, hd, scale, s);
+  return launch_fwd_nw<HD, NKT, 4>(qkv, o, lse, B, N, H, hd, scale, s);
 }
 
 template <int HD, int NKT, int NW>

@@ -239,6 +239,30 @@ __device__ __forceinline__ void ld8bf(const bf16_t* p, float* v) {
 }
 
 // 8 consecutive columns n..n+7 of row m (all in range, aligned: p.vec).
+// GELU(u) and GELU'(u) of two values on packed f32 math (v_pk_fma/mul/add_f32: two lanes' worth per
+// instruction; the two transcendentals per value stay scalar). erf from Abramowitz & Stegun 7.1.25,
+// |error| <= 2.5e-5 — two orders below the bf16 rounding of both outputs. This is the fc1 forward
+// epilogue, whose VALU (not its stores) was the largest cost of that GEMM after its main loop.
+typedef float f2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void gelu_dgelu2(f2v u, f2v& gelu, f2v& dgelu) {
+  const f2v one = {1.f, 1.f}, half = {0.5f, 0.5f};
+  const f2v x2 = u * u;
+  const f2v e = {__builtin_amdgcn_exp2f(x2.x * -0.72134752044448170f),  // exp(-u^2/2) = 2^(-u^2 log2(e)/2)
+                 __builtin_amdgcn_exp2f(x2.y * -0.72134752044448170f)};
+  const f2v au = __builtin_elementwise_abs(u);
+  const f2v a = __builtin_elementwise_fma(au, f2v{0.47047f * 0.70710678118654752f, 0.47047f * 0.70710678118654752f}, one);
+  const f2v t = {__builtin_amdgcn_rcpf(a.x), __builtin_amdgcn_rcpf(a.y)};
+  f2v q = __builtin_elementwise_fma(t, f2v{0.7478556f, 0.7478556f}, f2v{-0.0958798f, -0.0958798f});
+  q = __builtin_elementwise_fma(q, t, f2v{0.3480242f, 0.3480242f});
+  q = q * t;
+  const f2v erfa = __builtin_elementwise_fma(-q, e, one);  // erf(|u| / sqrt 2)
+  const f2v sg = {__builtin_copysignf(erfa.x, u.x), __builtin_copysignf(erfa.y, u.y)};
+  const f2v cdf = __builtin_elementwise_fma(sg, half, half);
+  const f2v pdf = e * f2v{0.39894228040143268f, 0.39894228040143268f};
+  gelu = u * cdf;
+  dgelu = __builtin_elementwise_fma(u, pdf, cdf);
+}
+
 // pre: the 8 aux values of (m, n..n+7) already loaded by the caller (GELU_BWD / MUL / RESID), or null.
 template <int EPI>
 __device__ __forceinline__ void epi_store8(const GemmDev& p, int z, int split_idx, int m, int n, float* v,
@@ -299,12 +323,13 @@ __device__ __forceinline__ void epi_store8(const GemmDev& p, int z, int split_id
   } else if constexpr (E == VIT_EPI_BIAS_GELU_DGELU) {
     float gl[8];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const float u = v[k] + b[k];
-      float pdf;
-      const float cdf = phi_and_pdf(u, &pdf);
-      gl[k] = u * cdf;
-      v[k] = cdf + u * pdf;
+    for (int k = 0; k < 8; k += 2) {
+      f2v g2, d2;
+      gelu_dgelu2(f2v{v[k] + b[k], v[k + 1] + b[k + 1]}, g2, d2);
+      gl[k] = g2.x;
+      gl[k + 1] = g2.y;
+      v[k] = d2.x;
+      v[k + 1] = d2.y;
     }
     if constexpr (DROP) {
       float dm[8];
