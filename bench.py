@@ -31,6 +31,7 @@ ARCHS = {
     "b32": dict(patch_size=32, emb_dim=768, mlp_dim=3072, num_heads=12, num_layers=12),
     "l16": dict(patch_size=16, emb_dim=1024, mlp_dim=4096, num_heads=16, num_layers=24),
     "l32": dict(patch_size=32, emb_dim=1024, mlp_dim=4096, num_heads=16, num_layers=24),
+    "h14": dict(patch_size=14, emb_dim=1280, mlp_dim=5120, num_heads=16, num_layers=32),
 }
 
 

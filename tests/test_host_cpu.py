@@ -23,7 +23,7 @@ def test_library_exports_every_header_symbol():
     for name in declared:
         assert hasattr(lib, name), name
     assert declared == set(_lib.EXPORTED), declared ^ set(_lib.EXPORTED)
-    assert lib.vit_abi_version() == 2
+    assert lib.vit_abi_version() == _lib.ABI_VERSION
 
 
 def test_flat_layout_and_buckets():

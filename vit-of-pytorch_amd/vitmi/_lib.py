@@ -16,6 +16,8 @@ c_i32 = ctypes.c_int32
 c_f32 = ctypes.c_float
 c_vp = ctypes.c_void_p
 
+ABI_VERSION = 2  # vit_abi_version() of the library these prototypes describe
+
 # enum vit_layout / vit_epilogue (include/vit_hip.h)
 K_CONTIG, MN_CONTIG = 0, 1
 (EPI_F32, EPI_BF16, EPI_BIAS_BF16, EPI_BIAS_GELU, EPI_BIAS_RESID_F32, EPI_GELU_BWD, EPI_PATCH, EPI_SPLITK,
@@ -100,6 +102,9 @@ def load(path: str | None = None):
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    if lib.vit_abi_version() != ABI_VERSION:
+        raise VitHipError(f"{p} has ABI {lib.vit_abi_version()}, the bindings expect {ABI_VERSION}: rebuild it "
+                          "(make -C vit-of-pytorch_amd)")
     _lib = lib
     return lib
 
