@@ -231,3 +231,25 @@ def test_bf16_step_head_dim_80():
     assert rel(logits, ref_logits) < 1e-2
     assert abs(float(loss.detach()) - float(ref_loss)) <= 1e-3 * abs(float(ref_loss))
     check_grads(m, ref_grads)
+
+
+def test_wgrad_side_stream_overlap_is_bit_identical():
+    """VITMI_OVERLAP=1 (weight-gradient GEMMs on a side stream) and the default serial order run the
+    same kernels on the same operands, so every gradient must agree bit for bit."""
+    cfg = SMALL
+    params = tame_params(init_params(cfg, seed=42))
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn(6, 3, cfg.image_size, cfg.image_size, generator=g).cuda()
+    y = torch.randint(0, cfg.num_classes, (6,), generator=g).cuda()
+    from vitmi.model import CrossEntropyLoss
+    grads = []
+    for overlap in (False, True):
+        m = make_model(cfg, params)
+        m(x[:1])  # builds the engine
+        m._engine.overlap_wgrad = overlap
+        m.zero_grad()
+        CrossEntropyLoss()(m(x), y).backward()
+        torch.cuda.synchronize()
+        grads.append({k: p.grad.detach().cpu().clone() for k, p in m.named_parameters()})
+    for k in grads[0]:
+        assert torch.equal(grads[0][k], grads[1][k]), k

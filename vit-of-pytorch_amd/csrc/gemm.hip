@@ -975,9 +975,12 @@ extern "C" int vit_gemm_bf16(const vit_gemm_args* a, vit_stream_t stream) {
   VIT_CHECK_ARG(!d.drop.thr || (a->a_layout == VIT_K_CONTIG && a->b_layout == VIT_K_CONTIG),
                 "vit_gemm_bf16: dropout epilogues need K-contiguous A and B");
   {
+    // tile order: groups of 8 tile rows, column-major inside, so the workgroups resident at once
+    // share A row panels and B column panels in L2 (fc1 fwd 326 -> 306 us; VIT_GEMM_GROUP_M=1:
+    // row-major)
     static const int env_gm = [] {
       const char* e = getenv("VIT_GEMM_GROUP_M");
-      return e ? atoi(e) : 0;
+      return e ? atoi(e) : 8;
     }();
     static const int env_nt = [] {
       const char* e = getenv("VIT_GEMM_NT");

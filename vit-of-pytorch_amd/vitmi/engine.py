@@ -209,8 +209,11 @@ class ViTEngine:
         self._ws = None
         self.step_id = 0
         self.grad_ready_hook = None  # callable(grad_buf, bucket_name, start, end, events) during backward
-        # weight-gradient GEMMs on a side stream, overlapped with the dgrad chain (VITMI_OVERLAP=0: serial)
-        self.overlap_wgrad = os.environ.get("VITMI_OVERLAP", "1") != "0"
+        # weight-gradient GEMMs on a side stream, overlapped with the dgrad chain (VITMI_OVERLAP=1).
+        # Off by default: the GEMMs of both streams share the CUs and each runs 30-40% slower than
+        # alone, so the serial order is faster on one MI355X (B/16 bs256: 6778 vs 6588 img/s,
+        # tools/sweep_env.sh). The DP all-reduce keeps its own stream either way (vitmi/dist.py).
+        self.overlap_wgrad = os.environ.get("VITMI_OVERLAP", "0") == "1"
         self._side = None
         self.probe = None  # list: (start, end) HIP events around every fc1 forward GEMM launch
         # dropout (nn.Dropout of PositionEmbs / EncoderBlock / MlpBlock, reference src/model.py:19-20,
