@@ -178,6 +178,20 @@ int vit_attention_bwd(const void* qkv, const void* o, const void* dout, const fl
 int vit_im2col(const float* x, void* out, int64_t B, int64_t img, int64_t P, int64_t Kpad,
                vit_stream_t stream);
 
+/* ----------------------------------------------------------------------------------------
+ * Training-input transform (src/data_loaders.py:66-80 CIFAR train, :100-112 ImageNet):
+ * torchvision Resize -> RandomHorizontalFlip -> ToTensor -> Normalize on the device.
+ * images uint8 HWC [B][H][W][3] (image b at images + b*image_stride bytes) -> out f32 NCHW
+ * [B,3,out_h,out_w] = (resized[c][y][flip ? out_w-1-x : x] / 255 - mean[c]) / std[c], with
+ * resized = Pillow Image.resize((out_w, out_h), BILINEAR) bit-exactly (8-bit fixed point,
+ * horizontal pass then vertical). flips: uint8 [B] (NULL = no flips). mean_std: host float[6] =
+ * {mean0..2, std0..2}. Replaces the reference's CPU DataLoader transform; the caller sizes
+ * out_h/out_w (torchvision's int-size rule lives in vitmi.data).
+ * ---------------------------------------------------------------------------------------- */
+int vit_preprocess_u8(const uint8_t* images, int64_t B, int64_t H, int64_t W, int64_t image_stride,
+                      const uint8_t* flips, int64_t out_h, int64_t out_w, const float* mean_std, float* out,
+                      vit_stream_t stream);
+
 /* token-level grads of the embedding (src/model.py:17,203-204): from dh0 f32 [B*N, D]:
  * dpos[n][d] = sum_b dh0[b*N+n][d]; dcls = dpos[0]; dconv_bias = sum_{n>=1} dpos[n].
  * dropout (optional): dh0 is taken through the position-embedding dropout's multipliers first. */

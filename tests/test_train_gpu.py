@@ -20,6 +20,32 @@ def test_train_main_b32_synthetic(capsys):
     assert "val_acc1" in out and "loss" in out
 
 
+def test_train_main_u8_images_through_device_transform(capsys):
+    """CIFAR-shaped uint8 32x32 images resized to 224 on the device (vitmi.data) feed the step."""
+    from vitmi import train
+    train.main(["--model-arch", "b32", "--batch-size", "8", "--synthetic", "--synthetic-source-size", "32",
+                "--checkpoint-path", "", "--steps-per-epoch", "4", "--train-steps", "8", "--warmup-steps", "2",
+                "--no-save", "--num-classes", "10"])
+    out = capsys.readouterr().out
+    assert "val_acc1" in out and "loss" in out
+
+
+def test_device_image_loader_batches_match_oracle_transform():
+    import numpy as np
+
+    from oracle.preprocess import transform_batch
+    from vitmi.train import DeviceImageLoader
+    rng = np.random.default_rng(0)
+    imgs = rng.integers(0, 256, (10, 32, 32, 3), dtype=np.uint8)
+    labels = np.arange(10)
+    ld = DeviceImageLoader(imgs, labels, 4, 48, "cuda", train=False)
+    got = [(x.cpu().numpy(), y.cpu().numpy()) for x, y in ld]
+    assert [len(y) for _, y in got] == [4, 4, 2]
+    x = np.concatenate([g[0] for g in got])
+    assert np.array_equal(np.concatenate([g[1] for g in got]), labels)
+    assert np.array_equal(x, transform_batch(imgs, 48))
+
+
 def test_data_parallel_two_ranks_replicas_identical(tmp_path):
     """2 ranks on one GPU over gloo (RCCL needs distinct GPUs): per-layer all-reduce overlapped with
     the backward; both replicas must end bit-identical and equal to one big-batch step."""

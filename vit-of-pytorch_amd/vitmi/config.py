@@ -4,6 +4,8 @@ Same flags, defaults and architecture presets (get_b16_config ... get_h14_config
 src/config.py:57-104). Additions for the MI355X path, all optional:
   --synthetic            synthetic N(0,1) images / uniform labels instead of torchvision datasets
   --steps-per-epoch      batches per synthetic epoch
+  --synthetic-source-size  >0: synthetic uint8 HWC images of this size, resized / flipped /
+                         normalised on the device like the reference's CIFAR transform (vitmi.data)
   --any-image-size       lift the reference's choices=[224, 384] on --image-size (src/config.py:37)
   --no-save              do not create experiments/ directories or checkpoints
 """
@@ -25,6 +27,8 @@ def _add_common(parser, train: bool):
     parser.add_argument("--seed", type=int, default=42, help="random seed for reproducibility")
     parser.add_argument("--synthetic", default=False, action="store_true", help="synthetic data (MI355X benchmark)")
     parser.add_argument("--steps-per-epoch", type=int, default=100, help="batches per synthetic epoch")
+    parser.add_argument("--synthetic-source-size", type=int, default=0,
+                        help="synthetic uint8 images of this size through the device transform (0: f32 N(0,1))")
     parser.add_argument("--any-image-size", default=False, action="store_true", help="allow any --image-size")
 
 

@@ -130,6 +130,25 @@ def im2col(x, out, B, img, P, Kpad):
     check(lib().vit_im2col(_p(x), _p(out), B, img, P, Kpad, _stream()), "vit_im2col")
 
 
+def preprocess_u8(images, out, flips=None, mean=(0.5, 0.5, 0.5), std=(0.5, 0.5, 0.5)):
+    """images uint8 [B, H, W, 3] (device, image rows contiguous) -> out f32 [B, 3, h, w]:
+    Pillow-exact bilinear resize, optional per-sample horizontal flip, ToTensor + Normalize."""
+    _chk(images, torch.uint8, "images")
+    _chk(out, F32, "out")
+    _chk(flips, torch.uint8, "flips")
+    if images.dim() != 4 or images.shape[3] != 3 or out.dim() != 4 or out.shape[1] != 3:
+        raise ValueError(f"preprocess_u8: images [B,H,W,3] -> out [B,3,h,w], got {tuple(images.shape)} -> "
+                         f"{tuple(out.shape)}")
+    B, H, W, _ = images.shape
+    if out.shape[0] != B or (flips is not None and flips.numel() != B):
+        raise ValueError("preprocess_u8: batch mismatch")
+    if images[0].stride() != (W * 3, 3, 1) or not out.is_contiguous():
+        raise ValueError("preprocess_u8: images must have contiguous [H, W, 3] rows and out must be contiguous")
+    ms = (ctypes.c_float * 6)(*[float(v) for v in mean], *[float(v) for v in std])
+    check(lib().vit_preprocess_u8(_p(images), B, H, W, images.stride(0) if B > 1 else H * W * 3, _p(flips),
+                                  out.shape[2], out.shape[3], ms, _p(out), _stream()), "vit_preprocess_u8")
+
+
 def embed_grad(dh0, B, N, D, dpos, dcls, dconv_bias, dropout=None):
     check(lib().vit_embed_grad(_p(dh0), B, N, D, _p(dpos), _p(dcls), _p(dconv_bias), _dp(dropout), _stream()),
           "vit_embed_grad")

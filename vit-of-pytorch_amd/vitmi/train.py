@@ -91,6 +91,35 @@ class SyntheticDataLoader:
             yield self.x, self.y
 
 
+class DeviceImageLoader:
+    """Batches of uint8 HWC images kept resident in HBM (CIFAR-100 train is 150 MB of uint8), run
+    through the reference loader's transform on the device (vitmi.data.GPUTransform:
+    Resize -> RandomHorizontalFlip -> ToTensor -> Normalize, src/data_loaders.py:66-80). Shuffled
+    per epoch with a seeded generator like the reference's DataLoader (`:84-92`); a ragged last
+    batch is kept (drop_last=False)."""
+
+    def __init__(self, images_u8, labels, batch_size, image_size, device, train=True, seed=42):
+        from .data import GPUTransform
+        self.images = torch.as_tensor(images_u8, dtype=torch.uint8).to(device).contiguous()
+        self.labels = torch.as_tensor(labels, dtype=torch.int64).to(device)
+        if self.images.dim() != 4 or self.images.shape[3] != 3 or self.labels.numel() != self.images.shape[0]:
+            raise ValueError("DeviceImageLoader: images uint8 [n, H, W, 3] and n labels")
+        self.batch_size, self.train = batch_size, train
+        self.generator = torch.Generator().manual_seed(seed)
+        self.transform = GPUTransform(image_size, train=train, generator=self.generator)
+
+    def __len__(self):
+        return (self.images.shape[0] + self.batch_size - 1) // self.batch_size
+
+    def __iter__(self):
+        n = self.images.shape[0]
+        order = torch.randperm(n, generator=self.generator) if self.train else torch.arange(n)
+        order = order.to(self.images.device)
+        for s in range(0, n, self.batch_size):
+            idx = order[s:s + self.batch_size]
+            yield self.transform(self.images.index_select(0, idx)), self.labels.index_select(0, idx)
+
+
 def _world():
     return dist.get_world_size() if dist.is_initialized() else 1
 
@@ -200,8 +229,17 @@ def main(argv=None):
     if not config.synthetic:
         raise SystemExit("torchvision datasets are not available in this environment; use --synthetic "
                          "(the input pipeline is outside the MI355X hot path, SURVEY.md §2 row 5)")
-    train_loader = SyntheticDataLoader(config.batch_size, config.image_size, config.num_classes,
-                                       config.steps_per_epoch, device, seed=config.seed + rank)
+    if config.synthetic_source_size > 0:
+        # uint8 images (CIFAR-shaped when 32) through the device-side reference transform
+        g = torch.Generator().manual_seed(config.seed + rank)
+        n = config.batch_size * config.steps_per_epoch
+        src = torch.randint(0, 256, (n, config.synthetic_source_size, config.synthetic_source_size, 3),
+                            generator=g, dtype=torch.uint8)
+        train_loader = DeviceImageLoader(src, torch.randint(0, config.num_classes, (n,), generator=g),
+                                         config.batch_size, config.image_size, device, seed=config.seed + rank)
+    else:
+        train_loader = SyntheticDataLoader(config.batch_size, config.image_size, config.num_classes,
+                                           config.steps_per_epoch, device, seed=config.seed + rank)
     valid_loader = SyntheticDataLoader(config.batch_size, config.image_size, config.num_classes,
                                        max(1, config.steps_per_epoch // 10), device, seed=10_000 + config.seed + rank)
 
