@@ -4,8 +4,8 @@
 // NCHW batch the model consumes. Resize is Pillow's 8-bit fixed-point bilinear resampling (the
 // library under torchvision's PIL path; restated and pinned in oracle/preprocess.py), reproduced
 // bit-exactly: coefficients in double without FMA contraction, horizontal pass clipped to uint8,
-// then the vertical pass. Ratios up to 4x (at most 9 taps per axis) run the tiled kernel, which
-// computes each column's and row's weights once per block; larger downsampling ratios run the
+// then the vertical pass. Ratios up to 4x (at most 9 taps per axis) run the tiled two-pass LDS
+// kernel, which computes each column's and row's weights once per block; larger ratios run the
 // generic kernel (one thread per output pixel, every weight recomputed - deterministically, so the
 // normalising sum and each weight still match Pillow).
 #include "common.h"
@@ -110,23 +110,27 @@ __global__ void __launch_bounds__(256) preprocess_kernel(PrepArgs p) {
   }
 }
 
-// Fast path (every axis with at most KMAX taps): a block owns 64 output columns x 32 output rows of
-// one image. The horizontal weights of a thread's column are computed once into registers (static
-// indexing, fully unrolled); the vertical weights of the block's 32 rows once into LDS by 32
-// threads. The per-pixel work is then the integer taps only (the generic kernel above recomputes
-// every weight, with its double division, per pixel).
-constexpr int kColsPerBlock = 64, kRowsPerBlock = 32, kRowLanes = 4;
+// Fast path (every axis with at most KMAX <= 9 taps, i.e. ratios up to 4x): a block owns 64 output
+// columns x 32 output rows of one image and runs Pillow's two passes through LDS. Pass 1: the
+// horizontal pass over the band of input rows those 32 output rows read (at most 31 * 4 + 1 + 9
+// rows), each thread one output column with its weights in registers (computed once), results
+// clipped to 8 bits into LDS. Pass 2: the vertical pass for the 32 rows from LDS with the row
+// weights (computed once per block by 32 threads). Every input pixel is gathered once per block
+// instead of once per output row that uses it.
+constexpr int kColsPerBlock = 64, kRowsPerBlock = 32, kRowLanes = 4, kBandMax = 31 * 4 + 1 + 9;
 
 template <int KMAX>
 __global__ void __launch_bounds__(kColsPerBlock* kRowLanes) preprocess_tiled_kernel(PrepArgs p) {
 #pragma clang fp contract(off)
   __shared__ int s_ky[kRowsPerBlock][KMAX];
   __shared__ int s_ymin[kRowsPerBlock], s_ycnt[kRowsPerBlock];
+  __shared__ uint32_t s_h[kBandMax][kColsPerBlock];  // horizontal pass, (r, g, b) bytes
   const Axis ax = make_axis(p.W, p.ow), ay = make_axis(p.H, p.oh);
   const int b = blockIdx.z;
   const int y0 = blockIdx.y * kRowsPerBlock;
+  const int rows = p.oh - y0 < kRowsPerBlock ? p.oh - y0 : kRowsPerBlock;
   const int tid = threadIdx.y * kColsPerBlock + threadIdx.x;
-  if (tid < kRowsPerBlock && y0 + tid < p.oh) {
+  if (tid < rows) {
     int ymin, ycnt;
     double yc, yw;
     taps(ay, y0 + tid, ymin, ycnt, yc, yw);
@@ -146,16 +150,12 @@ __global__ void __launch_bounds__(kColsPerBlock* kRowLanes) preprocess_tiled_ker
     for (int k = 0; k < KMAX; ++k) kx[k] = k < xcnt ? coeff(ax, k, xmin, xc, xw) : 0;
   }
   __syncthreads();
-  if (!live) return;
-  const uint8_t* img = p.in + (long)b * p.in_bs + (long)xmin * 3;
-  const long plane = (long)p.oh * p.ow;
-  float* o = p.out + (long)b * 3 * plane + x;
-  const int rows = p.oh - y0 < kRowsPerBlock ? p.oh - y0 : kRowsPerBlock;
-  for (int r = threadIdx.y; r < rows; r += kRowLanes) {
-    const int ymin = s_ymin[r], ycnt = s_ycnt[r];
-    int acc0 = 1 << (kPrecisionBits - 1), acc1 = acc0, acc2 = acc0;
-    for (int j = 0; j < ycnt; ++j) {
-      const uint8_t* row = img + (long)(ymin + j) * p.W * 3;
+  const int band0 = s_ymin[0];
+  const int nband = s_ymin[rows - 1] + s_ycnt[rows - 1] - band0;  // <= kBandMax (host: ksize <= 9)
+  if (live) {
+    const uint8_t* src = p.in + (long)b * p.in_bs + ((long)band0 * p.W + xmin) * 3;
+    for (int r = threadIdx.y; r < nband; r += kRowLanes) {
+      const uint8_t* row = src + (long)r * p.W * 3;
       int h0 = 1 << (kPrecisionBits - 1), h1 = h0, h2 = h0;
 #pragma unroll
       for (int k = 0; k < KMAX; ++k) {
@@ -165,10 +165,22 @@ __global__ void __launch_bounds__(kColsPerBlock* kRowLanes) preprocess_tiled_ker
           h2 += row[3 * k + 2] * kx[k];
         }
       }
+      s_h[r][threadIdx.x] = (uint32_t)clip8(h0) | ((uint32_t)clip8(h1) << 8) | ((uint32_t)clip8(h2) << 16);
+    }
+  }
+  __syncthreads();
+  if (!live) return;
+  const long plane = (long)p.oh * p.ow;
+  float* o = p.out + (long)b * 3 * plane + x;
+  for (int r = threadIdx.y; r < rows; r += kRowLanes) {
+    const int ymin = s_ymin[r] - band0, ycnt = s_ycnt[r];
+    int acc0 = 1 << (kPrecisionBits - 1), acc1 = acc0, acc2 = acc0;
+    for (int j = 0; j < ycnt; ++j) {
+      const uint32_t hv = s_h[ymin + j][threadIdx.x];
       const int cy = s_ky[r][j];
-      acc0 += clip8(h0) * cy;
-      acc1 += clip8(h1) * cy;
-      acc2 += clip8(h2) * cy;
+      acc0 += (int)(hv & 0xffu) * cy;
+      acc1 += (int)((hv >> 8) & 0xffu) * cy;
+      acc2 += (int)((hv >> 16) & 0xffu) * cy;
     }
     const long off = (long)(y0 + r) * p.ow;
     o[off] = ((float)clip8(acc0) / 255.0f - p.mean[0]) / p.stdv[0];
