@@ -187,6 +187,10 @@ def main():
     imgs = args.steps * b * world
     value = imgs / dt
     fpi = train_flops_per_image(arch, args.image_size, args.num_classes)
+    # executed work: with the last layer pruned to its cls rows (engine.prune_last, only they reach
+    # the classifier) its out-proj / fc1 / fc2 skip N-1 tokens per image in forward, dgrad and wgrad
+    D_, M_, N_ = cfg.emb_dim, cfg.mlp_dim, cfg.tokens
+    fpe = fpi - (3 * 2 * (N_ - 1) * (D_ * D_ + 2 * D_ * M_) if eng.prune_last else 0)
     traffic = pmc_traffic() if args.arch == "b16" and b == 256 else None
     step_tflops_per_gpu = value / world * fpi / 1e12
     out = {
@@ -215,8 +219,10 @@ def main():
                      "traffic_detail": traffic,
                      "algorithmic_bytes": T * cfg.emb_dim * 2 + cfg.mlp_dim * cfg.emb_dim * 2 + 2 * T * cfg.mlp_dim * 2,
                      "avg_launch_ms": round(fc1_ms, 4), "launches": len(probe)},
-        "step_mfma_frac": round(step_tflops_per_gpu / PEAK_BF16_TFLOPS, 4),
+        "step_mfma_frac": round(value / world * fpe / 1e12 / PEAK_BF16_TFLOPS, 4),
+        "step_mfma_frac_algorithmic": round(step_tflops_per_gpu / PEAK_BF16_TFLOPS, 4),
         "train_gflop_per_image": round(fpi / 1e9, 3),
+        "executed_gflop_per_image": round(fpe / 1e9, 3),
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(arch, args.image_size, args.num_classes, args.cpu_seconds)

@@ -253,3 +253,32 @@ def test_wgrad_side_stream_overlap_is_bit_identical():
         grads.append({k: p.grad.detach().cpu().clone() for k, p in m.named_parameters()})
     for k in grads[0]:
         assert torch.equal(grads[0][k], grads[1][k]), k
+
+
+def test_last_layer_cls_pruning_matches_full_tokens():
+    """ViTEngine.prune_last runs the last layer's out-proj / LN2 / MLP on the cls rows only; the
+    logits, loss and every gradient must match the all-token run (only summation order differs)."""
+    cfg = SMALL
+    params = tame_params(init_params(cfg, seed=42))
+    g = torch.Generator().manual_seed(12)
+    x = torch.randn(5, 3, cfg.image_size, cfg.image_size, generator=g).cuda()
+    y = torch.randint(0, cfg.num_classes, (5,), generator=g).cuda()
+    from vitmi.model import CrossEntropyLoss
+    runs = []
+    for prune in (False, True):
+        m = make_model(cfg, params)
+        m(x[:1])
+        m._engine.prune_last = prune
+        m.zero_grad()
+        logits = m(x)
+        loss = CrossEntropyLoss()(logits, y)
+        loss.backward()
+        torch.cuda.synchronize()
+        runs.append((logits.detach().cpu().clone(), float(loss.detach()),
+                     {k: p.grad.detach().cpu().clone() for k, p in m.named_parameters()}))
+    (l0, s0, g0), (l1, s1, g1) = runs
+    assert rel(l1, l0) < 1e-3 and abs(s1 - s0) <= 1e-4 * abs(s0)
+    tot = math.sqrt(sum(float(t.double().norm()) ** 2 for t in g0.values()))
+    for k in g0:
+        d = float((g1[k].double() - g0[k].double()).norm())
+        assert d <= max(2e-3 * float(g0[k].double().norm()), 1e-5 * tot), (k, d)

@@ -3,6 +3,8 @@
 // row is read once and written once; 16-B loads per lane). Statistics in fp32.
 #include "common.h"
 
+#include <cstdlib>
+
 namespace {
 
 // NV = float4 chunks per lane (D <= NV * 256).
@@ -65,7 +67,10 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(const float* __restrict__ x
   }
 }
 
-constexpr int LN_BWD_MAX_BLOCKS = 1024;
+// The row-pipelined backward needs 187 VGPRs (2 waves per SIMD): 512 four-wave blocks are all
+// resident at once on 256 CUs, and each wave walks ~25 rows (B/16 bs256: 123 vs 129 us isolated
+// at 1024 blocks, +0.3% step; VIT_LN_BWD_BLOCKS overrides).
+constexpr int LN_BWD_MAX_BLOCKS = 512;
 
 template <int NV>
 __global__ void __launch_bounds__(256) ln_bwd_kernel(const void* __restrict__ dy, long lddy, int dy_f32,
@@ -206,8 +211,12 @@ extern "C" int vit_layernorm_fwd(const float* x, int64_t ldx, const float* gamma
 }
 
 static int64_t ln_bwd_blocks(int64_t rows) {
+  static const int64_t cap = [] {
+    const char* e = getenv("VIT_LN_BWD_BLOCKS");
+    return e && atoi(e) > 0 ? (int64_t)atoi(e) : (int64_t)LN_BWD_MAX_BLOCKS;
+  }();
   int64_t b = (rows + 3) / 4;
-  if (b > LN_BWD_MAX_BLOCKS) b = LN_BWD_MAX_BLOCKS;
+  if (b > cap) b = cap;
   return b < 1 ? 1 : b;
 }
 

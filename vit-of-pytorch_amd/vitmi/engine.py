@@ -165,6 +165,13 @@ class _Acts:
         self.colpart = z(ops.colsum_partial_rows(T), max(3 * D, M, cfg.num_classes), dt=f)
         self.gelu_part = z(-(-T // 128), M, dt=f)   # per-M-tile column sums of dU (fc1 bias grad)
         self.qkv_bpart = z(b, 3 * D, dt=f)          # per-image column sums of dq|dk|dv (q/k/v bias grads)
+        # last encoder layer on the cls rows only (ViTEngine.prune_last): compact operands, rows
+        # padded to 64 with zeros that are never written (they are K rows of weight gradients)
+        bp = _rup(b, 64)
+        self.bp = bp
+        self.c_o, self.c_ln2, self.c_dh, self.c_dh2, self.c_dyln = (z(bp, D) for _ in range(5))
+        self.c_g, self.c_gp, self.c_dg = (z(bp, M) for _ in range(3))
+        self.c_mu2, self.c_rs2 = z(b, dt=f), z(b, dt=f)
 
 
 class ViTEngine:
@@ -214,6 +221,13 @@ class ViTEngine:
         # alone, so the serial order is faster on one MI355X (B/16 bs256: 6778 vs 6588 img/s,
         # tools/sweep_env.sh). The DP all-reduce keeps its own stream either way (vitmi/dist.py).
         self.overlap_wgrad = os.environ.get("VITMI_OVERLAP", "0") == "1"
+        # Only the cls token of the last layer's output reaches the classifier (src/model.py:210),
+        # so that layer's out-projection, LayerNorm 2 and MLP (forward and backward) run on the b cls
+        # rows; attention and the q|k|v projection stay full (every token is a key / value of the
+        # cls query). Same logits, loss and gradients (zero rows add exact zeros); VITMI_PRUNE_LAST=0
+        # runs every token. Off while dropout is active.
+        self.prune_last = os.environ.get("VITMI_PRUNE_LAST", "1") != "0"
+        self._pruned = False
         self._side = None
         self.probe = None  # list: (start, end) HIP events around every fc1 forward GEMM launch
         # dropout (nn.Dropout of PositionEmbs / EncoderBlock / MlpBlock, reference src/model.py:19-20,
@@ -348,6 +362,7 @@ class ViTEngine:
                  aux=f[self.off("transformer.pos_embedding.pos_embedding"):], ldaux=D,
                  aux2=f[self.off("cls_token"):], tokens=N, dropout=dd(0))
         scale = 1.0 / math.sqrt(hd)
+        self._pruned = self.prune_last and self._drop is None
         for i in range(L):
             ln = lambda s: self.off(self.lname(i, s))
             ops.layernorm_fwd(a.h[i], D, f[ln("norm1.weight"):], f[ln("norm1.bias"):], a.ln1[i], D, a.mu1[i],
@@ -355,6 +370,9 @@ class ViTEngine:
             ops.gemm(a.ln1[i], self.wqkvt[i], a.qkv[i], T, 3 * D, D, a_layout=K_CONTIG, b_layout=K_CONTIG, lda=D,
                      ldb=D, ldc=3 * D, epilogue=EPI_BIAS_BF16, bias=self.bqkv[i])
             ops.attention_fwd(a.qkv[i], a.o[i], a.lse[i], b, N, H, hd, scale)
+            if self._pruned and i == L - 1:
+                self._forward_last_cls(a, i, b)
+                break
             ops.gemm(a.o[i], self.woutt[i], a.hm[i], T, D, D, a_layout=K_CONTIG, b_layout=K_CONTIG,
                      lda=D, ldb=D, ldc=D, epilogue=EPI_BIAS_RESID_F32, bias=f[ln("attn.out.bias"):], aux=a.h[i],
                      ldaux=D, dropout=dd(1 + 3 * i))
@@ -382,6 +400,53 @@ class ViTEngine:
         self.step_id += 1
         self._last_b = b
         return a.logits
+
+    def _forward_last_cls(self, a, i, b):
+        """Out-projection + residual, LayerNorm 2 and MLP + residual of the last layer on the b cls
+        rows (row stride N*D in the token-major buffers); compact copies for the backward."""
+        cfg = self.cfg
+        D, M, N = cfg.emb_dim, cfg.mlp_dim, cfg.tokens
+        f, mv = self.flat, self.mirror
+        ln = lambda s: self.off(self.lname(i, s))
+        S = N * D
+        ops.gemm(a.o[i], self.woutt[i], a.hm[i], b, D, D, a_layout=K_CONTIG, b_layout=K_CONTIG, lda=S, ldb=D,
+                 ldc=S, epilogue=EPI_BIAS_RESID_F32, bias=f[ln("attn.out.bias"):], aux=a.h[i], ldaux=S)
+        a.c_o[:b].copy_(a.o[i][:b * N].view(b, N, D)[:, 0])   # out-proj weight-gradient operand
+        ops.layernorm_fwd(a.hm[i], S, f[ln("norm2.weight"):], f[ln("norm2.bias"):], a.c_ln2, D, a.c_mu2, a.c_rs2,
+                          b, D)
+        ops.gemm(a.c_ln2, mv[ln("mlp.fc1.weight"):], a.c_gp, b, M, D, a_layout=K_CONTIG, b_layout=K_CONTIG, lda=D,
+                 ldb=D, ldc=M, epilogue=EPI_BIAS_GELU_DGELU, bias=f[ln("mlp.fc1.bias"):], C2=a.c_g, ldc2=M)
+        ops.gemm(a.c_g, mv[ln("mlp.fc2.weight"):], a.h[i + 1], b, D, M, a_layout=K_CONTIG, b_layout=K_CONTIG,
+                 lda=M, ldb=M, ldc=S, epilogue=EPI_BIAS_RESID_F32, bias=f[ln("mlp.fc2.bias"):], aux=a.hm[i], ldaux=S)
+
+    def _backward_last_cls(self, a, i, b, g, on_side):
+        """Backward of _forward_last_cls: the gradient reaching the last layer's output is non-zero on
+        the cls rows only (a.c_dh, from the final LayerNorm backward), so fc2 / fc1 (data and weight
+        gradients), LayerNorm 2 and the out-projection run on those b rows (weight-gradient K = the
+        compact rows, zero-padded to 64). Leaves dO (attention-output gradient) zero except on the
+        cls rows, and dh = the gradient after the attention residual."""
+        cfg = self.cfg
+        D, M, N = cfg.emb_dim, cfg.mlp_dim, cfg.tokens
+        S = N * D
+        f, mv = self.flat, self.mirror
+        gv = lambda name: g[self.off(self.lname(i, name)):]
+        bp = a.bp
+        on_side(lambda: self._wgrad(a.c_dh, D, a.c_g, M, D, M, bp, gv("mlp.fc2.weight"), M))
+        kw = dict(a_layout=K_CONTIG, b_layout=K_CONTIG, lda=D, ldb=D, ldc=M, epilogue=EPI_MUL_BF16, aux=a.c_gp,
+                  ldaux=M, col_partial=a.gelu_part)
+        ops.gemm(a.c_dh, self.w2t[i], a.c_dg, b, M, D, **kw)
+        tiles_m = -(-b // ops.gemm_tile_rows(a.c_dh, self.w2t[i], a.c_dg, b, M, D, **kw))
+        ops.colsum(a.gelu_part, tiles_m, M, M, a.colpart, gv("mlp.fc1.bias"))
+        on_side(lambda: self._wgrad(a.c_dg, M, a.c_ln2, D, M, D, bp, gv("mlp.fc1.weight"), D))
+        ops.gemm(a.c_dg, self.w1t[i], a.c_dyln, b, D, M, a_layout=K_CONTIG, b_layout=K_CONTIG, lda=M, ldb=M, ldc=D,
+                 epilogue=EPI_BF16)
+        ops.layernorm_bwd(a.c_dyln, D, a.hm[i], S, a.c_mu2, a.c_rs2, f[self.off(self.lname(i, "norm2.weight")):],
+                          a.dh, S, a.lnpart, b, D, dres=a.dh, lddres=S, dx_bf16=a.c_dh2, lddxb=D,
+                          dgamma_dbeta=gv("norm2.weight"), dx_colsum=gv("attn.out.bias"))
+        on_side(lambda: self._wgrad(a.c_o, D, a.c_dh2, D, D, D, bp, gv("attn.out.weight"), D))
+        a.dO.zero_()
+        ops.gemm(a.c_dh2, mv[self.off(self.lname(i, "attn.out.weight")):], a.dO, b, D, D, a_layout=K_CONTIG,
+                 b_layout=K_CONTIG, lda=D, ldb=D, ldc=S, epilogue=EPI_BF16)
 
     # ---- fp32 ("exact") forward -------------------------------------------------------------------
     def forward_exact(self, x: torch.Tensor):
@@ -506,10 +571,12 @@ class ViTEngine:
         # final LN backward on cls rows -> residual grad (zero elsewhere)
         # (its dx column sum is the last layer's fc2 bias gradient: only the cls rows are non-zero)
         wb = 0  # index of the dhb buffer holding the current residual-gradient copy
+        pruned = self._pruned
         a.dh.zero_()
-        a.dhb[wb].zero_()
+        if not pruned:
+            a.dhb[wb].zero_()
         ops.layernorm_bwd(a.dlncls, D, a.h[L], N * D, a.muf, a.rsf, f[self.off("transformer.norm.weight"):], a.dh,
-                          N * D, a.lnpart, b, D, dx_bf16=a.dhb[wb], lddxb=N * D,
+                          N * D, a.lnpart, b, D, dx_bf16=a.c_dh if pruned else a.dhb[wb], lddxb=D if pruned else N * D,
                           dgamma_dbeta=gv("transformer.norm.weight"),
                           dx_colsum=gv(self.lname(L - 1, "mlp.fc2.bias")), dx_dropout=dd(3 + 3 * (L - 1), N))
         fire(self.layout.buckets[0])
@@ -517,34 +584,39 @@ class ViTEngine:
         for i in reversed(range(L)):
             ln = lambda s: self.off(self.lname(i, s))
             li = i & 1
-            dhb = a.dhb[wb]
-            # ---- MLP: h_{i+1} = hm + fc2(gelu(fc1(ln2(hm)))) ----
-            # (fc2 bias grad = column sums of dh, already produced by the LayerNorm backward above)
-            on_side(lambda: self._wgrad(dhb, D, a.g[i], M, D, M, a.Tp, gv(self.lname(i, "mlp.fc2.weight")), M))
-            release("dhb", wb)
-            dg = a.dg[li]
-            acquire("dg", li)
-            kw = dict(a_layout=K_CONTIG, b_layout=K_CONTIG, lda=D, ldb=D, ldc=M, epilogue=EPI_MUL_BF16, aux=a.gp[i],
-                      ldaux=M, col_partial=a.gelu_part)
-            ops.gemm(dhb, self.w2t[i], dg, T, M, D, **kw)
-            tiles_m = -(-T // ops.gemm_tile_rows(dhb, self.w2t[i], dg, T, M, D, **kw))
-            ops.colsum(a.gelu_part, tiles_m, M, M, a.colpart, gv(self.lname(i, "mlp.fc1.bias")))
-            on_side(lambda: self._wgrad(dg, M, a.ln2[i], D, M, D, a.Tp, gv(self.lname(i, "mlp.fc1.weight")), D))
-            release("dg", li)
-            ops.gemm(dg, self.w1t[i], a.dyln, T, D, M, a_layout=K_CONTIG, b_layout=K_CONTIG, lda=M,
-                     ldb=M, ldc=D, epilogue=EPI_BF16)
-            wb ^= 1
-            acquire("dhb", wb)
-            dhb = a.dhb[wb]
-            ops.layernorm_bwd(a.dyln, D, a.hm[i], D, a.mu2[i], a.rs2[i], f[ln("norm2.weight"):], a.dh, D, a.lnpart, T,
-                              D, dres=a.dh, lddres=D, dx_bf16=dhb, lddxb=D,
-                              dgamma_dbeta=gv(self.lname(i, "norm2.weight")),
-                              dx_colsum=gv(self.lname(i, "attn.out.bias")), dx_dropout=dd(1 + 3 * i))
-            # ---- attention: hm = h + out(attn(ln1(h))) ----
-            on_side(lambda: self._wgrad(a.o[i], D, dhb, D, D, D, a.Tp, gv(self.lname(i, "attn.out.weight")), D))
-            release("dhb", wb)
-            ops.gemm(dhb, mv[ln("attn.out.weight"):], a.dO, T, D, D, a_layout=K_CONTIG, b_layout=K_CONTIG, lda=D,
-                     ldb=D, ldc=D, epilogue=EPI_BF16)
+            if pruned and i == L - 1:
+                # MLP, LayerNorm 2 and out-projection backward on the cls rows; dO = 0 elsewhere
+                self._backward_last_cls(a, i, b, g, on_side)
+                wb ^= 1
+            else:
+                dhb = a.dhb[wb]
+                # ---- MLP: h_{i+1} = hm + fc2(gelu(fc1(ln2(hm)))) ----
+                # (fc2 bias grad = column sums of dh, already produced by the LayerNorm backward above)
+                on_side(lambda: self._wgrad(dhb, D, a.g[i], M, D, M, a.Tp, gv(self.lname(i, "mlp.fc2.weight")), M))
+                release("dhb", wb)
+                dg = a.dg[li]
+                acquire("dg", li)
+                kw = dict(a_layout=K_CONTIG, b_layout=K_CONTIG, lda=D, ldb=D, ldc=M, epilogue=EPI_MUL_BF16, aux=a.gp[i],
+                          ldaux=M, col_partial=a.gelu_part)
+                ops.gemm(dhb, self.w2t[i], dg, T, M, D, **kw)
+                tiles_m = -(-T // ops.gemm_tile_rows(dhb, self.w2t[i], dg, T, M, D, **kw))
+                ops.colsum(a.gelu_part, tiles_m, M, M, a.colpart, gv(self.lname(i, "mlp.fc1.bias")))
+                on_side(lambda: self._wgrad(dg, M, a.ln2[i], D, M, D, a.Tp, gv(self.lname(i, "mlp.fc1.weight")), D))
+                release("dg", li)
+                ops.gemm(dg, self.w1t[i], a.dyln, T, D, M, a_layout=K_CONTIG, b_layout=K_CONTIG, lda=M,
+                         ldb=M, ldc=D, epilogue=EPI_BF16)
+                wb ^= 1
+                acquire("dhb", wb)
+                dhb = a.dhb[wb]
+                ops.layernorm_bwd(a.dyln, D, a.hm[i], D, a.mu2[i], a.rs2[i], f[ln("norm2.weight"):], a.dh, D, a.lnpart, T,
+                                  D, dres=a.dh, lddres=D, dx_bf16=dhb, lddxb=D,
+                                  dgamma_dbeta=gv(self.lname(i, "norm2.weight")),
+                                  dx_colsum=gv(self.lname(i, "attn.out.bias")), dx_dropout=dd(1 + 3 * i))
+                # ---- attention: hm = h + out(attn(ln1(h))) ----
+                on_side(lambda: self._wgrad(a.o[i], D, dhb, D, D, D, a.Tp, gv(self.lname(i, "attn.out.weight")), D))
+                release("dhb", wb)
+                ops.gemm(dhb, mv[ln("attn.out.weight"):], a.dO, T, D, D, a_layout=K_CONTIG, b_layout=K_CONTIG, lda=D,
+                         ldb=D, ldc=D, epilogue=EPI_BF16)
             dqkv = a.dqkv[li]
             acquire("dqkv", li)
             ops.attention_bwd(a.qkv[i], a.o[i], a.dO, a.lse[i], dqkv, b, N, H, hd, scale, bias_partial=a.qkv_bpart)
