@@ -169,6 +169,15 @@ int vit_attention_fwd(const void* qkv, void* o, float* lse, int64_t B, int64_t N
 int vit_attention_bwd(const void* qkv, const void* o, const void* dout, const float* lse, void* dqkv,
                       float* bias_partial, int64_t B, int64_t N, int64_t H, int64_t hd, float scale,
                       vit_stream_t stream);
+/* as vit_attention_fwd / _bwd for queries [0, q_rows) only (1 <= q_rows <= N; rounded up to whole
+ * 32-row pairs): the forward writes o / lse of those rows; the backward assumes dout is zero on every
+ * other row (their dQ is written as 0, dK / dV / bias partials are exact). Used for the last encoder
+ * layer, whose output reaches the classifier through the cls row only (src/model.py:210). */
+int vit_attention_fwd_rows(const void* qkv, void* o, float* lse, int64_t B, int64_t N, int64_t H, int64_t hd,
+                           float scale, int64_t q_rows, vit_stream_t stream);
+int vit_attention_bwd_rows(const void* qkv, const void* o, const void* dout, const float* lse, void* dqkv,
+                           float* bias_partial, int64_t B, int64_t N, int64_t H, int64_t hd, float scale,
+                           int64_t q_rows, vit_stream_t stream);
 
 /* ------------------------------------------------------------------------------------------
  * Patch embedding im2col (Conv2d k=s=P as a GEMM, src/model.py:179,197-200):

@@ -389,3 +389,33 @@ def test_gemm_wave_split_rows(epi, K):
         ops.gemm(Am, Bm, C, M, N, K, a_layout=K_CONTIG, b_layout=K_CONTIG, lda=lda, ldb=ldb, ldc=N, epilogue=epi,
                  bias=bias, aux=C, ldaux=N)
         assert torch.equal(C.double(), ref + bias.double() + R.double())
+
+
+@pytest.mark.parametrize("B,N,H,hd", [(2, 197, 3, 64), (2, 257, 2, 80), (1, 50, 2, 32)])
+def test_attention_query_rows_match_full(B, N, H, hd):
+    """q_rows = 1 (the last layer's cls query): o / lse of the first 32-query pair equal the full
+    run; with dO zero past row 0, dK / dV / bias partials are bit-identical to the full backward and
+    every other dQ row is written as 0 (buffers start as NaN)."""
+    D = H * hd
+    sc = 1.0 / math.sqrt(hd)
+    qkv = (torch.randn(B * N, 3 * D, device=DEV) * 1.5).bfloat16()
+    o_f, o_r = (torch.empty(B * N, D, device=DEV, dtype=torch.bfloat16) for _ in range(2))
+    l_f, l_r = torch.empty(B, H, N, device=DEV), torch.full((B, H, N), float("nan"), device=DEV)
+    ops.attention_fwd(qkv, o_f, l_f, B, N, H, hd, sc)
+    ops.attention_fwd(qkv, o_r, l_r, B, N, H, hd, sc, q_rows=1)
+    rows = min(N, 32)
+    ov_f, ov_r = o_f.view(B, N, D)[:, :rows], o_r.view(B, N, D)[:, :rows]
+    assert torch.equal(ov_f, ov_r) and torch.equal(l_f[:, :, :rows], l_r[:, :, :rows])
+    dout = torch.zeros(B, N, D, device=DEV)
+    dout[:, 0] = torch.randn(B, D, device=DEV)
+    dout = dout.view(B * N, D).bfloat16()
+    outs = []
+    for qr in (None, 1):
+        dqkv = torch.full((B * N, 3 * D), float("nan"), device=DEV, dtype=torch.bfloat16)
+        bpart = torch.full((B, 3 * D), float("nan"), device=DEV)
+        ops.attention_bwd(qkv, o_f, dout, l_f, dqkv, B, N, H, hd, sc, bias_partial=bpart, q_rows=qr)
+        outs.append((dqkv, bpart))
+    (g_f, b_f), (g_r, b_r) = outs
+    assert torch.equal(g_f.view(B * N, 3, D)[:, 1:], g_r.view(B * N, 3, D)[:, 1:])   # dK, dV
+    assert torch.equal(g_f.view(B * N, 3, D)[:, 0], g_r.view(B * N, 3, D)[:, 0])     # dQ (0 past row 0)
+    assert torch.equal(b_f, b_r)

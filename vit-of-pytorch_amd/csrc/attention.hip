@@ -128,7 +128,7 @@ __device__ __forceinline__ v8bf gl_row(const bf16_t* __restrict__ src, long row_
 template <int HD, int NKT, int NW>
 __global__ void __launch_bounds__(NW * 64) attn_fwd_kernel(const bf16_t* __restrict__ qkv, bf16_t* __restrict__ o,
                                                            float* __restrict__ lse, int N, int H, int hd,
-                                                           float scale) {
+                                                           float scale, int nq) {
   constexpr int NP = NKT * 16;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* Ki = smem;
@@ -143,7 +143,10 @@ __global__ void __launch_bounds__(NW * 64) attn_fwd_kernel(const bf16_t* __restr
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int g = lane >> 4, i = lane & 15;
   const float c = scale * LOG2E;
-  const int nqt = (N + 15) / 16;
+  // queries [0, nq) are needed (nq < N: the last layer's cls rows); whole 32-row pairs are kept so
+  // the backward's stage 2 (query pairs) finds lse for every row it touches
+  const int nqa = min(N, (nq + 31) / 32 * 32);
+  const int nqt = (nqa + 15) / 16;
   // Q fragments come straight from HBM; the next strip's are requested before this strip's math
   v8bf qn[HD / 32];
 #pragma unroll
@@ -229,7 +232,7 @@ __global__ void __launch_bounds__(NW * 64, 2) attn_bwd_kernel(const bf16_t* __re
                                                               const bf16_t* __restrict__ dout,
                                                               const float* __restrict__ lse, bf16_t* __restrict__ dqkv,
                                                               float* __restrict__ bias_partial, int N, int H, int hd,
-                                                              float scale, int stages) {
+                                                              float scale, int stages, int nq) {
   constexpr int NP = NKT * 16;
   constexpr int IMG = NP * HD * 2;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -257,6 +260,10 @@ __global__ void __launch_bounds__(NW * 64, 2) attn_bwd_kernel(const bf16_t* __re
   const int g = lane >> 4, i = lane & 15;
   const float c = scale * LOG2E;
   const int npair = (N + 31) / 32;  // pairs of 16-row tiles holding valid rows
+  // queries [0, nq) carry a gradient (nq < N: dO is zero on every other row); the 32-row pairs
+  // holding them are processed, the other rows get dQ = 0 and contribute nothing to dK / dV
+  const int nqa = min(N, (nq + 31) / 32 * 32);
+  const int npair_q = (nqa + 31) / 32;
   float bq[HD / 16][4], bk[HD / 16][4], bv[HD / 16][4];
 #pragma unroll
   for (int dt = 0; dt < HD / 16; ++dt)
@@ -276,6 +283,18 @@ __global__ void __launch_bounds__(NW * 64, 2) attn_bwd_kernel(const bf16_t* __re
       dn[kk] = gl_row<HD>(dob, D, wave * 16, kk, N, hd, lane);
     }
     for (int qt = wave; qt < nqt; qt += NW) {
+      if (qt * 16 >= nqa) {  // no gradient reaches these queries: dQ = 0, delta = 0
+        const int q = qt * 16 + i;
+        if (g == 0) dlt_s[q] = 0.f;
+        if (q < N) {
+#pragma unroll
+          for (int dt = 0; dt < HD / 16; ++dt) {
+            const int d = dt * 16 + 4 * g;
+            if (d < hd) store4(dq_base + (long)q * rs + d, v4f{0.f, 0.f, 0.f, 0.f}, 1.f);
+          }
+        }
+        continue;
+      }
       v8bf qf[HD / 32], df[HD / 32];
 #pragma unroll
       for (int kk = 0; kk < HD / 32; ++kk) {
@@ -345,6 +364,19 @@ __global__ void __launch_bounds__(NW * 64, 2) attn_bwd_kernel(const bf16_t* __re
     }
   } else {
     for (int qp = wave; qp < npair; qp += NW) {
+      if (qp >= npair_q) {  // no gradient reaches these queries: dQ = 0, delta = 0
+        for (int u = 0; u < 2; ++u) {
+          const int q = (2 * qp + u) * 16 + i;
+          if (g == 0) dlt_s[q] = 0.f;
+          if (q < N) {
+            for (int dt = 0; dt < HD / 16; ++dt) {
+              const int d = dt * 16 + 4 * g;
+              if (d < hd) store4(dq_base + (long)q * rs + d, v4f{0.f, 0.f, 0.f, 0.f}, 1.f);
+            }
+          }
+        }
+        continue;
+      }
       v8bf qf[2][HD / 32], df[2][HD / 32];
       float ls[2], dl[2] = {0.f, 0.f};
   #pragma unroll
@@ -493,7 +525,7 @@ __global__ void __launch_bounds__(NW * 64, 2) attn_bwd_kernel(const bf16_t* __re
         dv[t][dt] = v4f{0.f, 0.f, 0.f, 0.f};
         dk[t][dt] = v4f{0.f, 0.f, 0.f, 0.f};
       }
-    for (int qs = 0; qs < npair; ++qs) {
+    for (int qs = 0; qs < npair_q; ++qs) {
       v4f P[2][2], DS[2][2];  // [key tile][query tile]
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
@@ -599,28 +631,28 @@ __global__ void __launch_bounds__(NW * 64, 2) attn_bwd_kernel(const bf16_t* __re
 
 template <int HD, int NKT, int NW>
 hipError_t launch_fwd_nw(const bf16_t* qkv, bf16_t* o, float* lse, int B, int N, int H, int hd, float scale,
-                         hipStream_t s) {
+                         int nq, hipStream_t s) {
   const size_t lds = (size_t)2 * NKT * 16 * HD * 2;
   auto kern = attn_fwd_kernel<HD, NKT, NW>;
   if (lds > 64 * 1024) (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL(kern, dim3(B * H), dim3(NW * 64), lds, s, qkv, o, lse, N, H, hd, scale);
+  hipLaunchKernelGGL(kern, dim3(B * H), dim3(NW * 64), lds, s, qkv, o, lse, N, H, hd, scale, nq);
   return hipGetLastError();
 }
 
 template <int HD, int NKT>
 hipError_t launch_fwd(const bf16_t* qkv, bf16_t* o, float* lse, int B, int N, int H, int hd, float scale,
-                      hipStream_t s) {
+                      int nq, hipStream_t s) {
   static const int nw = [] {
     const char* e = getenv("VIT_ATTN_FWD_NW");
     return e ? atoi(e) : 4;
   }();
-  if (nw == 8) return launch_fwd_nw<HD, NKT, 8>(qkv, o, lse, B, N, H, hd, scale, s);
-  return launch_fwd_nw<HD, NKT, 4>(qkv, o, lse, B, N, H, hd, scale, s);
+  if (nw == 8) return launch_fwd_nw<HD, NKT, 8>(qkv, o, lse, B, N, H, hd, scale, nq, s);
+  return launch_fwd_nw<HD, NKT, 4>(qkv, o, lse, B, N, H, hd, scale, nq, s);
 }
 
 template <int HD, int NKT, int NW>
 hipError_t launch_bwd_nw(const bf16_t* qkv, const bf16_t* dout, const float* lse, bf16_t* dqkv, float* bias_partial,
-                         int B, int N, int H, int hd, float scale, hipStream_t s) {
+                         int B, int N, int H, int hd, float scale, int nq, hipStream_t s) {
   const size_t lds = (size_t)2 * NKT * 16 * HD * 2 + 2 * NKT * 16 * 4 + (size_t)NW * 3 * HD * 4;
   auto kern = attn_bwd_kernel<HD, NKT, NW>;
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -629,30 +661,30 @@ hipError_t launch_bwd_nw(const bf16_t* qkv, const bf16_t* dout, const float* lse
     return e ? atoi(e) : 3;
   }();
   hipLaunchKernelGGL(kern, dim3(B * H), dim3(NW * 64), lds, s, qkv, dout, lse, dqkv, bias_partial, N, H, hd, scale,
-                     stages);
+                     stages, nq);
   return hipGetLastError();
 }
 
 template <int HD, int NKT>
 hipError_t launch_bwd(const bf16_t* qkv, const bf16_t* o, const bf16_t* dout, const float* lse, bf16_t* dqkv,
-                      float* bias_partial, int B, int N, int H, int hd, float scale, hipStream_t s) {
+                      float* bias_partial, int B, int N, int H, int hd, float scale, int nq, hipStream_t s) {
   (void)o;
   static const int nw = [] {
     const char* e = getenv("VIT_ATTN_BWD_NW");
     return e ? atoi(e) : 4;
   }();
-  if (nw == 8) return launch_bwd_nw<HD, NKT, 8>(qkv, dout, lse, dqkv, bias_partial, B, N, H, hd, scale, s);
-  return launch_bwd_nw<HD, NKT, 4>(qkv, dout, lse, dqkv, bias_partial, B, N, H, hd, scale, s);
+  if (nw == 8) return launch_bwd_nw<HD, NKT, 8>(qkv, dout, lse, dqkv, bias_partial, B, N, H, hd, scale, nq, s);
+  return launch_bwd_nw<HD, NKT, 4>(qkv, dout, lse, dqkv, bias_partial, B, N, H, hd, scale, nq, s);
 }
 
 #define VIT_NKT_CASES(X) X(2) X(4) X(6) X(8) X(10) X(12) X(14) X(16) X(18) X(20)
 
 template <int HD>
 hipError_t dispatch_fwd(int nkt, const bf16_t* qkv, bf16_t* o, float* lse, int B, int N, int H, int hd, float scale,
-                        hipStream_t s) {
+                        int nq, hipStream_t s) {
   switch (nkt) {
 #define C(n) \
-  case n: return launch_fwd<HD, n>(qkv, o, lse, B, N, H, hd, scale, s);
+  case n: return launch_fwd<HD, n>(qkv, o, lse, B, N, H, hd, scale, nq, s);
     VIT_NKT_CASES(C)
 #undef C
   }
@@ -660,10 +692,11 @@ hipError_t dispatch_fwd(int nkt, const bf16_t* qkv, bf16_t* o, float* lse, int B
 }
 template <int HD>
 hipError_t dispatch_bwd(int nkt, const bf16_t* qkv, const bf16_t* o, const bf16_t* dout, const float* lse,
-                        bf16_t* dqkv, float* bias_partial, int B, int N, int H, int hd, float scale, hipStream_t s) {
+                        bf16_t* dqkv, float* bias_partial, int B, int N, int H, int hd, float scale, int nq,
+                        hipStream_t s) {
   switch (nkt) {
 #define C(n) \
-  case n: return launch_bwd<HD, n>(qkv, o, dout, lse, dqkv, bias_partial, B, N, H, hd, scale, s);
+  case n: return launch_bwd<HD, n>(qkv, o, dout, lse, dqkv, bias_partial, B, N, H, hd, scale, nq, s);
     VIT_NKT_CASES(C)
 #undef C
   }
@@ -685,45 +718,63 @@ int image_width(int64_t hd) { return hd <= 32 ? 32 : hd <= 64 ? 64 : 96; }
 
 }  // namespace
 
-extern "C" int vit_attention_fwd(const void* qkv, void* o, float* lse, int64_t B, int64_t N, int64_t H, int64_t hd,
-                                 float scale, vit_stream_t stream) {
+extern "C" int vit_attention_fwd_rows(const void* qkv, void* o, float* lse, int64_t B, int64_t N, int64_t H,
+                                      int64_t hd, float scale, int64_t q_rows, vit_stream_t stream) {
   int st = check_shape(B, N, H, hd);
   if (st) return st;
   VIT_CHECK_ARG(qkv && o && lse, "vit_attention_fwd: null pointer");
+  VIT_CHECK_ARG(q_rows >= 1 && q_rows <= N, "vit_attention_fwd: q_rows=%lld outside [1, N]", (long long)q_rows);
   const int nkt = (int)((N + 31) / 32) * 2;
   const bf16_t* q = (const bf16_t*)qkv;
   hipStream_t s = (hipStream_t)stream;
+  const int nq = (int)q_rows;
   hipError_t e;
   switch (image_width(hd)) {
-    case 32: e = dispatch_fwd<32>(nkt, q, (bf16_t*)o, lse, (int)B, (int)N, (int)H, (int)hd, scale, s); break;
-    case 64: e = dispatch_fwd<64>(nkt, q, (bf16_t*)o, lse, (int)B, (int)N, (int)H, (int)hd, scale, s); break;
-    default: e = dispatch_fwd<96>(nkt, q, (bf16_t*)o, lse, (int)B, (int)N, (int)H, (int)hd, scale, s); break;
+    case 32: e = dispatch_fwd<32>(nkt, q, (bf16_t*)o, lse, (int)B, (int)N, (int)H, (int)hd, scale, nq, s); break;
+    case 64: e = dispatch_fwd<64>(nkt, q, (bf16_t*)o, lse, (int)B, (int)N, (int)H, (int)hd, scale, nq, s); break;
+    default: e = dispatch_fwd<96>(nkt, q, (bf16_t*)o, lse, (int)B, (int)N, (int)H, (int)hd, scale, nq, s); break;
   }
   return vit::check_hip(e, "vit_attention_fwd launch");
+}
+
+extern "C" int vit_attention_fwd(const void* qkv, void* o, float* lse, int64_t B, int64_t N, int64_t H, int64_t hd,
+                                 float scale, vit_stream_t stream) {
+  return vit_attention_fwd_rows(qkv, o, lse, B, N, H, hd, scale, N, stream);
+}
+
+extern "C" int vit_attention_bwd_rows(const void* qkv, const void* o, const void* dout, const float* lse, void* dqkv,
+                                      float* bias_partial, int64_t B, int64_t N, int64_t H, int64_t hd, float scale,
+                                      int64_t q_rows, vit_stream_t stream) {
+  int st = check_shape(B, N, H, hd);
+  if (st) return st;
+  VIT_CHECK_ARG(qkv && o && dout && lse && dqkv, "vit_attention_bwd: null pointer");
+  VIT_CHECK_ARG(q_rows >= 1 && q_rows <= N, "vit_attention_bwd: q_rows=%lld outside [1, N]", (long long)q_rows);
+  const int nkt = (int)((N + 31) / 32) * 2;
+  const bf16_t *q = (const bf16_t*)qkv, *ob = (const bf16_t*)o, *d = (const bf16_t*)dout;
+  hipStream_t s = (hipStream_t)stream;
+  const int nq = (int)q_rows;
+  hipError_t e;
+  switch (image_width(hd)) {
+    case 32:
+      e = dispatch_bwd<32>(nkt, q, ob, d, lse, (bf16_t*)dqkv, bias_partial, (int)B, (int)N, (int)H, (int)hd, scale, nq,
+                           s);
+      break;
+    case 64:
+      e = dispatch_bwd<64>(nkt, q, ob, d, lse, (bf16_t*)dqkv, bias_partial, (int)B, (int)N, (int)H, (int)hd, scale, nq,
+                           s);
+      break;
+    default:
+      e = dispatch_bwd<96>(nkt, q, ob, d, lse, (bf16_t*)dqkv, bias_partial, (int)B, (int)N, (int)H, (int)hd, scale, nq,
+                           s);
+      break;
+  }
+  return vit::check_hip(e, "vit_attention_bwd launch");
 }
 
 extern "C" int vit_attention_bwd(const void* qkv, const void* o, const void* dout, const float* lse, void* dqkv,
                                  float* bias_partial, int64_t B, int64_t N, int64_t H, int64_t hd, float scale,
                                  vit_stream_t stream) {
-  int st = check_shape(B, N, H, hd);
-  if (st) return st;
-  VIT_CHECK_ARG(qkv && o && dout && lse && dqkv, "vit_attention_bwd: null pointer");
-  const int nkt = (int)((N + 31) / 32) * 2;
-  const bf16_t *q = (const bf16_t*)qkv, *ob = (const bf16_t*)o, *d = (const bf16_t*)dout;
-  hipStream_t s = (hipStream_t)stream;
-  hipError_t e;
-  switch (image_width(hd)) {
-    case 32:
-      e = dispatch_bwd<32>(nkt, q, ob, d, lse, (bf16_t*)dqkv, bias_partial, (int)B, (int)N, (int)H, (int)hd, scale, s);
-      break;
-    case 64:
-      e = dispatch_bwd<64>(nkt, q, ob, d, lse, (bf16_t*)dqkv, bias_partial, (int)B, (int)N, (int)H, (int)hd, scale, s);
-      break;
-    default:
-      e = dispatch_bwd<96>(nkt, q, ob, d, lse, (bf16_t*)dqkv, bias_partial, (int)B, (int)N, (int)H, (int)hd, scale, s);
-      break;
-  }
-  return vit::check_hip(e, "vit_attention_bwd launch");
+  return vit_attention_bwd_rows(qkv, o, dout, lse, dqkv, bias_partial, B, N, H, hd, scale, N, stream);
 }
 
 // ---- fp32 (exact) attention forward -------------------------------------------------------------

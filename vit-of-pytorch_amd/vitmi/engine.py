@@ -223,8 +223,8 @@ class ViTEngine:
         self.overlap_wgrad = os.environ.get("VITMI_OVERLAP", "0") == "1"
         # Only the cls token of the last layer's output reaches the classifier (src/model.py:210),
         # so that layer's out-projection, LayerNorm 2 and MLP (forward and backward) run on the b cls
-        # rows; attention and the q|k|v projection stay full (every token is a key / value of the
-        # cls query). Same logits, loss and gradients (zero rows add exact zeros); VITMI_PRUNE_LAST=0
+        # rows and its attention on the first 32-query pair of each (image, head) (q_rows = 1); the
+        # q|k|v projection stays full (every token is a key / value of the cls query). Same logits, loss and gradients (zero rows add exact zeros); VITMI_PRUNE_LAST=0
         # runs every token. Off while dropout is active.
         self.prune_last = os.environ.get("VITMI_PRUNE_LAST", "1") != "0"
         self._pruned = False
@@ -369,8 +369,9 @@ class ViTEngine:
                               a.rs1[i], T, D)
             ops.gemm(a.ln1[i], self.wqkvt[i], a.qkv[i], T, 3 * D, D, a_layout=K_CONTIG, b_layout=K_CONTIG, lda=D,
                      ldb=D, ldc=3 * D, epilogue=EPI_BIAS_BF16, bias=self.bqkv[i])
-            ops.attention_fwd(a.qkv[i], a.o[i], a.lse[i], b, N, H, hd, scale)
-            if self._pruned and i == L - 1:
+            last = self._pruned and i == L - 1
+            ops.attention_fwd(a.qkv[i], a.o[i], a.lse[i], b, N, H, hd, scale, q_rows=1 if last else None)
+            if last:
                 self._forward_last_cls(a, i, b)
                 break
             ops.gemm(a.o[i], self.woutt[i], a.hm[i], T, D, D, a_layout=K_CONTIG, b_layout=K_CONTIG,
@@ -619,7 +620,8 @@ class ViTEngine:
                          ldb=D, ldc=D, epilogue=EPI_BF16)
             dqkv = a.dqkv[li]
             acquire("dqkv", li)
-            ops.attention_bwd(a.qkv[i], a.o[i], a.dO, a.lse[i], dqkv, b, N, H, hd, scale, bias_partial=a.qkv_bpart)
+            ops.attention_bwd(a.qkv[i], a.o[i], a.dO, a.lse[i], dqkv, b, N, H, hd, scale, bias_partial=a.qkv_bpart,
+                              q_rows=1 if pruned and i == L - 1 else None)
             qo = ln("attn.query.weight")
             zs = ln("attn.key.weight") - qo
             qb = ln("attn.query.bias")

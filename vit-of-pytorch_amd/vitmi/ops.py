@@ -112,16 +112,19 @@ def layernorm_bwd(dy, lddy, x, ldx, mean, rstd, gamma, dx, lddx, partial, rows, 
           "vit_layernorm_bwd")
 
 
-def attention_fwd(qkv, o, lse, B, N, H, hd, scale):
+def attention_fwd(qkv, o, lse, B, N, H, hd, scale, q_rows=None):
+    """q_rows: only queries [0, q_rows) are needed (None: all N)."""
     _chk(qkv, BF16, "qkv")
     _chk(o, BF16, "o")
     _chk(lse, F32, "lse")
-    check(lib().vit_attention_fwd(_p(qkv), _p(o), _p(lse), B, N, H, hd, scale, _stream()), "vit_attention_fwd")
+    check(lib().vit_attention_fwd_rows(_p(qkv), _p(o), _p(lse), B, N, H, hd, scale, N if q_rows is None else q_rows,
+                                       _stream()), "vit_attention_fwd")
 
 
-def attention_bwd(qkv, o, dout, lse, dqkv, B, N, H, hd, scale, bias_partial=None):
-    check(lib().vit_attention_bwd(_p(qkv), _p(o), _p(dout), _p(lse), _p(dqkv), _p(bias_partial), B, N, H, hd, scale,
-                                  _stream()), "vit_attention_bwd")
+def attention_bwd(qkv, o, dout, lse, dqkv, B, N, H, hd, scale, bias_partial=None, q_rows=None):
+    """q_rows: dout is zero outside queries [0, q_rows) (None: all N)."""
+    check(lib().vit_attention_bwd_rows(_p(qkv), _p(o), _p(dout), _p(lse), _p(dqkv), _p(bias_partial), B, N, H, hd,
+                                       scale, N if q_rows is None else q_rows, _stream()), "vit_attention_bwd")
 
 
 def im2col(x, out, B, img, P, Kpad):
