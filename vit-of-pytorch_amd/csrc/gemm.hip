@@ -1062,7 +1062,11 @@ extern "C" int vit_gemm_bf16(const vit_gemm_args* a, vit_stream_t stream) {
         if (d.aux) g2.aux = (const char*)d.aux + r0 * a->ldaux * (a->epilogue == VIT_EPI_BIAS_RESID_F32 ? 4 : 2);
         g2.drop.row0 = (int)r0;  // dropout masks are indexed by the absolute row
         hipError_t e = run(cfg, g1);
-        if (e == hipSuccess) e = run(0, g2);
+        static const int rem_cfg = [] {
+          const char* e = getenv("VIT_GEMM_REM_CFG");
+          return e ? atoi(e) : 0;
+        }();
+        if (e == hipSuccess) e = run(rem_cfg >= 0 && rem_cfg <= 4 ? rem_cfg : 0, g2);
         return vit::check_hip(e, "vit_gemm_bf16 launch");
       }
     }
