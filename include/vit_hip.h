@@ -162,7 +162,10 @@ int vit_layernorm_bwd(const void* dy, int64_t lddy, int32_t dy_f32, const float*
  * bwd: dqkv (bf16 [B*N, 3, H, hd]) from dO, recomputing P from lse; when bias_partial != NULL
  *      it also receives per-image column sums of dq | dk | dv (f32 [B][3*H*hd], the q/k/v bias
  *      gradient partials; reduce over B with vit_colsum).
- * Limits: N <= 320, hd in {32, 64}.
+ * Two implementations (`path`): 1 = LDS-resident (all keys of a head on chip, exact softmax;
+ * N <= 320: 197 tokens for B/16 and L/16 @224, 257 for H/14 @224), 2 = K/V-tiled (64-key blocks
+ * streamed through LDS, online softmax; any N: 577 tokens @384 for B/16 and L/16, 730 for H/14,
+ * src/config.py:12,37), 0 = pick by N. hd: multiple of 16, <= 96 (hd 80 runs on 96-wide images).
  * ---------------------------------------------------------------------------------------- */
 int vit_attention_fwd(const void* qkv, void* o, float* lse, int64_t B, int64_t N, int64_t H,
                       int64_t hd, float scale, vit_stream_t stream);
@@ -178,6 +181,18 @@ int vit_attention_fwd_rows(const void* qkv, void* o, float* lse, int64_t B, int6
 int vit_attention_bwd_rows(const void* qkv, const void* o, const void* dout, const float* lse, void* dqkv,
                            float* bias_partial, int64_t B, int64_t N, int64_t H, int64_t hd, float scale,
                            int64_t q_rows, vit_stream_t stream);
+/* Path-explicit forms. bias_partial of the backward holds vit_attention_bias_rows(N, path) rows per
+ * image ([B * rows][3*H*hd], reduce all B * rows rows with vit_colsum): 1 on path 1, ceil(N / 64) on
+ * path 2 (one per 64-row block). The tiled backward needs `workspace`, >= vit_attention_workspace_elems
+ * floats (the exact per-query delta = sum_j P dP handed from its dQ kernel to its dK/dV kernel);
+ * path 1 needs none (NULL). q_rows as for the *_rows forms (path 2 rounds it up to 64-row blocks). */
+int64_t vit_attention_bias_rows(int64_t N, int32_t path);
+int64_t vit_attention_workspace_elems(int64_t B, int64_t N, int64_t H, int32_t path);
+int vit_attention_fwd_ex(const void* qkv, void* o, float* lse, int64_t B, int64_t N, int64_t H, int64_t hd,
+                         float scale, int64_t q_rows, int32_t path, vit_stream_t stream);
+int vit_attention_bwd_ex(const void* qkv, const void* o, const void* dout, const float* lse, void* dqkv,
+                         float* bias_partial, int64_t B, int64_t N, int64_t H, int64_t hd, float scale,
+                         int64_t q_rows, int32_t path, float* workspace, vit_stream_t stream);
 
 /* ------------------------------------------------------------------------------------------
  * Patch embedding im2col (Conv2d k=s=P as a GEMM, src/model.py:179,197-200):
@@ -227,7 +242,8 @@ int vit_gemm_f32(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda, i
 
 /* Cross entropy (mean over the global batch), CrossEntropyLoss src/train.py:151,22, plus
  * accuracy counts (src/utils.py:28-41). dlogits = (softmax - onehot) * grad_scale.
- * row_stats[b] = {loss_b, top1_hit, top5_hit}. */
+ * row_stats[b] = {loss_b, top1_hit, top5_hit}. A label outside [0, C) is not read through: that row's
+ * loss and dlogits are NaN. */
 int vit_cross_entropy(const float* logits, const int64_t* labels, int64_t B, int64_t C,
                       float* dlogits, float grad_scale, float* row_stats, vit_stream_t stream);
 

@@ -208,22 +208,32 @@ def _attn_ref(qkv, B, N, H, hd):
     return o, lse
 
 
-@pytest.mark.parametrize("B,N,H,hd", [(2, 197, 12, 64), (3, 17, 2, 32), (2, 50, 4, 64), (1, 5, 3, 64), (2, 257, 2, 64),
-                                      (2, 257, 3, 80), (1, 197, 2, 48), (2, 33, 2, 96)])
-def test_attention(B, N, H, hd):
+ATTN_CASES = [(2, 197, 12, 64, 0), (3, 17, 2, 32, 0), (2, 50, 4, 64, 0), (1, 5, 3, 64, 0), (2, 257, 2, 64, 0),
+              (2, 257, 3, 80, 0), (1, 197, 2, 48, 0), (2, 33, 2, 96, 0),
+              # K/V-tiled path (ops.ATTN_TILED): forced at ViT-224 sizes, and the 384-px sequences it exists for
+              # (B/16, L/16 @384: 577 tokens; H/14 @384: 730 tokens, hd 80)
+              (2, 197, 3, 64, 2), (2, 257, 2, 80, 2), (3, 17, 2, 32, 2), (1, 65, 2, 48, 2), (2, 33, 2, 96, 2),
+              (2, 577, 3, 64, 0), (1, 730, 2, 80, 0), (1, 321, 2, 64, 0)]
+
+
+@pytest.mark.parametrize("B,N,H,hd,path", ATTN_CASES)
+def test_attention(B, N, H, hd, path):
     D = H * hd
     qkv = (torch.randn(B * N, 3 * D, device=DEV) * 1.5).bfloat16().requires_grad_(True)
     o = torch.empty(B * N, D, device=DEV, dtype=torch.bfloat16)
     lse = torch.empty(B, H, N, device=DEV)
-    ops.attention_fwd(qkv.detach(), o, lse, B, N, H, hd, 1.0 / math.sqrt(hd))
+    ops.attention_fwd(qkv.detach(), o, lse, B, N, H, hd, 1.0 / math.sqrt(hd), path=path)
     qf = qkv.float().detach().requires_grad_(True)
     oref, lref = _attn_ref(qf, B, N, H, hd)
     assert rel(o.float(), oref.detach()) < 1e-2
     assert rel(lse, lref.detach()) < 1e-4
     dout = torch.randn(B * N, D, device=DEV).bfloat16()
     dqkv = torch.full((B * N, 3 * D), float("nan"), device=DEV, dtype=torch.bfloat16)
-    bpart = torch.full((B, 3 * D), float("nan"), device=DEV)
-    ops.attention_bwd(qkv.detach(), o, dout, lse, dqkv, B, N, H, hd, 1.0 / math.sqrt(hd), bias_partial=bpart)
+    rows = ops.attention_bias_rows(N, path)
+    bpart = torch.full((B * rows, 3 * D), float("nan"), device=DEV)
+    ops.attention_bwd(qkv.detach(), o, dout, lse, dqkv, B, N, H, hd, 1.0 / math.sqrt(hd), bias_partial=bpart,
+                      path=path)
+    bpart = bpart.view(B, rows, 3 * D).sum(1)
     gref, = torch.autograd.grad(oref, qf, dout.float())
     gq, gk, gv = gref.view(B * N, 3, D).unbind(1)
     mq, mk, mv = dqkv.float().view(B * N, 3, D).unbind(1)
@@ -391,8 +401,9 @@ def test_gemm_wave_split_rows(epi, K):
         assert torch.equal(C.double(), ref + bias.double() + R.double())
 
 
-@pytest.mark.parametrize("B,N,H,hd", [(2, 197, 3, 64), (2, 257, 2, 80), (1, 50, 2, 32)])
-def test_attention_query_rows_match_full(B, N, H, hd):
+@pytest.mark.parametrize("B,N,H,hd,path", [(2, 197, 3, 64, 0), (2, 257, 2, 80, 0), (1, 50, 2, 32, 0),
+                                           (2, 197, 3, 64, 2), (1, 577, 2, 80, 0)])
+def test_attention_query_rows_match_full(B, N, H, hd, path):
     """q_rows = 1 (the last layer's cls query): o / lse of the first 32-query pair equal the full
     run; with dO zero past row 0, dK / dV / bias partials are bit-identical to the full backward and
     every other dQ row is written as 0 (buffers start as NaN)."""
@@ -401,9 +412,9 @@ def test_attention_query_rows_match_full(B, N, H, hd):
     qkv = (torch.randn(B * N, 3 * D, device=DEV) * 1.5).bfloat16()
     o_f, o_r = (torch.empty(B * N, D, device=DEV, dtype=torch.bfloat16) for _ in range(2))
     l_f, l_r = torch.empty(B, H, N, device=DEV), torch.full((B, H, N), float("nan"), device=DEV)
-    ops.attention_fwd(qkv, o_f, l_f, B, N, H, hd, sc)
-    ops.attention_fwd(qkv, o_r, l_r, B, N, H, hd, sc, q_rows=1)
-    rows = min(N, 32)
+    ops.attention_fwd(qkv, o_f, l_f, B, N, H, hd, sc, path=path)
+    ops.attention_fwd(qkv, o_r, l_r, B, N, H, hd, sc, q_rows=1, path=path)
+    rows = min(N, 32 if ops.attention_bias_rows(N, path) == 1 else 64)  # whole query pairs / 64-row blocks
     ov_f, ov_r = o_f.view(B, N, D)[:, :rows], o_r.view(B, N, D)[:, :rows]
     assert torch.equal(ov_f, ov_r) and torch.equal(l_f[:, :, :rows], l_r[:, :, :rows])
     dout = torch.zeros(B, N, D, device=DEV)
@@ -412,8 +423,8 @@ def test_attention_query_rows_match_full(B, N, H, hd):
     outs = []
     for qr in (None, 1):
         dqkv = torch.full((B * N, 3 * D), float("nan"), device=DEV, dtype=torch.bfloat16)
-        bpart = torch.full((B, 3 * D), float("nan"), device=DEV)
-        ops.attention_bwd(qkv, o_f, dout, l_f, dqkv, B, N, H, hd, sc, bias_partial=bpart, q_rows=qr)
+        bpart = torch.full((B * ops.attention_bias_rows(N, path), 3 * D), float("nan"), device=DEV)
+        ops.attention_bwd(qkv, o_f, dout, l_f, dqkv, B, N, H, hd, sc, bias_partial=bpart, q_rows=qr, path=path)
         outs.append((dqkv, bpart))
     (g_f, b_f), (g_r, b_r) = outs
     assert torch.equal(g_f.view(B * N, 3, D)[:, 1:], g_r.view(B * N, 3, D)[:, 1:])   # dK, dV

@@ -282,3 +282,50 @@ def test_last_layer_cls_pruning_matches_full_tokens():
     for k in g0:
         d = float((g1[k].double() - g0[k].double()).norm())
         assert d <= max(2e-3 * float(g0[k].double().norm()), 1e-5 * tot), (k, d)
+
+
+# ---- sequences longer than the LDS-resident attention (K/V-tiled kernels) ----------------------------
+LONG = ViTConfig(image_size=72, patch_size=4, emb_dim=128, mlp_dim=256, num_heads=2, num_layers=2, num_classes=10)
+
+
+def test_step_long_sequence_matches_oracle():
+    """325 tokens (> 320): the engine runs the K/V-tiled attention forward and backward."""
+    cfg, bs = LONG, 3
+    assert cfg.num_tokens == 325
+    params = tame_params(init_params(cfg, seed=42))
+    g = torch.Generator().manual_seed(21)
+    x = torch.randn(bs, 3, cfg.image_size, cfg.image_size, generator=g)
+    y = torch.randint(0, cfg.num_classes, (bs,), generator=g)
+    ref_logits, ref_loss, ref_grads = loss_and_grads(params, x, y, cfg)
+    m = make_model(cfg, params)
+    from vitmi.model import CrossEntropyLoss
+    logits = m(x.cuda())
+    loss = CrossEntropyLoss()(logits, y.cuda())
+    loss.backward()
+    assert rel(logits, ref_logits) < 1e-2
+    assert abs(float(loss.detach()) - float(ref_loss)) <= 1e-3 * abs(float(ref_loss))
+    check_grads(m, ref_grads)
+
+
+def test_b16_384_matches_oracle():
+    """ViT-B/16 @384 (577 tokens; the reference's --image-size 384, src/config.py:37, and its eval
+    default, src/config.py:12), tamed init, bs 1: bf16 step vs the oracle (G2/G3) and the fp32 forward
+    within 1e-3 (G1)."""
+    cfg = ViTConfig(image_size=384)
+    params = tame_params(init_params(cfg, seed=42))
+    g = torch.Generator().manual_seed(13)
+    x = torch.randn(1, 3, 384, 384, generator=g)
+    y = torch.randint(0, 1000, (1,), generator=g)
+    ref_logits, ref_loss, ref_grads = loss_and_grads(params, x, y, cfg)
+    m = make_model(cfg, params)
+    from vitmi.model import CrossEntropyLoss
+    logits = m(x.cuda())
+    loss = CrossEntropyLoss()(logits, y.cuda())
+    loss.backward()
+    assert rel(logits, ref_logits) < 1e-2
+    assert abs(float(loss.detach()) - float(ref_loss)) <= 1e-3 * abs(float(ref_loss))
+    check_grads(m, ref_grads)
+    m.precision = "fp32"
+    with torch.no_grad():
+        exact = m(x.cuda())
+    assert rel(exact, ref_logits) < 1e-3, rel(exact, ref_logits)

@@ -46,9 +46,12 @@ def test_device_image_loader_batches_match_oracle_transform():
     assert np.array_equal(x, transform_batch(imgs, 48))
 
 
-def test_data_parallel_two_ranks_replicas_identical(tmp_path):
+@pytest.mark.parametrize("set_to_none", [True, False])
+def test_data_parallel_two_ranks_replicas_identical(tmp_path, set_to_none):
     """2 ranks on one GPU over gloo (RCCL needs distinct GPUs): per-layer all-reduce overlapped with
-    the backward; both replicas must end bit-identical and equal to one big-batch step."""
+    the backward; both replicas must end bit-identical and equal to one big-batch step. With
+    zero_grad(set_to_none=False) the second step accumulates into existing .grad tensors, so the
+    reduced buckets must be complete before autograd adds them."""
     script = tmp_path / "dp.py"
     script.write_text(r'''
 import os, sys, torch, torch.distributed as dist
@@ -68,7 +71,7 @@ g = torch.Generator().manual_seed(3)
 X = torch.randn(8, 3, 32, 32, generator=g); Y = torch.randint(0, 10, (8,), generator=g)
 x, y = X[rank * 4:(rank + 1) * 4].cuda(), Y[rank * 4:(rank + 1) * 4].cuda()
 for _ in range(2):
-    opt.zero_grad()
+    opt.zero_grad(set_to_none=os.environ["SET_TO_NONE"] == "1")
     CrossEntropyLoss()(m(x), y).backward()
     red.finish()
     opt.step()
@@ -96,9 +99,11 @@ dist.barrier()
 dist.destroy_process_group()
 open(os.path.join(os.environ["OUTDIR"], f"rank{rank}.ok"), "w").write("ok")
 ''')
-    env = dict(os.environ, REPO=REPO, OUTDIR=str(tmp_path), MASTER_ADDR="127.0.0.1", MASTER_PORT="29533")
+    port = "29533" if set_to_none else "29534"
+    env = dict(os.environ, REPO=REPO, OUTDIR=str(tmp_path), MASTER_ADDR="127.0.0.1", MASTER_PORT=port,
+               SET_TO_NONE="1" if set_to_none else "0")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
-           "--master-addr", "127.0.0.1", "--master-port", "29533", str(script)]
+           "--master-addr", "127.0.0.1", "--master-port", port, str(script)]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     # (the ranks' stdout interleaves: each rank leaves a marker file instead)

@@ -15,114 +15,11 @@
 //        dK = dS^T Q in registers. No atomics, deterministic (details above attn_bwd_kernel).
 // LDS images: [rows][HD] bf16 with a 16-B-chunk XOR swizzle that is conflict-free for both the
 // row read (ds_read_b128) and the transposed read (ds_read_b64_tr_b16) at HD = 64.
-#include "common.h"
+#include "attn_common.h"
 #include <stdlib.h>
 
 namespace {
-
-constexpr float LOG2E = 1.4426950408889634f;
-typedef unsigned v4u __attribute__((ext_vector_type(4)));
-
-template <int HD>
-__device__ __forceinline__ int aswz(int row) {
-  if constexpr (HD == 64) return ((row >> 1) & 3) << 1;
-  return 0;
-}
-
-template <int HD>
-__device__ __forceinline__ int img_off(int row, int chunk) {
-  return row * HD * 2 + ((chunk ^ aswz<HD>(row)) << 4);
-}
-
-// Load rows [0, NP) x [0, HD) of two strided bf16 matrices into swizzled LDS images (zero padded).
-// Every load of the thread is issued before the first LDS write (one HBM latency per image pair
-// instead of one per 16-B chunk): buffer loads against a descriptor that covers the valid rows, so
-// padding rows / columns >= hd read as zero without a branch around the load.
-template <int HD, int NP, int NT>
-__device__ __forceinline__ void load_images(char* imgA, const bf16_t* srcA, long strideA, char* imgB,
-                                            const bf16_t* srcB, long strideB, int N, int hd) {
-  constexpr int CPR = HD / 8;
-  constexpr int TOTAL = NP * CPR;
-  constexpr int PER = (TOTAL + NT - 1) / NT;
-  const __amdgpu_buffer_rsrc_t ra = make_rsrc(srcA, (uint32_t)(((long)(N - 1) * strideA + hd) * 2));
-  const __amdgpu_buffer_rsrc_t rb = make_rsrc(srcB, (uint32_t)(((long)(N - 1) * strideB + hd) * 2));
-  v4u a[PER], b[PER];
-#pragma unroll
-  for (int k = 0; k < PER; ++k) {
-    const int c = threadIdx.x + k * NT;
-    const int row = c / CPR, ch = c % CPR;
-    const bool ok = c < TOTAL && row < N && ch * 8 < hd;
-    const int offa = ok ? (int)(((long)row * strideA + ch * 8) * 2) : 0x7ffffff0;
-    const int offb = ok ? (int)(((long)row * strideB + ch * 8) * 2) : 0x7ffffff0;
-    a[k] = __builtin_amdgcn_raw_buffer_load_b128(ra, offa, 0, 0);
-    b[k] = __builtin_amdgcn_raw_buffer_load_b128(rb, offb, 0, 0);
-  }
-#pragma unroll
-  for (int k = 0; k < PER; ++k) {
-    const int c = threadIdx.x + k * NT;
-    if (c < TOTAL) {
-      const int row = c / CPR, ch = c % CPR;
-      *reinterpret_cast<v4u*>(imgA + img_off<HD>(row, ch)) = a[k];
-      *reinterpret_cast<v4u*>(imgB + img_off<HD>(row, ch)) = b[k];
-    }
-  }
-}
-
-// 16 rows x 32 k fragment: lane holds row r0 + (lane&15), k = kk*32 + 8*(lane>>4) + j.
-template <int HD>
-__device__ __forceinline__ v8bf rd_row(const char* img, int r0, int kk, int lane) {
-  const int row = r0 + (lane & 15);
-  const int ch = kk * 4 + (lane >> 4);
-  return __builtin_bit_cast(v8bf, *reinterpret_cast<const v8s*>(img + img_off<HD>(row, ch)));
-}
-
-// Transposed fragment: lane (g, i) gets column d0+i of image rows {16ta+4g+0..3, 16tb+4g+0..3}.
-template <int HD>
-__device__ __forceinline__ v8bf rd_tr(const char* img, int ta, int tb, int d0, int lane) {
-  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
-  const int colb = (d0 + 4 * p) * 2;
-  const int ch = colb >> 4, within = colb & 15;
-  const int ra = 16 * ta + 4 * g + q, rb = 16 * tb + 4 * g + q;
-  v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(v4s, img + img_off<HD>(ra, ch) + within));
-  v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(v4s, img + img_off<HD>(rb, ch) + within));
-  v8s r;
-  r.lo = lo;
-  r.hi = hi;
-  return __builtin_bit_cast(v8bf, r);
-}
-
-__device__ __forceinline__ v8bf pack8(const v4f& a, const v4f& b) {
-  v8s r;
-  r[0] = (short)f2bf(a[0]); r[1] = (short)f2bf(a[1]); r[2] = (short)f2bf(a[2]); r[3] = (short)f2bf(a[3]);
-  r[4] = (short)f2bf(b[0]); r[5] = (short)f2bf(b[1]); r[6] = (short)f2bf(b[2]); r[7] = (short)f2bf(b[3]);
-  return __builtin_bit_cast(v8bf, r);
-}
-
-// 2^x on the transcendental unit (bare v_exp_f32). Arguments are s*log2e - lse <= ~0, so results
-// only underflow (to 0) for keys whose softmax weight is below f32 resolution anyway.
-__device__ __forceinline__ float ex2(float x) { return __builtin_amdgcn_exp2f(x); }
-
-__device__ __forceinline__ v4f mfma(const v8bf& a, const v8bf& b, const v4f& c) {
-  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
-}
-
-__device__ __forceinline__ void store4(bf16_t* dst, const v4f& v, float s) {
-  uint2 u;
-  u.x = pack2bf(v[0] * s, v[1] * s);
-  u.y = pack2bf(v[2] * s, v[3] * s);
-  *reinterpret_cast<uint2*>(dst) = u;
-}
-
-// Global row fragment (16 rows x 32 k, MFMA operand layout) straight to registers: lane (g, i) gets
-// row r0 + i, columns kk*32 + 8g .. +7; rows >= N and columns >= hd read as zero.
-template <int HD>
-__device__ __forceinline__ v8bf gl_row(const bf16_t* __restrict__ src, long row_stride, int r0, int kk, int N, int hd,
-                                       int lane) {
-  const int row = r0 + (lane & 15), col = kk * 32 + 8 * (lane >> 4);
-  v8s v = {0, 0, 0, 0, 0, 0, 0, 0};
-  if (row < N && col < hd) v = *reinterpret_cast<const v8s*>(src + (long)row * row_stride + col);
-  return __builtin_bit_cast(v8bf, v);
-}
+using namespace vit_attn;
 
 // ------------------------------------------------------------------------------------------------
 template <int HD, int NKT, int NW>
@@ -202,15 +99,6 @@ __global__ void __launch_bounds__(NW * 64) attn_fwd_kernel(const bf16_t* __restr
       if (q < N && d < hd) store4(o + ((long)b * N + q) * D + (long)h * hd + d, acc, inv_l);
     }
   }
-}
-
-// sum of the 16 lanes that share (lane >> 4): reduction over the MFMA column (key / query) index
-__device__ __forceinline__ float sum16(float v) {
-  v += __shfl_xor(v, 1, 64);
-  v += __shfl_xor(v, 2, 64);
-  v += __shfl_xor(v, 4, 64);
-  v += __shfl_xor(v, 8, 64);
-  return v;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -706,7 +594,7 @@ hipError_t dispatch_bwd(int nkt, const bf16_t* qkv, const bf16_t* o, const bf16_
 int check_shape(int64_t B, int64_t N, int64_t H, int64_t hd) {
   VIT_CHECK_ARG(B >= 1 && H >= 1 && N >= 1, "attention: bad sizes B=%lld N=%lld H=%lld", (long long)B, (long long)N,
                 (long long)H);
-  VIT_CHECK_ARG(N <= 320, "attention: N=%lld > 320 unsupported", (long long)N);
+  VIT_CHECK_ARG(N <= 16384 && B * H <= 0x7fffffff, "attention: N=%lld too large", (long long)N);
   VIT_CHECK_ARG(hd >= 16 && hd <= 96 && hd % 16 == 0, "attention: head_dim %lld unsupported (multiple of 16, <= 96)",
                 (long long)hd);
   return VIT_OK;
@@ -716,19 +604,48 @@ int check_shape(int64_t B, int64_t N, int64_t H, int64_t hd) {
 // runs on 96-wide images whose last 16 columns are zero).
 int image_width(int64_t hd) { return hd <= 32 ? 32 : hd <= 64 ? 64 : 96; }
 
+constexpr int64_t RESIDENT_MAX_N = 320;  // all keys of a head in LDS (attn_fwd_kernel / attn_bwd_kernel)
+
+// 1: LDS-resident kernels, 2: K/V-tiled kernels (attention_tiled.hip); 0 picks by N
+int resolve_path(int32_t path, int64_t N) {
+  if (path == 1 || path == 2) return path;
+  return N <= RESIDENT_MAX_N ? 1 : 2;
+}
+
 }  // namespace
 
-extern "C" int vit_attention_fwd_rows(const void* qkv, void* o, float* lse, int64_t B, int64_t N, int64_t H,
-                                      int64_t hd, float scale, int64_t q_rows, vit_stream_t stream) {
+hipError_t vit_attn_tiled_fwd(const void* qkv, void* o, float* lse, int B, int N, int H, int hd, float scale, int nq,
+                              hipStream_t s);
+hipError_t vit_attn_tiled_bwd(const void* qkv, const void* dout, const float* lse, float* delta, void* dqkv,
+                              float* bias_partial, int B, int N, int H, int hd, float scale, int nq, hipStream_t s);
+
+extern "C" int64_t vit_attention_bias_rows(int64_t N, int32_t path) {
+  return resolve_path(path, N) == 1 ? 1 : (N + 63) / 64;
+}
+
+extern "C" int64_t vit_attention_workspace_elems(int64_t B, int64_t N, int64_t H, int32_t path) {
+  return resolve_path(path, N) == 1 ? 0 : B * H * N;
+}
+
+extern "C" int vit_attention_fwd_ex(const void* qkv, void* o, float* lse, int64_t B, int64_t N, int64_t H, int64_t hd,
+                                    float scale, int64_t q_rows, int32_t path, vit_stream_t stream) {
   int st = check_shape(B, N, H, hd);
   if (st) return st;
   VIT_CHECK_ARG(qkv && o && lse, "vit_attention_fwd: null pointer");
   VIT_CHECK_ARG(q_rows >= 1 && q_rows <= N, "vit_attention_fwd: q_rows=%lld outside [1, N]", (long long)q_rows);
-  const int nkt = (int)((N + 31) / 32) * 2;
+  VIT_CHECK_ARG(path >= 0 && path <= 2, "vit_attention_fwd: path %d", (int)path);
+  const int p = resolve_path(path, N);
+  VIT_CHECK_ARG(p == 2 || N <= RESIDENT_MAX_N, "vit_attention_fwd: N=%lld > %lld on the LDS-resident path",
+                (long long)N, (long long)RESIDENT_MAX_N);
   const bf16_t* q = (const bf16_t*)qkv;
   hipStream_t s = (hipStream_t)stream;
   const int nq = (int)q_rows;
   hipError_t e;
+  if (p == 2) {
+    e = vit_attn_tiled_fwd(qkv, o, lse, (int)B, (int)N, (int)H, (int)hd, scale, nq, s);
+    return vit::check_hip(e, "vit_attention_fwd (tiled) launch");
+  }
+  const int nkt = (int)((N + 31) / 32) * 2;
   switch (image_width(hd)) {
     case 32: e = dispatch_fwd<32>(nkt, q, (bf16_t*)o, lse, (int)B, (int)N, (int)H, (int)hd, scale, nq, s); break;
     case 64: e = dispatch_fwd<64>(nkt, q, (bf16_t*)o, lse, (int)B, (int)N, (int)H, (int)hd, scale, nq, s); break;
@@ -737,23 +654,39 @@ extern "C" int vit_attention_fwd_rows(const void* qkv, void* o, float* lse, int6
   return vit::check_hip(e, "vit_attention_fwd launch");
 }
 
+extern "C" int vit_attention_fwd_rows(const void* qkv, void* o, float* lse, int64_t B, int64_t N, int64_t H,
+                                      int64_t hd, float scale, int64_t q_rows, vit_stream_t stream) {
+  return vit_attention_fwd_ex(qkv, o, lse, B, N, H, hd, scale, q_rows, 0, stream);
+}
+
 extern "C" int vit_attention_fwd(const void* qkv, void* o, float* lse, int64_t B, int64_t N, int64_t H, int64_t hd,
                                  float scale, vit_stream_t stream) {
   return vit_attention_fwd_rows(qkv, o, lse, B, N, H, hd, scale, N, stream);
 }
 
-extern "C" int vit_attention_bwd_rows(const void* qkv, const void* o, const void* dout, const float* lse, void* dqkv,
-                                      float* bias_partial, int64_t B, int64_t N, int64_t H, int64_t hd, float scale,
-                                      int64_t q_rows, vit_stream_t stream) {
+extern "C" int vit_attention_bwd_ex(const void* qkv, const void* o, const void* dout, const float* lse, void* dqkv,
+                                    float* bias_partial, int64_t B, int64_t N, int64_t H, int64_t hd, float scale,
+                                    int64_t q_rows, int32_t path, float* workspace, vit_stream_t stream) {
   int st = check_shape(B, N, H, hd);
   if (st) return st;
   VIT_CHECK_ARG(qkv && o && dout && lse && dqkv, "vit_attention_bwd: null pointer");
   VIT_CHECK_ARG(q_rows >= 1 && q_rows <= N, "vit_attention_bwd: q_rows=%lld outside [1, N]", (long long)q_rows);
-  const int nkt = (int)((N + 31) / 32) * 2;
-  const bf16_t *q = (const bf16_t*)qkv, *ob = (const bf16_t*)o, *d = (const bf16_t*)dout;
+  VIT_CHECK_ARG(path >= 0 && path <= 2, "vit_attention_bwd: path %d", (int)path);
+  const int p = resolve_path(path, N);
+  VIT_CHECK_ARG(p == 2 || N <= RESIDENT_MAX_N, "vit_attention_bwd: N=%lld > %lld on the LDS-resident path",
+                (long long)N, (long long)RESIDENT_MAX_N);
   hipStream_t s = (hipStream_t)stream;
   const int nq = (int)q_rows;
   hipError_t e;
+  if (p == 2) {
+    VIT_CHECK_ARG(workspace, "vit_attention_bwd: the tiled path (N=%lld) needs a workspace of "
+                  "vit_attention_workspace_elems() floats", (long long)N);
+    e = vit_attn_tiled_bwd(qkv, dout, lse, workspace, dqkv, bias_partial, (int)B, (int)N, (int)H, (int)hd, scale, nq,
+                           s);
+    return vit::check_hip(e, "vit_attention_bwd (tiled) launch");
+  }
+  const int nkt = (int)((N + 31) / 32) * 2;
+  const bf16_t *q = (const bf16_t*)qkv, *ob = (const bf16_t*)o, *d = (const bf16_t*)dout;
   switch (image_width(hd)) {
     case 32:
       e = dispatch_bwd<32>(nkt, q, ob, d, lse, (bf16_t*)dqkv, bias_partial, (int)B, (int)N, (int)H, (int)hd, scale, nq,
@@ -769,6 +702,12 @@ extern "C" int vit_attention_bwd_rows(const void* qkv, const void* o, const void
       break;
   }
   return vit::check_hip(e, "vit_attention_bwd launch");
+}
+
+extern "C" int vit_attention_bwd_rows(const void* qkv, const void* o, const void* dout, const float* lse, void* dqkv,
+                                      float* bias_partial, int64_t B, int64_t N, int64_t H, int64_t hd, float scale,
+                                      int64_t q_rows, vit_stream_t stream) {
+  return vit_attention_bwd_ex(qkv, o, dout, lse, dqkv, bias_partial, B, N, H, hd, scale, q_rows, 0, nullptr, stream);
 }
 
 extern "C" int vit_attention_bwd(const void* qkv, const void* o, const void* dout, const float* lse, void* dqkv,

@@ -1,0 +1,121 @@
+// Shared device helpers of the attention kernels (attention.hip: LDS-resident exact softmax for
+// N <= 320; attention_tiled.hip: K/V-tiled online softmax for longer sequences).
+#pragma once
+#include "common.h"
+
+namespace vit_attn {
+
+constexpr float LOG2E = 1.4426950408889634f;
+typedef unsigned v4u __attribute__((ext_vector_type(4)));
+
+template <int HD>
+__device__ __forceinline__ int aswz(int row) {
+  if constexpr (HD == 64) return ((row >> 1) & 3) << 1;
+  return 0;
+}
+
+template <int HD>
+__device__ __forceinline__ int img_off(int row, int chunk) {
+  return row * HD * 2 + ((chunk ^ aswz<HD>(row)) << 4);
+}
+
+// Load rows [0, NP) x [0, HD) of two strided bf16 matrices into swizzled LDS images (zero padded).
+// Every load of the thread is issued before the first LDS write (one HBM latency per image pair
+// instead of one per 16-B chunk): buffer loads against a descriptor that covers the valid rows, so
+// padding rows / columns >= hd read as zero without a branch around the load.
+template <int HD, int NP, int NT>
+__device__ __forceinline__ void load_images(char* imgA, const bf16_t* srcA, long strideA, char* imgB,
+                                            const bf16_t* srcB, long strideB, int N, int hd) {
+  constexpr int CPR = HD / 8;
+  constexpr int TOTAL = NP * CPR;
+  constexpr int PER = (TOTAL + NT - 1) / NT;
+  const __amdgpu_buffer_rsrc_t ra = make_rsrc(srcA, (uint32_t)(((long)(N - 1) * strideA + hd) * 2));
+  const __amdgpu_buffer_rsrc_t rb = make_rsrc(srcB, (uint32_t)(((long)(N - 1) * strideB + hd) * 2));
+  v4u a[PER], b[PER];
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const int c = threadIdx.x + k * NT;
+    const int row = c / CPR, ch = c % CPR;
+    const bool ok = c < TOTAL && row < N && ch * 8 < hd;
+    const int offa = ok ? (int)(((long)row * strideA + ch * 8) * 2) : 0x7ffffff0;
+    const int offb = ok ? (int)(((long)row * strideB + ch * 8) * 2) : 0x7ffffff0;
+    a[k] = __builtin_amdgcn_raw_buffer_load_b128(ra, offa, 0, 0);
+    b[k] = __builtin_amdgcn_raw_buffer_load_b128(rb, offb, 0, 0);
+  }
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const int c = threadIdx.x + k * NT;
+    if (c < TOTAL) {
+      const int row = c / CPR, ch = c % CPR;
+      *reinterpret_cast<v4u*>(imgA + img_off<HD>(row, ch)) = a[k];
+      *reinterpret_cast<v4u*>(imgB + img_off<HD>(row, ch)) = b[k];
+    }
+  }
+}
+
+// 16 rows x 32 k fragment: lane holds row r0 + (lane&15), k = kk*32 + 8*(lane>>4) + j.
+template <int HD>
+__device__ __forceinline__ v8bf rd_row(const char* img, int r0, int kk, int lane) {
+  const int row = r0 + (lane & 15);
+  const int ch = kk * 4 + (lane >> 4);
+  return __builtin_bit_cast(v8bf, *reinterpret_cast<const v8s*>(img + img_off<HD>(row, ch)));
+}
+
+// Transposed fragment: lane (g, i) gets column d0+i of image rows {16ta+4g+0..3, 16tb+4g+0..3}.
+template <int HD>
+__device__ __forceinline__ v8bf rd_tr(const char* img, int ta, int tb, int d0, int lane) {
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  const int colb = (d0 + 4 * p) * 2;
+  const int ch = colb >> 4, within = colb & 15;
+  const int ra = 16 * ta + 4 * g + q, rb = 16 * tb + 4 * g + q;
+  v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(v4s, img + img_off<HD>(ra, ch) + within));
+  v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(v4s, img + img_off<HD>(rb, ch) + within));
+  v8s r;
+  r.lo = lo;
+  r.hi = hi;
+  return __builtin_bit_cast(v8bf, r);
+}
+
+__device__ __forceinline__ v8bf pack8(const v4f& a, const v4f& b) {
+  v8s r;
+  r[0] = (short)f2bf(a[0]); r[1] = (short)f2bf(a[1]); r[2] = (short)f2bf(a[2]); r[3] = (short)f2bf(a[3]);
+  r[4] = (short)f2bf(b[0]); r[5] = (short)f2bf(b[1]); r[6] = (short)f2bf(b[2]); r[7] = (short)f2bf(b[3]);
+  return __builtin_bit_cast(v8bf, r);
+}
+
+// 2^x on the transcendental unit (bare v_exp_f32). Arguments are s*log2e - lse <= ~0, so results
+// only underflow (to 0) for keys whose softmax weight is below f32 resolution anyway.
+__device__ __forceinline__ float ex2(float x) { return __builtin_amdgcn_exp2f(x); }
+
+__device__ __forceinline__ v4f mfma(const v8bf& a, const v8bf& b, const v4f& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ void store4(bf16_t* dst, const v4f& v, float s) {
+  uint2 u;
+  u.x = pack2bf(v[0] * s, v[1] * s);
+  u.y = pack2bf(v[2] * s, v[3] * s);
+  *reinterpret_cast<uint2*>(dst) = u;
+}
+
+// Global row fragment (16 rows x 32 k, MFMA operand layout) straight to registers: lane (g, i) gets
+// row r0 + i, columns kk*32 + 8g .. +7; rows >= N and columns >= hd read as zero.
+template <int HD>
+__device__ __forceinline__ v8bf gl_row(const bf16_t* __restrict__ src, long row_stride, int r0, int kk, int N, int hd,
+                                       int lane) {
+  const int row = r0 + (lane & 15), col = kk * 32 + 8 * (lane >> 4);
+  v8s v = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (row < N && col < hd) v = *reinterpret_cast<const v8s*>(src + (long)row * row_stride + col);
+  return __builtin_bit_cast(v8bf, v);
+}
+
+// sum of the 16 lanes that share (lane >> 4): reduction over the MFMA column (key / query) index
+__device__ __forceinline__ float sum16(float v) {
+  v += __shfl_xor(v, 1, 64);
+  v += __shfl_xor(v, 2, 64);
+  v += __shfl_xor(v, 4, 64);
+  v += __shfl_xor(v, 8, 64);
+  return v;
+}
+
+}  // namespace vit_attn

@@ -206,7 +206,11 @@ __global__ void __launch_bounds__(256) ce_kernel(const float* __restrict__ logit
   __shared__ float red2[4];
   const int b = blockIdx.x;
   const float* x = logits + (long)b * C;
-  const int y = (int)labels[b];
+  const int64_t y64 = labels[b];
+  // a label outside [0, C) (torch's CrossEntropyLoss raises) is never dereferenced: the row's loss and
+  // gradient become NaN instead
+  const bool ok = y64 >= 0 && y64 < C;
+  const int y = ok ? (int)y64 : 0;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   float mx = -INFINITY;
   for (int c = threadIdx.x; c < C; c += 256) mx = fmaxf(mx, x[c]);
@@ -215,7 +219,7 @@ __global__ void __launch_bounds__(256) ce_kernel(const float* __restrict__ logit
   __syncthreads();
   mx = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
   __syncthreads();
-  const float xy = x[y];
+  const float xy = ok ? x[y] : __builtin_nanf("");
   float s = 0.f, gt = 0.f;
   for (int c = threadIdx.x; c < C; c += 256) {
     s += __expf(x[c] - mx);
@@ -234,7 +238,7 @@ __global__ void __launch_bounds__(256) ce_kernel(const float* __restrict__ logit
   if (dlogits) {
     for (int c = threadIdx.x; c < C; c += 256) {
       const float p = __expf(x[c] - lse);
-      dlogits[(long)b * C + c] = (p - (c == y ? 1.f : 0.f)) * grad_scale;
+      dlogits[(long)b * C + c] = ok ? (p - (c == y ? 1.f : 0.f)) * grad_scale : __builtin_nanf("");
     }
   }
   if (threadIdx.x == 0 && row_stats) {

@@ -37,10 +37,12 @@ class GradAllReducer:
 
     def attach(self):
         self.engine.grad_ready_hook = self.hook
+        self.engine.grad_ready_finish = self.finish
         return self
 
     def detach(self):
         self.engine.grad_ready_hook = None
+        self.engine.grad_ready_finish = None
 
     def _launch(self, buf, start, end, events=()):
         t = buf[start:end]

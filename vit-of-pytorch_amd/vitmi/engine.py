@@ -164,7 +164,12 @@ class _Acts:
         self.lnpart = z(ops.layernorm_bwd_partial_rows(T), 3 * D, dt=f)
         self.colpart = z(ops.colsum_partial_rows(T), max(3 * D, M, cfg.num_classes), dt=f)
         self.gelu_part = z(-(-T // 128), M, dt=f)   # per-M-tile column sums of dU (fc1 bias grad)
-        self.qkv_bpart = z(b, 3 * D, dt=f)          # per-image column sums of dq|dk|dv (q/k/v bias grads)
+        # column sums of dq|dk|dv (q/k/v bias grads): per image (LDS-resident attention, N <= 320) or per
+        # image and 64-row block (K/V-tiled attention, longer sequences)
+        self.attn_bias_rows = ops.attention_bias_rows(N)
+        self.qkv_bpart = z(b * self.attn_bias_rows, 3 * D, dt=f)
+        nws = ops.attention_workspace_elems(b, N, H)
+        self.attn_ws = z(nws, dt=f) if nws else None
         # last encoder layer on the cls rows only (ViTEngine.prune_last): compact operands, rows
         # padded to 64 with zeros that are never written (they are K rows of weight gradients)
         bp = _rup(b, 64)
@@ -185,8 +190,6 @@ class ViTEngine:
                                       "(multiples of 16 up to 96)")
         if cfg.emb_dim % 64 or cfg.mlp_dim % 64:
             raise NotImplementedError("emb_dim and mlp_dim must be multiples of 64")
-        if cfg.tokens > 320:
-            raise NotImplementedError(f"{cfg.tokens} tokens > 320 not supported by the attention kernel")
         self.cfg = cfg
         self.dev = torch.device(device)
         self.layout = FlatLayout(cfg)
@@ -216,6 +219,10 @@ class ViTEngine:
         self._ws = None
         self.step_id = 0
         self.grad_ready_hook = None  # callable(grad_buf, bucket_name, start, end, events) during backward
+        # callable() that completes every bucket the hook started (stream wait + any 1/world scaling); the
+        # autograd node calls it before handing gradients to autograd, which may add them into existing
+        # .grad tensors on the compute stream
+        self.grad_ready_finish = None
         # weight-gradient GEMMs on a side stream, overlapped with the dgrad chain (VITMI_OVERLAP=1).
         # Off by default: the GEMMs of both streams share the CUs and each runs 30-40% slower than
         # alone, so the serial order is faster on one MI355X (B/16 bs256: 6778 vs 6588 img/s,
@@ -621,11 +628,11 @@ class ViTEngine:
             dqkv = a.dqkv[li]
             acquire("dqkv", li)
             ops.attention_bwd(a.qkv[i], a.o[i], a.dO, a.lse[i], dqkv, b, N, H, hd, scale, bias_partial=a.qkv_bpart,
-                              q_rows=1 if pruned and i == L - 1 else None)
+                              q_rows=1 if pruned and i == L - 1 else None, workspace=a.attn_ws)
             qo = ln("attn.query.weight")
             zs = ln("attn.key.weight") - qo
             qb = ln("attn.query.bias")
-            ops.colsum3(a.qkv_bpart, b, D, 3 * D, a.colpart, g[qb:], g[qb + zs:], g[qb + 2 * zs:])
+            ops.colsum3(a.qkv_bpart, b * a.attn_bias_rows, D, 3 * D, a.colpart, g[qb:], g[qb + zs:], g[qb + 2 * zs:])
             on_side(lambda: self._wgrad(a.ln1[i], D, dqkv, 3 * D, D, D, a.Tp, g[qo:], D, batch=3, b_bs=D,
                                         out_bs=zs))
             release("dqkv", li)

@@ -146,6 +146,10 @@ class _ViTFunction(torch.autograd.Function):
         else:
             buf = eng.grad
         eng.backward(dlogits, buf)
+        if eng.grad_ready_finish is not None:
+            # data parallel: the buckets must be reduced (and averaged) before autograd adds them into
+            # existing .grad tensors (zero_grad(set_to_none=False), gradient accumulation)
+            eng.grad_ready_finish()
         grads = [eng.layout.view(buf, n) for n in model._flat_names]
         return (None, None, *grads)
 

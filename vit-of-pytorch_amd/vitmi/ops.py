@@ -112,19 +112,42 @@ def layernorm_bwd(dy, lddy, x, ldx, mean, rstd, gamma, dx, lddx, partial, rows, 
           "vit_layernorm_bwd")
 
 
-def attention_fwd(qkv, o, lse, B, N, H, hd, scale, q_rows=None):
-    """q_rows: only queries [0, q_rows) are needed (None: all N)."""
+ATTN_AUTO, ATTN_RESIDENT, ATTN_TILED = 0, 1, 2
+
+
+def attention_bias_rows(N, path=ATTN_AUTO):
+    """rows of the backward's bias_partial per image (1 resident, ceil(N/64) tiled)."""
+    return int(lib().vit_attention_bias_rows(N, path))
+
+
+def attention_workspace_elems(B, N, H, path=ATTN_AUTO):
+    return int(lib().vit_attention_workspace_elems(B, N, H, path))
+
+
+def attention_fwd(qkv, o, lse, B, N, H, hd, scale, q_rows=None, path=ATTN_AUTO):
+    """q_rows: only queries [0, q_rows) are needed (None: all N). path: ATTN_AUTO picks the
+    LDS-resident kernels for N <= 320 and the K/V-tiled ones above."""
     _chk(qkv, BF16, "qkv")
     _chk(o, BF16, "o")
     _chk(lse, F32, "lse")
-    check(lib().vit_attention_fwd_rows(_p(qkv), _p(o), _p(lse), B, N, H, hd, scale, N if q_rows is None else q_rows,
-                                       _stream()), "vit_attention_fwd")
+    check(lib().vit_attention_fwd_ex(_p(qkv), _p(o), _p(lse), B, N, H, hd, scale, N if q_rows is None else q_rows,
+                                     path, _stream()), "vit_attention_fwd")
 
 
-def attention_bwd(qkv, o, dout, lse, dqkv, B, N, H, hd, scale, bias_partial=None, q_rows=None):
-    """q_rows: dout is zero outside queries [0, q_rows) (None: all N)."""
-    check(lib().vit_attention_bwd_rows(_p(qkv), _p(o), _p(dout), _p(lse), _p(dqkv), _p(bias_partial), B, N, H, hd,
-                                       scale, N if q_rows is None else q_rows, _stream()), "vit_attention_bwd")
+def attention_bwd(qkv, o, dout, lse, dqkv, B, N, H, hd, scale, bias_partial=None, q_rows=None, path=ATTN_AUTO,
+                  workspace=None):
+    """q_rows: dout is zero outside queries [0, q_rows) (None: all N). bias_partial:
+    [B * attention_bias_rows(N, path)][3D] f32. workspace: >= attention_workspace_elems floats
+    (allocated here when None and the path needs one)."""
+    _chk(workspace, F32, "workspace")
+    need = attention_workspace_elems(B, N, H, path)
+    if need and (workspace is None or workspace.numel() < need):
+        if workspace is not None:
+            raise ValueError(f"attention workspace has {workspace.numel()} floats, needs {need}")
+        workspace = torch.empty(need, device=qkv.device, dtype=F32)
+    check(lib().vit_attention_bwd_ex(_p(qkv), _p(o), _p(dout), _p(lse), _p(dqkv), _p(bias_partial), B, N, H, hd,
+                                     scale, N if q_rows is None else q_rows, path, _p(workspace if need else None),
+                                     _stream()), "vit_attention_bwd")
 
 
 def im2col(x, out, B, img, P, Kpad):
