@@ -1,11 +1,13 @@
 """JAX .npz checkpoint import (reference src/checkpoint.py) on CPU.
 
-The reference's converter imports tensorflow (absent here), so it cannot run in this image: the
-expected names and layouts below are written from the Flax ViT parameter tree the reference converts
-(`Transformer/encoderblock_i/...`, HWIO conv kernel, [in][out] Dense kernels, [D][H][hd] q/k/v
-kernels) and from the reference model's own parameter names (src/model.py). Parity with an executed
-reference is therefore unpinned for this module; the round trip below pins every name and layout rule.
+Pinned to the reference: tests/golden/jax_convert.npz holds the output of the reference's own
+load_checkpoint -> load_jax -> convert_jax_pytorch (src/checkpoint.py:7-25, 80-115), run on a
+synthetic Flax-named ViT parameter dump with a stub `tensorflow.io.gfile` (the only tensorflow use,
+:3, :22); tests/golden/make_jax_golden.py is the generator. vitmi.checkpoint must reproduce it bit for
+bit. The round trip below additionally pins every name and layout rule against the model itself.
 """
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -94,3 +96,26 @@ def test_layout_rules_and_errors(tmp_path):
     assert sd["x.query.bias"].shape == (2, 3)     # multi-head biases keep [H][hd]
     with pytest.raises(ValueError):
         load_checkpoint(str(tmp_path / "w.bin"))
+
+
+def test_convert_matches_reference_converter_golden(golden_dir, tmp_path):
+    """vitmi.checkpoint vs the reference's executed converter (tests/golden/jax_convert.npz)."""
+    z = np.load(os.path.join(golden_dir, "jax_convert.npz"))
+    order = [str(k) for k in z["order"]]
+    values = [z["in/" + k] for k in order]
+    expect = {k[4:]: z[k] for k in z.files if k.startswith("out/")}
+    got = convert_jax_pytorch(order, values)
+    assert list(got) == list(expect)  # same keys, same order
+    for k, v in expect.items():
+        assert got[k].dtype == torch.float32
+        assert tuple(got[k].shape) == v.shape, k
+        assert np.array_equal(got[k].numpy(), v), k
+    # through the file path (load_checkpoint -> load_jax), as the reference reads it
+    path = tmp_path / "ViT-tiny.npz"
+    np.savez(path, **{k: z["in/" + k] for k in order})
+    from_file = load_checkpoint(str(path))
+    assert list(from_file) == list(expect)
+    assert all(np.array_equal(from_file[k].numpy(), expect[k]) for k in expect)
+    # and the converted weights load into the drop-in model (tiny config: D 64, H 2, P 8, 10 classes)
+    m = VisionTransformer(**ARCH)
+    m.load_state_dict(from_file)

@@ -329,3 +329,66 @@ def test_b16_384_matches_oracle():
     with torch.no_grad():
         exact = m(x.cuda())
     assert rel(exact, ref_logits) < 1e-3, rel(exact, ref_logits)
+
+
+# ---- the BASELINE configs' shapes through the HIP step ----------------------------------------------
+L16 = ViTConfig(emb_dim=1024, mlp_dim=4096, num_heads=16, num_layers=24)                 # C3 per-rank shape
+H14 = ViTConfig(patch_size=14, emb_dim=1280, mlp_dim=5120, num_heads=16, num_layers=32)  # C4: N 257, hd 80
+
+
+@pytest.mark.parametrize("cfg,bs", [(L16, 2), (H14, 1)], ids=["l16", "h14"])
+def test_large_arch_step_matches_oracle(cfg, bs):
+    """ViT-L/16 and ViT-H/14 @224 (all 24 / 32 layers, tamed init): the bf16 training step vs the
+    oracle (G2 loss 1e-3 / logits 1e-2, G3 every gradient tensor) and the fp32 forward (G1, 1e-3)."""
+    params = tame_params(init_params(cfg, seed=42))
+    g = torch.Generator().manual_seed(17)
+    x = torch.randn(bs, 3, 224, 224, generator=g)
+    y = torch.randint(0, 1000, (bs,), generator=g)
+    ref_logits, ref_loss, ref_grads = loss_and_grads(params, x, y, cfg)
+    m = make_model(cfg, params)
+    from vitmi.model import CrossEntropyLoss
+    logits = m(x.cuda())
+    loss = CrossEntropyLoss()(logits, y.cuda())
+    loss.backward()
+    assert rel(logits, ref_logits) < 1e-2
+    assert abs(float(loss.detach()) - float(ref_loss)) <= 1e-3 * abs(float(ref_loss))
+    check_grads(m, ref_grads)
+    m.precision = "fp32"
+    with torch.no_grad():
+        exact = m(x.cuda())
+    assert rel(exact, ref_logits) < 1e-3, rel(exact, ref_logits)
+
+
+def test_b16_bs256_step_consistent_with_small_batches():
+    """The benchmarked shape (ViT-B/16 @224, bs 256, T = 50 432 rows: wave-split GEMM tiles, split-K
+    weight gradients, 3072-(image, head) attention grid) against 128 bs-2 runs of the same images:
+    logits / per-image loss equal within bf16 tolerance, and the bs-256 gradient equals the mean of
+    the bs-2 gradients; an 8-image slice's loss against the oracle (fp32 CPU)."""
+    from vitmi.engine import ArchConfig, ViTEngine
+    cfg = B16
+    params = tame_params(init_params(cfg, seed=42))
+    eng = ViTEngine(ArchConfig())
+    eng.load_params(params)
+    eng.refresh_mirror()
+    g = torch.Generator().manual_seed(23)
+    x = torch.randn(256, 3, 224, 224, generator=g)
+    y = torch.randint(0, 1000, (256,), generator=g)
+    xd, yd = x.cuda(), y.cuda()
+    logits = eng.forward(xd).clone()
+    _, st = eng.cross_entropy(yd)
+    loss_rows = st[:, 0].clone()
+    gbig = eng.backward(eng.cross_entropy(yd, grad_scale=1.0 / 256)[0]).clone()
+    small_logits, small_loss = [], []
+    gsum = torch.zeros_like(gbig)
+    for k in range(0, 256, 2):
+        small_logits.append(eng.forward(xd[k:k + 2]).clone())
+        dl, st2 = eng.cross_entropy(yd[k:k + 2], grad_scale=1.0 / 256)
+        small_loss.append(st2[:, 0].clone())
+        gsum += eng.backward(dl)
+    torch.cuda.synchronize()
+    assert rel(logits, torch.cat(small_logits)) < 5e-3
+    assert rel(loss_rows, torch.cat(small_loss)) < 1e-3
+    assert rel(gbig, gsum) < 1e-2, rel(gbig, gsum)
+    ref_logits, ref_loss, _ = loss_and_grads(params, x[:8], y[:8], cfg)
+    assert rel(logits[:8], ref_logits) < 1e-2
+    assert abs(float(loss_rows[:8].mean()) - float(ref_loss)) <= 1e-3 * float(ref_loss)

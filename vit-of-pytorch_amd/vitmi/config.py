@@ -8,6 +8,7 @@ src/config.py:57-104). Additions for the MI355X path, all optional:
                          normalised on the device like the reference's CIFAR transform (vitmi.data)
   --any-image-size       lift the reference's choices=[224, 384] on --image-size (src/config.py:37)
   --no-save              do not create experiments/ directories or checkpoints
+  --precision            (eval) bf16 MFMA forward (default) or the reference's f32 arithmetic
 """
 from __future__ import annotations
 
@@ -44,6 +45,8 @@ def get_eval_config(argv=None):
     _image_size_arg(parser, 384)
     parser.add_argument("--num-workers", type=int, default=8, help="number of workers")
     parser.add_argument("--dataset", type=str, default="ImageNet", help="dataset for fine-tunning/evaluation")
+    parser.add_argument("--precision", type=str, default="bf16", choices=["bf16", "fp32"],
+                        help="bf16 MFMA forward or the reference's f32 arithmetic")
     config = parser.parse_args(argv)
     _check_image_size(config)
     config = globals()["get_{}_config".format(config.model_arch)](config)

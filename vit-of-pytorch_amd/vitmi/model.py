@@ -250,26 +250,33 @@ class VisionTransformer(nn.Module):
 
 
 class CrossEntropyLoss(nn.Module):
-    """nn.CrossEntropyLoss() (mean) on the HIP cross-entropy kernel (reference src/train.py:151)."""
+    """nn.CrossEntropyLoss() (mean) on the HIP cross-entropy kernel (reference src/train.py:151).
+    The kernel also counts top-1 / top-5 hits per row (src/utils.py:28-41): `last_row_stats`
+    holds {loss, top1, top5} [b, 3] of the latest call, which vitmi.train uses for accuracy."""
+
+    def __init__(self):
+        super().__init__()
+        self.last_row_stats = None
 
     def forward(self, logits, target):
-        return _CEFunction.apply(logits, target)
+        st = torch.empty(logits.shape[0], 3, device=logits.device)
+        loss = _CEFunction.apply(logits, target, st)
+        self.last_row_stats = st
+        return loss
 
 
 class _CEFunction(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, logits, target):
+    def forward(ctx, logits, target, st):
         from . import ops
         logits = logits.float().contiguous()
         b, c = logits.shape
         dl = torch.empty_like(logits)
-        st = torch.empty(b, 3, device=logits.device)
         ops.cross_entropy(logits, target.to(torch.int64).contiguous(), dl, 1.0 / b, st)
         ctx.save_for_backward(dl)
-        ctx.row_stats = st
         return st[:, 0].mean()
 
     @staticmethod
     def backward(ctx, g):
         dl, = ctx.saved_tensors
-        return dl * g, None
+        return dl * g, None, None

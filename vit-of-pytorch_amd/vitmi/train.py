@@ -4,20 +4,24 @@
     torchrun --nproc-per-node 8 -m vitmi.train ...   # data parallel, one process per GPU (RCCL)
 
 Entry points keep the reference signatures: train_epoch (src/train.py:12-37), valid_epoch (:40-66),
-save_model (:69-81), main (:84-194). Differences, all on the execution side:
+save_model (:69-81), main (:84-194); MetricTracker / the step writer follow src/utils.py:79-100,
+177-230. Differences, all on the execution side:
   * the model is vitmi.model.VisionTransformer (HIP engine), the optimizer vitmi.optim.SGD
     (torch.optim.SGD semantics, fused HIP update), the scheduler torch's OneCycleLR as configured
     by the reference (:159-163);
   * multi-GPU is one process per GPU with gradient all-reduce over RCCL overlapped with the
-    backward (vitmi.dist), instead of single-process nn.DataParallel (:128-129);
-  * loss / accuracy are accumulated on the device and read back when printed, instead of three
-    .item() host syncs per step (:29-32); the reported means are the same.
+    backward (vitmi.dist, attached to the model's engine: the backward hands autograd reduced
+    gradients), instead of single-process nn.DataParallel (:128-129);
+  * loss / top-1 / top-5 come from the fused cross-entropy kernel's per-row statistics and are
+    accumulated on the device, read back when printed, instead of three .item() host syncs per
+    step (:29-32); the reported means are the same.
 """
 from __future__ import annotations
 
 import os
 import random
 import sys
+import time
 
 import numpy as np
 import torch
@@ -49,11 +53,40 @@ def accuracy(output, target, topk=(1,)):
     return [correct[:k].reshape(-1).float().sum(0) / batch_size * 100.0 for k in topk]
 
 
+class StepWriter:
+    """The metrics writer interface train_epoch / valid_epoch drive (reference SwanLabWriter,
+    src/utils.py:177-230, with SwanLab absent): set_step / add_scalar / log_metric, keeping the
+    step, mode and steps_per_sec in memory (device scalars stay on the device)."""
+
+    def __init__(self, log_dir=None, enabled=False):
+        self.enabled = False  # no SwanLab / TensorBoard backend in this environment
+        self.step = 0
+        self.mode = ""
+        self.timer = time.perf_counter()
+        self.scalars = []  # (step, tag, value)
+
+    def set_step(self, step, mode="train"):
+        self.mode = mode
+        self.step = step
+        now = time.perf_counter()
+        if step != 0:
+            self.log_metric("steps_per_sec", 1.0 / max(now - self.timer, 1e-9))
+        self.timer = now
+
+    def add_scalar(self, tag, data, *args, **kwargs):
+        self.scalars.append((self.step, f"{tag}/{self.mode}" if self.mode else tag, data))
+        if len(self.scalars) > 4096:
+            del self.scalars[:2048]
+
+    def log_metric(self, tag, data, *args, **kwargs):
+        self.add_scalar(tag, data)
+
+
 class MetricTracker:
     """Running means of named scalars (reference src/utils.py:79-100), device-resident."""
 
     def __init__(self, *keys, writer=None):
-        self.writer = writer
+        self.writer = writer if writer is not None else StepWriter()
         self.keys = keys
         self.reset()
 
@@ -62,6 +95,8 @@ class MetricTracker:
         self._count = {k: 0 for k in self.keys}
 
     def update(self, key, value, n=1):
+        if self.writer is not None:
+            self.writer.add_scalar(key, value)
         self._total[key] = self._total[key] + value * n
         self._count[key] += n
 
@@ -72,6 +107,15 @@ class MetricTracker:
 
     def result(self):
         return {k: self.avg(k) for k in self.keys}
+
+
+def _step_accuracy(criterion, pred, target):
+    """top-1 / top-5 (%) of the batch: from the fused CE kernel's per-row hit counts when the
+    criterion is vitmi's CrossEntropyLoss (no extra pass), else src/utils.py:28-41's topk."""
+    st = getattr(criterion, "last_row_stats", None)
+    if st is not None and st.shape[0] == target.shape[0]:
+        return st[:, 1].mean() * 100.0, st[:, 2].mean() * 100.0
+    return accuracy(pred.detach(), target, topk=(1, 5))
 
 
 class SyntheticDataLoader:
@@ -124,8 +168,7 @@ def _world():
     return dist.get_world_size() if dist.is_initialized() else 1
 
 
-def train_epoch(epoch, model, data_loader, criterion, optimizer, lr_scheduler, metrics, device=torch.device("cpu"),
-                reducer=None, log_every=100):
+def train_epoch(epoch, model, data_loader, criterion, optimizer, lr_scheduler, metrics, device=torch.device("cpu")):
     """reference src/train.py:12-37 (one optimizer step per batch)."""
     metrics.reset()
     for batch_idx, (batch_data, batch_target) in enumerate(data_loader):
@@ -135,22 +178,21 @@ def train_epoch(epoch, model, data_loader, criterion, optimizer, lr_scheduler, m
         batch_pred = model(batch_data)
         loss = criterion(batch_pred, batch_target)
         loss.backward()
-        if reducer is not None:
-            reducer.finish()
         optimizer.step()
         lr_scheduler.step()
-        acc1, acc5 = accuracy(batch_pred.detach(), batch_target, topk=(1, 5))
+        acc1, acc5 = _step_accuracy(criterion, batch_pred, batch_target)
+        metrics.writer.set_step((epoch - 1) * len(data_loader) + batch_idx)
         metrics.update("loss", loss.detach())
         metrics.update("acc1", acc1)
         metrics.update("acc5", acc5)
-        if batch_idx % log_every == 0 and (not dist.is_initialized() or dist.get_rank() == 0):
+        if batch_idx % 100 == 0 and (not dist.is_initialized() or dist.get_rank() == 0):
             print("Train Epoch: {:03d} Batch: {:05d}/{:05d} Loss: {:.4f} Acc@1: {:.2f}, Acc@5: {:.2f}"
                   .format(epoch, batch_idx, len(data_loader), float(loss.detach()), float(acc1), float(acc5)), flush=True)
     return metrics.result()
 
 
 def valid_epoch(epoch, model, data_loader, criterion, metrics, device=torch.device("cpu")):
-    """reference src/train.py:40-66 (forward-only)."""
+    """reference src/train.py:40-66 (forward-only; means over batches)."""
     metrics.reset()
     losses, acc1s, acc5s = [], [], []
     with torch.no_grad():
@@ -159,10 +201,11 @@ def valid_epoch(epoch, model, data_loader, criterion, metrics, device=torch.devi
             batch_target = batch_target.to(device)
             batch_pred = model(batch_data)
             loss = criterion(batch_pred, batch_target)
-            acc1, acc5 = accuracy(batch_pred, batch_target, topk=(1, 5))
+            acc1, acc5 = _step_accuracy(criterion, batch_pred, batch_target)
             losses.append(loss)
             acc1s.append(acc1)
             acc5s.append(acc5)
+    metrics.writer.set_step(epoch, "valid")
     metrics.update("loss", float(torch.stack(losses).mean()))
     metrics.update("acc1", float(torch.stack(acc1s).mean()))
     metrics.update("acc5", float(torch.stack(acc5s).mean()))
@@ -221,10 +264,9 @@ def main(argv=None):
         print("Load pretrained weights from {}".format(config.checkpoint_path))
     model = model.to(device)
     engine = model.engine()
-    reducer = None
     if world > 1:
         dist.broadcast(engine.flat, 0)  # identical replicas
-        reducer = GradAllReducer(engine).attach()
+        GradAllReducer(engine).attach()  # the backward returns all-reduced (averaged) gradients
 
     if not config.synthetic:
         raise SystemExit("torchvision datasets are not available in this environment; use --synthetic "
@@ -248,16 +290,18 @@ def main(argv=None):
     lr_scheduler = torch.optim.lr_scheduler.OneCycleLR(optimizer=optimizer, max_lr=config.lr,
                                                        pct_start=config.warmup_steps / config.train_steps,
                                                        total_steps=config.train_steps)
+    writer = StepWriter(config.summary_dir, config.swanlab)
     metric_names = ["loss", "acc1", "acc5"]
-    train_metrics = MetricTracker(*metric_names)
-    valid_metrics = MetricTracker(*metric_names)
+    train_metrics = MetricTracker(*metric_names, writer=writer)
+    valid_metrics = MetricTracker(*metric_names, writer=writer)
     best_acc = 0.0
-    epochs = max(1, config.train_steps // len(train_loader))
+    epochs = config.train_steps // len(train_loader)  # the reference's count (src/train.py:172): may be 0
+    if rank == 0:
+        print(config.train_steps, len(train_loader), epochs)
     for epoch in range(1, epochs + 1):
         log = {"epoch": epoch}
         model.train()
-        log.update(train_epoch(epoch, model, train_loader, criterion, optimizer, lr_scheduler, train_metrics, device,
-                               reducer=reducer))
+        log.update(train_epoch(epoch, model, train_loader, criterion, optimizer, lr_scheduler, train_metrics, device))
         model.eval()
         result = valid_epoch(epoch, model, valid_loader, criterion, valid_metrics, device)
         log.update(**{"val_" + k: v for k, v in result.items()})
@@ -271,6 +315,7 @@ def main(argv=None):
                 print("    {:15s}: {}".format(str(key), value), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    return best_acc
 
 
 if __name__ == "__main__":
