@@ -288,6 +288,22 @@ int vit_gelu_f32(const float* in, float* out, int64_t n, vit_stream_t stream);
 int vit_attention_fwd_f32(const float* qkv, float* o, int64_t B, int64_t N, int64_t H, int64_t hd,
                           float inv_sqrt_hd, vit_stream_t stream);
 
+/* ------------------------------------------------------------------------------------------
+ * Standalone sub-module path (vitmi.model Encoder / EncoderBlock / SelfAttention / MlpBlock /
+ * LinearGeneral / PositionEmbs .forward on their own, composed from the kernels above plus these):
+ * ---------------------------------------------------------------------------------------- */
+/* dx = dy * GELU'(u), exact erf (autograd of nn.GELU, src/model.py:33,44) */
+int vit_gelu_bwd_f32(const float* u, const float* dy, float* dx, int64_t n, vit_stream_t stream);
+/* out[r*cols + c] = in[r*cols + c] * multiplier(r, c) of dropout descriptor d (in == out allowed);
+ * forward and backward of nn.Dropout (src/model.py:19-20,46-51,124-125) regenerate the same mask */
+int vit_dropout_apply_f32(const vit_dropout* d, const float* in, float* out, int64_t rows, int64_t cols,
+                          vit_stream_t stream);
+/* out[o*inner + i] = x[o*inner + i] + y[i]  (PositionEmbs: x + pos_embedding, src/model.py:17) */
+int vit_add_bcast_f32(const float* x, const float* y, float* out, int64_t outer, int64_t inner, vit_stream_t stream);
+/* out[r*ldo + c] = f32(in[r*ldi + c]) for bf16 `in` (attention outputs / gradients back to f32 modules) */
+int vit_unpack_bf16_f32(const void* in, int64_t ldi, int64_t rows, int64_t cols, float* out, int64_t ldo,
+                        vit_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -153,6 +153,71 @@ def tame_params(params: "OrderedDict[str, torch.Tensor]", seed: int = 1) -> "Ord
     return out
 
 
+# ---- per-block restatements (the standalone sub-module forwards of reference src/model.py) ----------
+def position_embs(x, pos):
+    """PositionEmbs.forward without dropout (reference src/model.py:16-22): x + pos_embedding."""
+    return x + pos
+
+
+def linear_general(x, w, b, n_in):
+    """LinearGeneral.forward (reference src/model.py:61-63) for dims = (trailing n_in dims of x,
+    leading n_in dims of w): tensordot(x, w, dims) + b."""
+    k = math.prod(w.shape[:n_in])
+    out_shape = tuple(x.shape[:x.dim() - n_in]) + tuple(w.shape[n_in:])
+    return (x.reshape(-1, k) @ w.reshape(k, -1) + b.reshape(-1)).reshape(out_shape)
+
+
+def attention_core(q, k, v):
+    """SelfAttention.forward's core (reference src/model.py:90-97): q, k, v [b, n, H, hd] ->
+    softmax((q k^T) / sqrt(hd)) v, [b, n, H, hd]; the scores are divided AFTER the matmul (:94)."""
+    hd = q.shape[-1]
+    q, k, v = (t.transpose(1, 2) for t in (q, k, v))
+    s = (q @ k.transpose(-2, -1)) / (hd ** 0.5)
+    return (torch.softmax(s, dim=-1) @ v).transpose(1, 2)
+
+
+def self_attention(p, pre, x):
+    """SelfAttention.forward (reference src/model.py:83-101); p[pre + 'query.weight'] etc."""
+    q = linear_general(x, p[pre + "query.weight"], p[pre + "query.bias"], 1)
+    k = linear_general(x, p[pre + "key.weight"], p[pre + "key.bias"], 1)
+    v = linear_general(x, p[pre + "value.weight"], p[pre + "value.bias"], 1)
+    return linear_general(attention_core(q, k, v), p[pre + "out.weight"], p[pre + "out.bias"], 2)
+
+
+def mlp_block(p, pre, x, d1=None, d2=None):
+    """MlpBlock.forward (reference src/model.py:41-51): fc1 -> exact-erf GELU -> [dropout1] -> fc2 ->
+    [dropout2]; d1 / d2 optional dropout multipliers."""
+    g = F.gelu(F.linear(x, p[pre + "fc1.weight"], p[pre + "fc1.bias"]))
+    if d1 is not None:
+        g = g * d1
+    y = F.linear(g, p[pre + "fc2.weight"], p[pre + "fc2.bias"])
+    return y * d2 if d2 is not None else y
+
+
+def encoder_block(p, pre, h, da=None, d1=None, d2=None):
+    """EncoderBlock.forward (reference src/model.py:117-130), pre-LN, eps 1e-5, in-place residuals."""
+    D = h.shape[-1]
+    y = F.layer_norm(h, (D,), p[pre + "norm1.weight"], p[pre + "norm1.bias"], 1e-5)
+    o = self_attention(p, pre + "attn.", y)
+    h = h + (o * da if da is not None else o)
+    y = F.layer_norm(h, (D,), p[pre + "norm2.weight"], p[pre + "norm2.bias"], 1e-5)
+    return h + mlp_block(p, pre + "mlp.", y, d1, d2)
+
+
+def encoder(p, pre, x, num_layers, drop=None):
+    """Encoder.forward (reference src/model.py:148-156): position embedding, blocks, final LayerNorm
+    over every token. drop: as for forward()."""
+    g = (lambda key: drop[key]) if drop else (lambda key: None)
+    h = position_embs(x, p[pre + "pos_embedding.pos_embedding"])
+    if drop:
+        h = h * drop["pos"]
+    for i in range(num_layers):
+        q_ = f"{pre}encoder_layers.{i}."
+        h = encoder_block(p, q_, h, g(("attn", i)), g(("d1", i)), g(("d2", i)))
+    D = h.shape[-1]
+    return F.layer_norm(h, (D,), p[pre + "norm.weight"], p[pre + "norm.bias"], 1e-5)
+
+
 def forward(params, x: torch.Tensor, cfg: ViTConfig, drop=None) -> torch.Tensor:
     """Functional ViT forward (reference src/model.py:196-211 and the modules it calls).
 
@@ -160,43 +225,16 @@ def forward(params, x: torch.Tensor, cfg: ViTConfig, drop=None) -> torch.Tensor:
     the reference: drop["pos"] [b, n, D] after the position embedding (:19-20); per layer i
     drop[("attn", i)] [b, n, D] on the attention output (:124-125), drop[("d1", i)] [b, n, M] after
     GELU (:46-47) and drop[("d2", i)] [b, n, D] after fc2 (:50-51)."""
-    dm = (lambda key, t: t * drop[key].to(t.dtype)) if drop else (lambda key, t: t)
-    D, H = cfg.emb_dim, cfg.num_heads
-    hd = D // H
+    D = cfg.emb_dim
     p = params
     # patch embedding: Conv2d(k=s=P) (reference :179,197), token-major (:198-200)
     emb = F.conv2d(x, p["embedding.weight"], p["embedding.bias"], stride=cfg.patch_size)
     b = emb.shape[0]
     emb = emb.permute(0, 2, 3, 1).reshape(b, -1, D)
-    # prepend cls (:203-204), + pos-emb (PositionEmbs.forward :16-22)
+    # prepend cls (:203-204), then the encoder (:207; PositionEmbs, blocks, final LN)
     h = torch.cat([p["cls_token"].expand(b, 1, D), emb], dim=1)
-    h = dm("pos", h + p["transformer.pos_embedding.pos_embedding"])
-    n = h.shape[1]
-    for i in range(cfg.num_layers):
-        q_ = f"transformer.encoder_layers.{i}."
-        # EncoderBlock.forward (:117-130), pre-LN, eps 1e-5
-        y = F.layer_norm(h, (D,), p[q_ + "norm1.weight"], p[q_ + "norm1.bias"], 1e-5)
-        # LinearGeneral: tensordot(x, W[D,H,hd]) + b[H,hd] (:61-63, :86-88)
-        q = (y @ p[q_ + "attn.query.weight"].reshape(D, D) + p[q_ + "attn.query.bias"].reshape(D))
-        k = (y @ p[q_ + "attn.key.weight"].reshape(D, D) + p[q_ + "attn.key.bias"].reshape(D))
-        v = (y @ p[q_ + "attn.value.weight"].reshape(D, D) + p[q_ + "attn.value.bias"].reshape(D))
-        q = q.reshape(b, n, H, hd).transpose(1, 2)
-        k = k.reshape(b, n, H, hd).transpose(1, 2)
-        v = v.reshape(b, n, H, hd).transpose(1, 2)
-        # scores divided AFTER the matmul by sqrt(hd) (:94), softmax(-1) (:95), @ v (:96)
-        s = (q @ k.transpose(-2, -1)) / (hd ** 0.5)
-        a = torch.softmax(s, dim=-1) @ v
-        a = a.transpose(1, 2).reshape(b, n, D)
-        # out LinearGeneral W[H,hd,D] contracted over (H,hd) (:97-99)
-        o = a @ p[q_ + "attn.out.weight"].reshape(D, D) + p[q_ + "attn.out.bias"]
-        h = h + dm(("attn", i), o)
-        y = F.layer_norm(h, (D,), p[q_ + "norm2.weight"], p[q_ + "norm2.bias"], 1e-5)
-        # MlpBlock: fc1 -> exact-erf GELU -> fc2 (:41-51)
-        u = F.linear(y, p[q_ + "mlp.fc1.weight"], p[q_ + "mlp.fc1.bias"])
-        g = dm(("d1", i), F.gelu(u))
-        h = h + dm(("d2", i), F.linear(g, p[q_ + "mlp.fc2.weight"], p[q_ + "mlp.fc2.bias"]))
-    # final LayerNorm over all tokens (:155), classifier on the cls row (:210)
-    h = F.layer_norm(h, (D,), p["transformer.norm.weight"], p["transformer.norm.bias"], 1e-5)
+    h = encoder(p, "transformer.", h, cfg.num_layers, drop)
+    # classifier on the cls row (:210)
     return F.linear(h[:, 0], p["classifier.weight"], p["classifier.bias"])
 
 

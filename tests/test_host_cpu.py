@@ -72,3 +72,14 @@ def test_cpu_forward_refuses():
                           num_classes=10, dropout_rate=0.0)
     with pytest.raises(RuntimeError, match="MI355X HIP path only"):
         m(torch.randn(1, 3, 32, 32))
+
+
+def test_cpu_submodule_forwards_refuse():
+    """standalone sub-modules run on the HIP kernels only (no PyTorch CPU fallback)"""
+    from vitmi.model import EncoderBlock, LinearGeneral, MlpBlock
+    with pytest.raises(RuntimeError, match="MI355X HIP path only"):
+        EncoderBlock(64, 128, 2, dropout_rate=0.0)(torch.randn(1, 5, 64))
+    with pytest.raises(RuntimeError, match="MI355X HIP path only"):
+        MlpBlock(64, 128, 64, dropout_rate=0.0)(torch.randn(1, 5, 64))
+    with pytest.raises(RuntimeError, match="MI355X HIP path only"):
+        LinearGeneral((64,), (2, 32))(torch.randn(1, 5, 64), dims=([2], [0]))

@@ -569,3 +569,80 @@ extern "C" int vit_dropout_mask(const vit_dropout* d, int64_t row0, int64_t rows
                      (hipStream_t)stream, make_drop(d), (long)row0, (long)rows, (int)cols, mult, (long)ld);
   VIT_LAUNCH_CHECK("vit_dropout_mask");
 }
+
+// ---- standalone sub-module path (vitmi.model Encoder / EncoderBlock / MlpBlock / ... .forward) ----
+namespace {
+// dx = dy * GELU'(u), exact erf (nn.GELU backward, src/model.py:33)
+__global__ void gelu_bwd_f32_kernel(const float* __restrict__ u, const float* __restrict__ dy, float* __restrict__ dx,
+                                    long n) {
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const float x = u[i];
+    const float cdf = 0.5f * (1.0f + erff(x * 0.70710678118654752f));
+    const float pdf = 0.39894228040143268f * expf(-0.5f * x * x);
+    dx[i] = dy[i] * (cdf + x * pdf);
+  }
+}
+// out[r][c] = in[r][c] * dropout multiplier of (r, c)  (nn.Dropout, src/model.py:19-20,46-51,124-125)
+__global__ void dropout_apply_kernel(DropDev drop, const float* __restrict__ in, float* __restrict__ out, long rows,
+                                     int cols) {
+  const long total = rows * cols;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const long r = i / cols;
+    const int c = (int)(i % cols);
+    out[i] = in[i] * drop_mult1(drop, r, c);
+  }
+}
+// out[o*inner + i] = x[o*inner + i] + y[i]   (broadcast add: PositionEmbs, src/model.py:17)
+__global__ void add_bcast_kernel(const float* __restrict__ x, const float* __restrict__ y, float* __restrict__ out,
+                                 long outer, long inner) {
+  const long total = outer * inner;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x)
+    out[i] = x[i] + y[i % inner];
+}
+}  // namespace
+
+extern "C" int vit_gelu_bwd_f32(const float* u, const float* dy, float* dx, int64_t n, vit_stream_t stream) {
+  VIT_CHECK_ARG(u && dy && dx && n >= 0, "vit_gelu_bwd_f32: bad args");
+  if (n == 0) return VIT_OK;
+  hipLaunchKernelGGL(gelu_bwd_f32_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, u, dy, dx, (long)n);
+  VIT_LAUNCH_CHECK("vit_gelu_bwd_f32");
+}
+
+extern "C" int vit_dropout_apply_f32(const vit_dropout* d, const float* in, float* out, int64_t rows, int64_t cols,
+                                     vit_stream_t stream) {
+  VIT_CHECK_ARG(in && out && rows >= 0 && cols > 0, "vit_dropout_apply_f32: bad args");
+  if (rows == 0) return VIT_OK;
+  hipLaunchKernelGGL(dropout_apply_kernel, dim3(grid_for(rows * cols)), dim3(256), 0, (hipStream_t)stream,
+                     make_drop(d), in, out, (long)rows, (int)cols);
+  VIT_LAUNCH_CHECK("vit_dropout_apply_f32");
+}
+
+extern "C" int vit_add_bcast_f32(const float* x, const float* y, float* out, int64_t outer, int64_t inner,
+                                 vit_stream_t stream) {
+  VIT_CHECK_ARG(x && y && out && outer >= 0 && inner > 0, "vit_add_bcast_f32: bad args");
+  if (outer == 0) return VIT_OK;
+  hipLaunchKernelGGL(add_bcast_kernel, dim3(grid_for(outer * inner)), dim3(256), 0, (hipStream_t)stream, x, y, out,
+                     (long)outer, (long)inner);
+  VIT_LAUNCH_CHECK("vit_add_bcast_f32");
+}
+
+namespace {
+__global__ void unpack_bf16_f32_kernel(const bf16_t* __restrict__ in, long ldi, long rows, int cols,
+                                       float* __restrict__ out, long ldo) {
+  const long total = rows * cols;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const long r = i / cols;
+    const int c = (int)(i % cols);
+    out[r * ldo + c] = bf2f(in[r * ldi + c]);
+  }
+}
+}  // namespace
+
+extern "C" int vit_unpack_bf16_f32(const void* in, int64_t ldi, int64_t rows, int64_t cols, float* out, int64_t ldo,
+                                   vit_stream_t stream) {
+  VIT_CHECK_ARG(in && out && rows >= 0 && cols > 0 && ldi >= cols && ldo >= cols, "vit_unpack_bf16_f32: bad args");
+  if (rows == 0) return VIT_OK;
+  hipLaunchKernelGGL(unpack_bf16_f32_kernel, dim3(grid_for(rows * cols)), dim3(256), 0, (hipStream_t)stream,
+                     (const bf16_t*)in, (long)ldi, (long)rows, (int)cols, out, (long)ldo);
+  VIT_LAUNCH_CHECK("vit_unpack_bf16_f32");
+}

@@ -87,6 +87,10 @@ _SIGS = {
     "vit_embed_fwd_f32": (c_i32, [c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp]),
     "vit_gelu_f32": (c_i32, [c_vp, c_vp, c_i64, c_vp]),
     "vit_attention_fwd_f32": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_f32, c_vp]),
+    "vit_gelu_bwd_f32": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_vp]),
+    "vit_dropout_apply_f32": (c_i32, [ctypes.POINTER(Dropout), c_vp, c_vp, c_i64, c_i64, c_vp]),
+    "vit_add_bcast_f32": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_i64, c_vp]),
+    "vit_unpack_bf16_f32": (c_i32, [c_vp, c_i64, c_i64, c_i64, c_vp, c_i64, c_vp]),
 }
 
 EXPORTED = tuple(_SIGS)

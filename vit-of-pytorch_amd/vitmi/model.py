@@ -6,29 +6,57 @@ interoperate with the reference's checkpoints (src/train.py:69-81, src/checkpoin
 seeded construction draws bit-identical initial weights.
 
 `VisionTransformer.forward` runs the whole network (patch embedding, encoder, head) as one
-autograd node whose forward and backward are the hand-written gfx950 kernels of
-libvit_hip.so (vitmi.engine). There is no CPU or PyTorch-op fallback: the model must live on a
-ROCm GPU. The sub-modules (Encoder, EncoderBlock, SelfAttention, MlpBlock, LinearGeneral,
-PositionEmbs) exist for the parameter tree and state_dict; only the whole-model forward is
-on the accelerated path.
+autograd node whose forward and backward are the hand-written gfx950 kernels of libvit_hip.so
+(vitmi.engine). The sub-modules (Encoder, EncoderBlock, SelfAttention, MlpBlock, LinearGeneral,
+PositionEmbs) and the torch.nn leaves inside them (Linear, LayerNorm, GELU, Dropout: vitmi
+subclasses with identical constructors and parameters) can also be called on their own, as in the
+reference: their forwards are written like the reference's and run, forward and backward, on the
+same kernels through vitmi.functional. There is no CPU or PyTorch-op fallback: the model must live
+on a ROCm GPU.
 """
 from __future__ import annotations
 
 import torch
 import torch.nn as nn
 
+from . import functional as HF
 from .engine import ArchConfig, ViTEngine
 
 __all__ = ["PositionEmbs", "MlpBlock", "MLPBlock", "LinearGeneral", "SelfAttention", "EncoderBlock", "Encoder",
-           "VisionTransformer", "CrossEntropyLoss"]
+           "VisionTransformer", "CrossEntropyLoss", "Linear", "LayerNorm", "GELU", "Dropout"]
 
 
-def _submodule_forward(name):
-    def forward(self, *args, **kwargs):
-        raise NotImplementedError(
-            f"{name}.forward on its own is not on the MI355X path; run the whole VisionTransformer "
-            "(the encoder executes as one fused HIP engine)")
-    return forward
+# ---- torch.nn leaves on the HIP kernels (same constructors, parameters and RNG draws) --------------
+class Linear(nn.Linear):
+    """nn.Linear (src/model.py:31-32,194) with its forward on the bf16 MFMA GEMM."""
+
+    def forward(self, x):
+        return HF.linear(x, self.weight, self.bias)
+
+
+class LayerNorm(nn.LayerNorm):
+    """nn.LayerNorm (src/model.py:108,114,146) with its forward on the HIP LayerNorm kernels."""
+
+    def forward(self, x):
+        if tuple(self.normalized_shape) != (x.shape[-1],):
+            raise NotImplementedError("vitmi LayerNorm normalizes the last dim (the reference's use)")
+        return HF.layer_norm(x, self.weight, self.bias, self.eps)
+
+
+class GELU(nn.GELU):
+    """nn.GELU() exact erf (src/model.py:33)."""
+
+    def forward(self, x):
+        if self.approximate != "none":
+            raise NotImplementedError("vitmi GELU is the exact-erf form (the reference's default)")
+        return HF.gelu(x)
+
+
+class Dropout(nn.Dropout):
+    """nn.Dropout (src/model.py:19-20,46-51,124-125) with a counter-based Philox mask on the device."""
+
+    def forward(self, x):
+        return HF.dropout(x, self.p, self.training)
 
 
 class PositionEmbs(nn.Module):
@@ -37,9 +65,13 @@ class PositionEmbs(nn.Module):
     def __init__(self, num_patches, emb_dim, dropout_rate=0.1):
         super().__init__()
         self.pos_embedding = nn.Parameter(torch.randn(1, num_patches + 1, emb_dim))
-        self.dropout = nn.Dropout(dropout_rate) if dropout_rate > 0 else None
+        self.dropout = Dropout(dropout_rate) if dropout_rate > 0 else None
 
-    forward = _submodule_forward("PositionEmbs")
+    def forward(self, x):
+        out = HF.add(x, self.pos_embedding)
+        if self.dropout:
+            out = self.dropout(out)
+        return out
 
 
 class MlpBlock(nn.Module):
@@ -47,17 +79,25 @@ class MlpBlock(nn.Module):
 
     def __init__(self, in_dim, mlp_dim, out_dim, dropout_rate=0.1):
         super().__init__()
-        self.fc1 = nn.Linear(in_dim, mlp_dim)
-        self.fc2 = nn.Linear(mlp_dim, out_dim)
-        self.act = nn.GELU()
+        self.fc1 = Linear(in_dim, mlp_dim)
+        self.fc2 = Linear(mlp_dim, out_dim)
+        self.act = GELU()
         if dropout_rate > 0.0:
-            self.dropout1 = nn.Dropout(dropout_rate)
-            self.dropout2 = nn.Dropout(dropout_rate)
+            self.dropout1 = Dropout(dropout_rate)
+            self.dropout2 = Dropout(dropout_rate)
         else:
             self.dropout1 = None
             self.dropout2 = None
 
-    forward = _submodule_forward("MlpBlock")
+    def forward(self, x):
+        out = self.fc1(x)
+        out = self.act(out)
+        if self.dropout1:
+            out = self.dropout1(out)
+        out = self.fc2(out)
+        if self.dropout2:
+            out = self.dropout2(out)
+        return out
 
 
 MLPBlock = MlpBlock  # the reference README calls it MLPBlock (README.md:35)
@@ -71,7 +111,8 @@ class LinearGeneral(nn.Module):
         self.weight = nn.Parameter(torch.randn(*in_dim, *feat_dim))
         self.bias = nn.Parameter(torch.zeros(*feat_dim))
 
-    forward = _submodule_forward("LinearGeneral")
+    def forward(self, x, dims):
+        return HF.linear_general(x, self.weight, self.bias, dims)
 
 
 class SelfAttention(nn.Module):
@@ -87,9 +128,14 @@ class SelfAttention(nn.Module):
         self.value = LinearGeneral((in_dim,), (self.heads, self.head_dim))
         self.out = LinearGeneral((self.heads, self.head_dim), (in_dim,))
         # built but never applied by the reference forward (src/model.py:78-81 vs :83-101)
-        self.dropout = nn.Dropout(dropout_rate) if dropout_rate > 0 else None
+        self.dropout = Dropout(dropout_rate) if dropout_rate > 0 else None
 
-    forward = _submodule_forward("SelfAttention")
+    def forward(self, x):
+        q = self.query(x, dims=([2], [0]))
+        k = self.key(x, dims=([2], [0]))
+        v = self.value(x, dims=([2], [0]))
+        out = HF.attention(q, k, v)  # (q k^T) / sqrt(hd), softmax, @ v (src/model.py:90-97)
+        return self.out(out, dims=([2, 3], [0, 1]))
 
 
 class EncoderBlock(nn.Module):
@@ -97,13 +143,23 @@ class EncoderBlock(nn.Module):
 
     def __init__(self, in_dim, mlp_dim, num_heads, dropout_rate=0.1, attn_dropout_rate=0.1):
         super().__init__()
-        self.norm1 = nn.LayerNorm(in_dim)
+        self.norm1 = LayerNorm(in_dim)
         self.attn = SelfAttention(in_dim, heads=num_heads, dropout_rate=attn_dropout_rate)
-        self.dropout = nn.Dropout(dropout_rate) if dropout_rate > 0 else None
-        self.norm2 = nn.LayerNorm(in_dim)
+        self.dropout = Dropout(dropout_rate) if dropout_rate > 0 else None
+        self.norm2 = LayerNorm(in_dim)
         self.mlp = MlpBlock(in_dim, mlp_dim, in_dim, dropout_rate)
 
-    forward = _submodule_forward("EncoderBlock")
+    def forward(self, x):
+        residual = x
+        out = self.norm1(x)
+        out = self.attn(out)
+        if self.dropout:
+            out = self.dropout(out)
+        out = HF.add(out, residual)
+        residual = out
+        out = self.norm2(out)
+        out = self.mlp(out)
+        return HF.add(out, residual)
 
 
 class Encoder(nn.Module):
@@ -116,9 +172,13 @@ class Encoder(nn.Module):
         self.encoder_layers = nn.ModuleList()
         for _ in range(num_layers):
             self.encoder_layers.append(EncoderBlock(emb_dim, mlp_dim, num_heads, dropout_rate, attn_dropout_rate))
-        self.norm = nn.LayerNorm(emb_dim)
+        self.norm = LayerNorm(emb_dim)
 
-    forward = _submodule_forward("Encoder")
+    def forward(self, x):
+        out = self.pos_embedding(x)
+        for layer in self.encoder_layers:
+            out = layer(out)
+        return self.norm(out)
 
 
 class _ViTFunction(torch.autograd.Function):
@@ -171,7 +231,7 @@ class VisionTransformer(nn.Module):
         self.transformer = Encoder(num_patches=num_patches, emb_dim=emb_dim, mlp_dim=mlp_dim, num_layers=num_layers,
                                    num_heads=num_heads, dropout_rate=dropout_rate,
                                    attn_dropout_rate=attn_dropout_rate)
-        self.classifier = nn.Linear(emb_dim, num_classes)
+        self.classifier = Linear(emb_dim, num_classes)
         self.arch = ArchConfig(image_size=h, patch_size=fh, emb_dim=emb_dim, mlp_dim=mlp_dim, num_heads=num_heads,
                                num_layers=num_layers, num_classes=num_classes)
         self.dropout_rate = dropout_rate

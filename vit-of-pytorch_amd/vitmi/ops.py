@@ -256,3 +256,23 @@ def attention_fwd_f32(qkv, o, B, N, H, hd, inv_sqrt_hd):
     _chk(qkv, F32, "qkv")
     _chk(o, F32, "o")
     check(lib().vit_attention_fwd_f32(_p(qkv), _p(o), B, N, H, hd, inv_sqrt_hd, _stream()), "vit_attention_fwd_f32")
+
+
+# ---- standalone sub-module path -----------------------------------------------------------------
+def gelu_bwd_f32(u, dy, dx, n):
+    check(lib().vit_gelu_bwd_f32(_p(u), _p(dy), _p(dx), n, _stream()), "vit_gelu_bwd_f32")
+
+
+def dropout_apply_f32(d, inp, out, rows, cols):
+    check(lib().vit_dropout_apply_f32(_dp(d), _p(inp), _p(out), rows, cols, _stream()), "vit_dropout_apply_f32")
+
+
+def add_bcast_f32(x, y, out, outer, inner):
+    check(lib().vit_add_bcast_f32(_p(x), _p(y), _p(out), outer, inner, _stream()), "vit_add_bcast_f32")
+
+
+def unpack_bf16_f32(inp, ldi, rows, cols, out, ldo):
+    """out[r*ldo + c] = f32(inp[r*ldi + c])"""
+    _chk(inp, BF16, "inp")
+    _chk(out, F32, "out")
+    check(lib().vit_unpack_bf16_f32(_p(inp), ldi, rows, cols, _p(out), ldo, _stream()), "vit_unpack_bf16_f32")
