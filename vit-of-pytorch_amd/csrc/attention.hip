@@ -102,6 +102,624 @@ __global__ void __launch_bounds__(NW * 64) attn_fwd_kernel(const bf16_t* __restr
 }
 
 // ------------------------------------------------------------------------------------------------
+// Forward, lean form: one (image, head) per workgroup, keys padded to whole 16-row tiles only (an odd
+// last tile takes v_mfma_f32_16x16x16_bf16 in P V), so B/16's 197 tokens need 2 x 208 x 64 x 2 B =
+// 53 KB of LDS and three workgroups share a CU. Per 16-query strip and lane: S^T = K Q^T accumulators
+// (keys 4g + r of every tile, query i), masking only on the last tile, max via max3, p = exp2(s c - m c)
+// (one fma + one v_exp), bf16 packing of the accumulators as the P^T operand. LDS addresses are
+// per-lane bases + immediates (ImgLane), so the inner loops carry no address arithmetic.
+template <int HD, int NP, int NT>
+__device__ __forceinline__ void load_images_lds(lds_t* imgA, const bf16_t* srcA, long strideA, lds_t* imgB,
+                                                const bf16_t* srcB, long strideB, int N, int hd) {
+  constexpr int CPR = HD / 8;
+  constexpr int TOTAL = NP * CPR;
+  constexpr int PER = (TOTAL + NT - 1) / NT;
+  const __amdgpu_buffer_rsrc_t ra = make_rsrc(srcA, (uint32_t)(((long)(N - 1) * strideA + hd) * 2));
+  const __amdgpu_buffer_rsrc_t rb = make_rsrc(srcB, (uint32_t)(((long)(N - 1) * strideB + hd) * 2));
+  v4u a[PER], b[PER];
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const int c = threadIdx.x + k * NT;
+    const int row = c / CPR, ch = c % CPR;
+    const bool ok = c < TOTAL && row < N && ch * 8 < hd;
+    const int offa = ok ? (int)(((long)row * strideA + ch * 8) * 2) : 0x7ffffff0;
+    const int offb = ok ? (int)(((long)row * strideB + ch * 8) * 2) : 0x7ffffff0;
+    a[k] = __builtin_amdgcn_raw_buffer_load_b128(ra, offa, 0, 0);
+    b[k] = __builtin_amdgcn_raw_buffer_load_b128(rb, offb, 0, 0);
+  }
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const int c = threadIdx.x + k * NT;
+    if (TOTAL % NT == 0 || c < TOTAL) {
+      const int row = c / CPR, ch = c % CPR;
+      lds_st(imgA + img_off<HD>(row, ch), a[k]);
+      lds_st(imgB + img_off<HD>(row, ch), b[k]);
+    }
+  }
+}
+
+template <int HD, int NKT, int NW>
+__global__ void __launch_bounds__(NW * 64, NW == 8 ? 2 : 3) attn_fwd2_kernel(const bf16_t* __restrict__ qkv,
+                                                               bf16_t* __restrict__ o, float* __restrict__ lse,
+                                                               int N, int H, int hd, float scale, int nq, int diag) {
+  constexpr int NP = NKT * 16;
+  constexpr int IMG = NP * HD * 2;
+  constexpr int T = ImgLane<HD>::TILE;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  lds_t* Ki = (lds_t*)smem;
+  lds_t* Vi = Ki + IMG;
+  const int bh = blockIdx.x, b = bh / H, h = bh % H;
+  const int D = H * hd;
+  const long rs = 3L * D;
+  const bf16_t* base = qkv + (long)b * N * rs + (long)h * hd;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int g = lane >> 4, i = lane & 15;
+  const ImgLane<HD> L(lane);
+  if (!(diag & 1)) load_images_lds<HD, NP, NW * 64>(Ki, base + D, rs, Vi, base + 2 * D, rs, N, hd);
+  const float c = scale * LOG2E;
+  const int nqa = min(N, (nq + 31) / 32 * 32);  // whole 32-row pairs (the backward's stage 2 reads their lse)
+  const int nqt = (nqa + 15) / 16;
+  // every Q fragment of this wave's strips is requested up front, beside the K / V image loads: one HBM
+  // latency per workgroup instead of one per strip
+  constexpr int MAXS = (NKT + NW - 1) / NW;
+  v8bf qa[MAXS][HD / 32];
+#pragma unroll
+  for (int u = 0; u < MAXS; ++u)
+#pragma unroll
+    for (int kk = 0; kk < HD / 32; ++kk) qa[u][kk] = gl_row<HD>(base, rs, (wave + u * NW) * 16, kk, N, hd, lane);
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < MAXS; ++u) {
+    const int qt = wave + u * NW;
+    if (qt >= nqt) break;
+    const v8bf* qf = qa[u];
+    v4f s[NKT];
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt) {
+      s[kt] = v4f{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < HD / 32; ++kk)
+        s[kt] = mfma(__builtin_bit_cast(v8bf, lds_ld<v8s>(Ki + kt * T + L.row[kk])), qf[kk], s[kt]);
+    }
+    if (N < NP) {  // only the last tile holds padded keys
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if ((NKT - 1) * 16 + 4 * g + r >= N) s[NKT - 1][r] = -INFINITY;
+    }
+    // row max: two v_max3 per tile (max(mx, a, b))
+    float mx = max3f(s[0][0], s[0][1], s[0][2]);
+    mx = fmaxf(mx, s[0][3]);
+#pragma unroll
+    for (int kt = 1; kt < NKT; ++kt) {
+      mx = max3f(mx, s[kt][0], s[kt][1]);
+      mx = max3f(mx, s[kt][2], s[kt][3]);
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float mc = mx * c;
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) s[kt][r] = ex2(fmaf(s[kt][r], c, -mc));
+    // P V and the row sums of the bf16 P it uses: an all-ones A operand sums P^T over the keys on the
+    // matrix core (every row of lsum holds the query's sum), replacing a VALU add per score
+    const v8bf ones8 = __builtin_bit_cast(v8bf, v8s{0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80});
+    v4f acc[HD / 16], lsum = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int dt = 0; dt < HD / 16; ++dt) acc[dt] = v4f{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < NKT / 2; ++ks) {
+      const v8bf pp = pack8(s[2 * ks], s[2 * ks + 1]);
+      lsum = mfma(ones8, pp, lsum);
+#pragma unroll
+      for (int dt = 0; dt < HD / 16; ++dt) {
+        v8s vt;
+        vt.lo = lds_tr(Vi + 2 * ks * T + L.tr[dt]);
+        vt.hi = lds_tr(Vi + (2 * ks + 1) * T + L.tr[dt]);
+        acc[dt] = mfma(__builtin_bit_cast(v8bf, vt), pp, acc[dt]);
+      }
+    }
+    if constexpr (NKT % 2 == 1) {
+      const v4s pp = pack4(s[NKT - 1]);
+      lsum = mfma16(v4s{0x3F80, 0x3F80, 0x3F80, 0x3F80}, pp, lsum);
+#pragma unroll
+      for (int dt = 0; dt < HD / 16; ++dt) acc[dt] = mfma16(lds_tr(Vi + (NKT - 1) * T + L.tr[dt]), pp, acc[dt]);
+    }
+    const float l = lsum[0];
+    const int q = qt * 16 + i;
+    if (g == 0 && q < N && !(diag & 2)) lse[(long)bh * N + q] = mx * scale + logf(l);
+    const float inv_l = 1.0f / l;
+    if (!(diag & 2)) {  // whole 2*hd-byte rows through the wave's LDS strip (StripOut)
+      lds_t* so = Vi + IMG + wave * StripOut<HD>::BYTES;
+      StripOut<HD>::stage(so, acc, inv_l, lane);
+      StripOut<HD>::store(so, o + ((long)b * N + qt * 16) * D + (long)h * hd, D, N - qt * 16, hd, lane);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Forward, persistent form: one workgroup of 8 waves per CU walks (image, head) items with stride
+// gridDim.x; the next item's K / V rows (register-staged, 4 + 4 x 16 B per thread) and Q fragments are
+// requested before the current item's MFMAs and land in the second LDS image pair after them, so the
+// HBM stream never waits for a workgroup's compute phase (the one-shot kernel above loads, then
+// computes, and ran at 3.5 TB/s). One barrier per item.
+template <int HD, int NKT>
+struct KVStage {
+  static constexpr int NP = NKT * 16, CPR = HD / 8, TOTAL = NP * CPR, NT = 512;
+  static constexpr int PER = (TOTAL + NT - 1) / NT;
+  v4u a[PER], b[PER];
+  __device__ __forceinline__ void issue(const bf16_t* src, long rs, int D, int N, int hd) {
+    const __amdgpu_buffer_rsrc_t rk = make_rsrc(src + D, (uint32_t)(((long)(N - 1) * rs + hd) * 2));
+    const __amdgpu_buffer_rsrc_t rv = make_rsrc(src + 2 * D, (uint32_t)(((long)(N - 1) * rs + hd) * 2));
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const int c = threadIdx.x + k * NT;
+      const int row = c / CPR, ch = c % CPR;
+      const bool ok = c < TOTAL && row < N && ch * 8 < hd;
+      const int off = ok ? (int)(((long)row * rs + ch * 8) * 2) : 0x7ffffff0;
+      a[k] = __builtin_amdgcn_raw_buffer_load_b128(rk, off, 0, 0);
+      b[k] = __builtin_amdgcn_raw_buffer_load_b128(rv, off, 0, 0);
+    }
+  }
+  __device__ __forceinline__ void write(lds_t* K, lds_t* V) const {
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const int c = threadIdx.x + k * NT;
+      if (TOTAL % NT == 0 || c < TOTAL) {
+        const int row = c / CPR, ch = c % CPR;
+        lds_st(K + img_off<HD>(row, ch), a[k]);
+        lds_st(V + img_off<HD>(row, ch), b[k]);
+      }
+    }
+  }
+};
+
+template <int HD, int NKT>
+__global__ void __launch_bounds__(512, 1) attn_fwd_p_kernel(const bf16_t* __restrict__ qkv, bf16_t* __restrict__ o,
+                                                            float* __restrict__ lse, int BH, int N, int H, int hd,
+                                                            float scale, int nq, int diag) {
+  constexpr int NW = 8;
+  constexpr int NP = NKT * 16;
+  constexpr int IMG = NP * HD * 2;
+  constexpr int T = ImgLane<HD>::TILE;
+  constexpr int MAXS = (NKT + NW - 1) / NW;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  lds_t* const L0 = (lds_t*)smem;  // [2 buffers][K image, V image]
+  const int D = H * (int)hd;
+  const long rs = 3L * D;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int g = lane >> 4, i = lane & 15;
+  const ImgLane<HD> L(lane);
+  const float c = scale * LOG2E;
+  const int nqa = min(N, (nq + 31) / 32 * 32);
+  const int nqt = (nqa + 15) / 16;
+  auto item_base = [&](int it) { return qkv + (long)(it / H) * N * rs + (long)(it % H) * hd; };
+
+  KVStage<HD, NKT> st;
+  v8bf qa[MAXS][HD / 32], qn[MAXS][HD / 32];
+  int it = blockIdx.x;
+  {
+    const bf16_t* base = item_base(it);
+    st.issue(base, rs, D, N, hd);
+#pragma unroll
+    for (int u = 0; u < MAXS; ++u)
+#pragma unroll
+      for (int kk = 0; kk < HD / 32; ++kk) qa[u][kk] = gl_row<HD>(base, rs, (wave + u * NW) * 16, kk, N, hd, lane);
+    st.write(L0, L0 + IMG);
+  }
+  __syncthreads();
+  int cur = 0;
+  for (; it < BH; it += gridDim.x) {
+    const int nx = it + gridDim.x;
+    if (nx < BH && !(diag & 1)) {  // diag bit 0 (timing only): keep the first item's operands
+      const bf16_t* nb = item_base(nx);
+      st.issue(nb, rs, D, N, hd);
+#pragma unroll
+      for (int u = 0; u < MAXS; ++u)
+#pragma unroll
+        for (int kk = 0; kk < HD / 32; ++kk) qn[u][kk] = gl_row<HD>(nb, rs, (wave + u * NW) * 16, kk, N, hd, lane);
+    }
+    const lds_t* Ki = L0 + cur * 2 * IMG;
+    const lds_t* Vi = Ki + IMG;
+    const int b = it / H, h = it % H;
+#pragma unroll
+    for (int u = 0; u < MAXS; ++u) {
+      const int qt = wave + u * NW;
+      if (qt < nqt) {
+        v4f s[NKT];
+#pragma unroll
+        for (int kt = 0; kt < NKT; ++kt) {
+          s[kt] = v4f{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int kk = 0; kk < HD / 32; ++kk)
+            s[kt] = mfma(__builtin_bit_cast(v8bf, lds_ld<v8s>(Ki + kt * T + L.row[kk])), qa[u][kk], s[kt]);
+        }
+        if (N < NP) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if ((NKT - 1) * 16 + 4 * g + r >= N) s[NKT - 1][r] = -INFINITY;
+        }
+        float mx = fmaxf(fmaxf(s[0][0], s[0][1]), fmaxf(s[0][2], s[0][3]));
+#pragma unroll
+        for (int kt = 1; kt < NKT; ++kt) mx = fmaxf(fmaxf(mx, fmaxf(s[kt][0], s[kt][1])), fmaxf(s[kt][2], s[kt][3]));
+        mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+        const float mc = mx * c;
+        float l = 0.f;
+#pragma unroll
+        for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float p = ex2(fmaf(s[kt][r], c, -mc));
+            s[kt][r] = p;
+            l += p;
+          }
+        l += __shfl_xor(l, 16, 64);
+        l += __shfl_xor(l, 32, 64);
+        const int q = qt * 16 + i;
+        if (g == 0 && q < N) lse[(long)it * N + q] = mx * scale + logf(l);
+        const float inv_l = 1.0f / l;
+        v4f acc[HD / 16];
+#pragma unroll
+        for (int dt = 0; dt < HD / 16; ++dt) acc[dt] = v4f{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < NKT / 2; ++ks) {
+          const v8bf pp = pack8(s[2 * ks], s[2 * ks + 1]);
+#pragma unroll
+          for (int dt = 0; dt < HD / 16; ++dt) {
+            v8s vt;
+            vt.lo = lds_tr(Vi + 2 * ks * T + L.tr[dt]);
+            vt.hi = lds_tr(Vi + (2 * ks + 1) * T + L.tr[dt]);
+            acc[dt] = mfma(__builtin_bit_cast(v8bf, vt), pp, acc[dt]);
+          }
+        }
+        if constexpr (NKT % 2 == 1) {
+          const v4s pp = pack4(s[NKT - 1]);
+#pragma unroll
+          for (int dt = 0; dt < HD / 16; ++dt) acc[dt] = mfma16(lds_tr(Vi + (NKT - 1) * T + L.tr[dt]), pp, acc[dt]);
+        }
+        {
+          lds_t* so = L0 + 4 * IMG + wave * StripOut<HD>::BYTES;
+          StripOut<HD>::stage(so, acc, inv_l, lane);
+          StripOut<HD>::store(so, o + ((long)b * N + qt * 16) * D + (long)h * hd, D, N - qt * 16, hd, lane);
+        }
+      }
+    }
+    if (nx < BH && !(diag & 1)) {
+      st.write(L0 + (cur ^ 1) * 2 * IMG, L0 + (cur ^ 1) * 2 * IMG + IMG);
+#pragma unroll
+      for (int u = 0; u < MAXS; ++u)
+#pragma unroll
+        for (int kk = 0; kk < HD / 32; ++kk) qa[u][kk] = qn[u][kk];
+    }
+    __syncthreads();
+    if (!(diag & 1)) cur ^= 1;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Backward, lean two-kernel form (HD <= 64). Each kernel has ONE load phase: its two LDS images and
+// every register fragment its waves will use are requested together at the start.
+//   bwd_dq    (K, V images): per 16-query strip, S^T / dP^T of all keys stay in registers, delta =
+//             sum_j P dP (exact; see the round-1 kernel below), dS = P (dP - delta), dQ^T = K^T dS^T.
+//             Writes dQ and delta (f32 [B, H, N], the workspace) for the second kernel.
+//   bwd_dkdv  (Q, dO images + lse, delta): per pair of 16-key tiles and 32-query pair, S and dP with
+//             the key on the lane, P / dS packed as the B operands of dV^T = dO^T P, dK^T = Q^T dS.
+// Keys and queries are padded to whole 16-row tiles only; an odd last tile takes the 16x16x16 MFMA.
+template <int HD, int NKT, int NW>
+__global__ void __launch_bounds__(NW * 64, 2) attn_bwd_dq_kernel(const bf16_t* __restrict__ qkv,
+                                                                 const bf16_t* __restrict__ dout,
+                                                                 const float* __restrict__ lse,
+                                                                 bf16_t* __restrict__ dqkv, float* __restrict__ delta,
+                                                                 float* __restrict__ bias_partial, int N, int H,
+                                                                 int hd, float scale, int nq) {
+  constexpr int NP = NKT * 16;
+  constexpr int IMG = NP * HD * 2;
+  constexpr int T = ImgLane<HD>::TILE;
+  constexpr int MAXS = (NKT + NW - 1) / NW;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  lds_t* Ki = (lds_t*)smem;
+  lds_t* Vi = Ki + IMG;
+  float* bsum = reinterpret_cast<float*>(smem + 2 * IMG);  // [NW][HD]
+  const int bh = blockIdx.x, b = bh / H, h = bh % H;
+  const int D = H * hd;
+  const long rs = 3L * D;
+  const bf16_t* base = qkv + (long)b * N * rs + (long)h * hd;
+  const bf16_t* dob = dout + (long)b * N * D + (long)h * hd;
+  bf16_t* dq_base = dqkv + (long)b * N * rs + (long)h * hd;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int g = lane >> 4, i = lane & 15;
+  const ImgLane<HD> L(lane);
+  const float c = scale * LOG2E;
+  const int nqa = min(N, (nq + 31) / 32 * 32);
+  const int nqt = (nqa + 15) / 16;
+  load_images_lds<HD, NP, NW * 64>(Ki, base + D, rs, Vi, base + 2 * D, rs, N, hd);
+  v8bf qa[MAXS][HD / 32], da[MAXS][HD / 32];
+  float lsa[MAXS];
+#pragma unroll
+  for (int u = 0; u < MAXS; ++u) {
+    const int r0 = (wave + u * NW) * 16;
+#pragma unroll
+    for (int kk = 0; kk < HD / 32; ++kk) {
+      qa[u][kk] = gl_row<HD>(base, rs, r0, kk, N, hd, lane);
+      da[u][kk] = gl_row<HD>(dob, D, r0, kk, N, hd, lane);
+    }
+    const int q = r0 + i;
+    lsa[u] = q < N ? lse[(long)bh * N + q] * LOG2E : INFINITY;  // padded queries: P = 2^-inf = 0
+  }
+  __syncthreads();
+  float bq[HD / 16][4];
+#pragma unroll
+  for (int dt = 0; dt < HD / 16; ++dt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bq[dt][r] = 0.f;
+#pragma unroll
+  for (int u = 0; u < MAXS; ++u) {
+    const int qt = wave + u * NW;
+    if (qt * 16 >= N) break;
+    const int q = qt * 16 + i;
+    if (qt >= nqt) {  // no gradient reaches these queries (pruned last layer): dQ = 0, delta = 0
+      if (q < N) {
+        if (g == 0) delta[(long)bh * N + q] = 0.f;
+#pragma unroll
+        for (int dt = 0; dt < HD / 16; ++dt) {
+          const int d = dt * 16 + 4 * g;
+          if (d < hd) store4(dq_base + (long)q * rs + d, v4f{0.f, 0.f, 0.f, 0.f}, 1.f);
+        }
+      }
+      continue;
+    }
+    const float ls = lsa[u];
+    v4f P[NKT], DP[NKT];
+    float dl = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt) {
+      v4f st = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < HD / 32; ++kk) {
+        st = mfma(__builtin_bit_cast(v8bf, lds_ld<v8s>(Ki + kt * T + L.row[kk])), qa[u][kk], st);
+        dp = mfma(__builtin_bit_cast(v8bf, lds_ld<v8s>(Vi + kt * T + L.row[kk])), da[u][kk], dp);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) P[kt][r] = ex2(fmaf(st[r], c, -ls));
+      if (kt == NKT - 1 && N < NP) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if ((NKT - 1) * 16 + 4 * g + r >= N) P[kt][r] = 0.f;
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) dl = fmaf(P[kt][r], dp[r], dl);
+      DP[kt] = dp;
+    }
+    dl += __shfl_xor(dl, 16, 64);
+    dl += __shfl_xor(dl, 32, 64);
+    if (q >= N) dl = 0.f;
+    if (g == 0 && q < N) delta[(long)bh * N + q] = dl;
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) P[kt][r] *= DP[kt][r] - dl;  // dS
+    v4f dq[HD / 16];
+#pragma unroll
+    for (int dt = 0; dt < HD / 16; ++dt) dq[dt] = v4f{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < NKT / 2; ++ks) {
+      const v8bf dd = pack8(P[2 * ks], P[2 * ks + 1]);
+#pragma unroll
+      for (int dt = 0; dt < HD / 16; ++dt) {
+        v8s kt8;
+        kt8.lo = lds_tr(Ki + 2 * ks * T + L.tr[dt]);
+        kt8.hi = lds_tr(Ki + (2 * ks + 1) * T + L.tr[dt]);
+        dq[dt] = mfma(__builtin_bit_cast(v8bf, kt8), dd, dq[dt]);
+      }
+    }
+    if constexpr (NKT % 2 == 1) {
+      const v4s dd = pack4(P[NKT - 1]);
+#pragma unroll
+      for (int dt = 0; dt < HD / 16; ++dt) dq[dt] = mfma16(lds_tr(Ki + (NKT - 1) * T + L.tr[dt]), dd, dq[dt]);
+    }
+    {
+      lds_t* so = (lds_t*)(smem + 2 * IMG + NW * HD * 4) + wave * StripOut<HD>::BYTES;
+      StripOut<HD>::stage(so, dq, scale, lane);
+      StripOut<HD>::store(so, dq_base + (long)qt * 16 * rs, rs, N - qt * 16, hd, lane);
+    }
+#pragma unroll
+    for (int dt = 0; dt < HD / 16; ++dt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) bq[dt][r] += dq[dt][r];  // padded queries: dS = 0
+  }
+  if (bias_partial) {
+#pragma unroll
+    for (int dt = 0; dt < HD / 16; ++dt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float v = sum16(bq[dt][r]);
+        if (i == 0) bsum[wave * HD + dt * 16 + 4 * g + r] = v * scale;
+      }
+    __syncthreads();
+    for (int d = threadIdx.x; d < hd; d += NW * 64) {
+      float acc = 0.f;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) acc += bsum[w * HD + d];
+      bias_partial[(long)b * 3 * D + h * hd + d] = acc;
+    }
+  }
+}
+
+template <int HD, int NKT, int NW>
+__global__ void __launch_bounds__(NW * 64, 2) attn_bwd_dkdv_kernel(const bf16_t* __restrict__ qkv,
+                                                                   const bf16_t* __restrict__ dout,
+                                                                   const float* __restrict__ lse,
+                                                                   const float* __restrict__ delta,
+                                                                   bf16_t* __restrict__ dqkv,
+                                                                   float* __restrict__ bias_partial, int N, int H,
+                                                                   int hd, float scale, int nq) {
+  constexpr int NP = NKT * 16;
+  constexpr int IMG = NP * HD * 2;
+  constexpr int T = ImgLane<HD>::TILE;
+  constexpr int NKP = (NKT + 1) / 2;               // key-tile pairs
+  constexpr int MAXP = (NKP + NW - 1) / NW;        // pairs per wave
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  lds_t* Qi = (lds_t*)smem;
+  lds_t* Oi = Qi + IMG;
+  float* lse_s = reinterpret_cast<float*>(smem + 2 * IMG);
+  float* dlt_s = lse_s + NP;
+  float* bsum = dlt_s + NP;  // [NW][2][HD]
+  const int bh = blockIdx.x, b = bh / H, h = bh % H;
+  const int D = H * hd;
+  const long rs = 3L * D;
+  const bf16_t* base = qkv + (long)b * N * rs + (long)h * hd;
+  const bf16_t* dob = dout + (long)b * N * D + (long)h * hd;
+  bf16_t* dk_base = dqkv + (long)b * N * rs + (long)h * hd + D;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int g = lane >> 4, i = lane & 15;
+  const ImgLane<HD> L(lane);
+  const float c = scale * LOG2E;
+  const int nqa = min(N, (nq + 31) / 32 * 32);
+  const int nqt = (nqa + 15) / 16;  // query tiles that carry a gradient (their lse / delta are valid)
+  load_images_lds<HD, NP, NW * 64>(Qi, base, rs, Oi, dob, D, N, hd);
+  v8bf ka[MAXP][2][HD / 32], va[MAXP][2][HD / 32];
+#pragma unroll
+  for (int u = 0; u < MAXP; ++u)
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int kk = 0; kk < HD / 32; ++kk) {
+        const int r0 = (2 * (wave + u * NW) + t) * 16;
+        ka[u][t][kk] = gl_row<HD>(base + D, rs, r0, kk, N, hd, lane);
+        va[u][t][kk] = gl_row<HD>(base + 2 * D, rs, r0, kk, N, hd, lane);
+      }
+  for (int r = threadIdx.x; r < NP; r += NW * 64) {
+    const bool ok = r < N && r < nqt * 16;
+    lse_s[r] = ok ? lse[(long)bh * N + r] * LOG2E : INFINITY;  // P = 0 on padded / gradient-free rows
+    dlt_s[r] = ok ? delta[(long)bh * N + r] : 0.f;
+  }
+  __syncthreads();
+  float bk[HD / 16][4], bv[HD / 16][4];
+#pragma unroll
+  for (int dt = 0; dt < HD / 16; ++dt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bk[dt][r] = bv[dt][r] = 0.f;
+  const int nqp = nqt / 2;            // whole query-tile pairs carrying a gradient
+  const bool qtail = (nqt & 1) != 0;  // and a single last tile
+#pragma unroll
+  for (int u = 0; u < MAXP; ++u) {
+    const int kp = wave + u * NW;
+    if (kp >= NKP) break;
+    const bool two = 2 * kp + 1 < NKT;  // the last pair of an odd tile count holds one key tile
+    v4f dv[2][HD / 16], dk[2][HD / 16];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int dt = 0; dt < HD / 16; ++dt) dv[t][dt] = dk[t][dt] = v4f{0.f, 0.f, 0.f, 0.f};
+    bool kval[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) kval[t] = (2 * kp + t) * 16 + i < N;
+    for (int qs = 0; qs < nqp + (qtail ? 1 : 0); ++qs) {
+      const bool full = qs < nqp;  // a query pair (else the single last tile)
+      v4f P[2][2], DS[2][2];       // [key tile t][query tile w]
+#pragma unroll
+      for (int w = 0; w < 2; ++w) {
+        if (w == 1 && !full) break;
+        const int qt = 2 * qs + w;
+        const v4f lq = *reinterpret_cast<const v4f*>(lse_s + qt * 16 + 4 * g);
+        const v4f dq4 = *reinterpret_cast<const v4f*>(dlt_s + qt * 16 + 4 * g);
+        v8bf qr[HD / 32], orr[HD / 32];
+#pragma unroll
+        for (int kk = 0; kk < HD / 32; ++kk) {
+          qr[kk] = __builtin_bit_cast(v8bf, lds_ld<v8s>(Qi + qt * T + L.row[kk]));
+          orr[kk] = __builtin_bit_cast(v8bf, lds_ld<v8s>(Oi + qt * T + L.row[kk]));
+        }
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          if (t == 1 && !two) break;
+          v4f sv = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int kk = 0; kk < HD / 32; ++kk) {
+            sv = mfma(qr[kk], ka[u][t][kk], sv);
+            dp = mfma(orr[kk], va[u][t][kk], dp);
+          }
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float p = kval[t] ? ex2(fmaf(sv[r], c, -lq[r])) : 0.f;
+            P[t][w][r] = p;
+            DS[t][w][r] = p * (dp[r] - dq4[r]);
+          }
+        }
+      }
+      if (full) {
+#pragma unroll
+        for (int dt = 0; dt < HD / 16; ++dt) {
+          v8s o8, q8;
+          o8.lo = lds_tr(Oi + 2 * qs * T + L.tr[dt]);
+          o8.hi = lds_tr(Oi + (2 * qs + 1) * T + L.tr[dt]);
+          q8.lo = lds_tr(Qi + 2 * qs * T + L.tr[dt]);
+          q8.hi = lds_tr(Qi + (2 * qs + 1) * T + L.tr[dt]);
+#pragma unroll
+          for (int t = 0; t < 2; ++t) {
+            if (t == 1 && !two) break;
+            dv[t][dt] = mfma(__builtin_bit_cast(v8bf, o8), pack8(P[t][0], P[t][1]), dv[t][dt]);
+            dk[t][dt] = mfma(__builtin_bit_cast(v8bf, q8), pack8(DS[t][0], DS[t][1]), dk[t][dt]);
+          }
+        }
+      } else {
+#pragma unroll
+        for (int dt = 0; dt < HD / 16; ++dt) {
+          const v4s o4 = lds_tr(Oi + 2 * qs * T + L.tr[dt]);
+          const v4s q4 = lds_tr(Qi + 2 * qs * T + L.tr[dt]);
+#pragma unroll
+          for (int t = 0; t < 2; ++t) {
+            if (t == 1 && !two) break;
+            dv[t][dt] = mfma16(o4, pack4(P[t][0]), dv[t][dt]);
+            dk[t][dt] = mfma16(q4, pack4(DS[t][0]), dk[t][dt]);
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      if (t == 1 && !two) break;
+      {
+        const int k0 = (2 * kp + t) * 16;
+        lds_t* so = (lds_t*)(bsum + NW * 2 * HD) + wave * StripOut<HD>::BYTES;
+        StripOut<HD>::stage(so, dk[t], scale, lane);
+        StripOut<HD>::store(so, dk_base + (long)k0 * rs, rs, N - k0, hd, lane);
+        StripOut<HD>::stage(so, dv[t], 1.0f, lane);
+        StripOut<HD>::store(so, dk_base + (long)k0 * rs + D, rs, N - k0, hd, lane);
+      }
+#pragma unroll
+      for (int dt = 0; dt < HD / 16; ++dt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {  // invalid keys hold exact zeros (P = 0)
+          bk[dt][r] += dk[t][dt][r];
+          bv[dt][r] += dv[t][dt][r];
+        }
+    }
+  }
+  if (bias_partial) {
+#pragma unroll
+    for (int dt = 0; dt < HD / 16; ++dt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float a = sum16(bk[dt][r]), v = sum16(bv[dt][r]);
+        if (i == 0) {
+          bsum[(wave * 2 + 0) * HD + dt * 16 + 4 * g + r] = a * scale;
+          bsum[(wave * 2 + 1) * HD + dt * 16 + 4 * g + r] = v;
+        }
+      }
+    __syncthreads();
+    for (int e = threadIdx.x; e < 2 * HD; e += NW * 64) {
+      const int z = e / HD, d = e % HD;
+      if (d >= hd) continue;
+      float acc = 0.f;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) acc += bsum[(w * 2 + z) * HD + d];
+      bias_partial[(long)b * 3 * D + (1 + z) * D + h * hd + d] = acc;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
 // Backward, two LDS images at a time (56 KB at N = 197, hd = 64: two workgroups per CU, so one
 // workgroup's image loads overlap the other's MFMA work).
 //   stage 1 (K, V images): each wave owns 16-query strips, Q / dO rows in registers (the next
@@ -527,9 +1145,68 @@ hipError_t launch_fwd_nw(const bf16_t* qkv, bf16_t* o, float* lse, int B, int N,
   return hipGetLastError();
 }
 
+template <int HD, int NKT16, int NW = 4>
+hipError_t launch_fwd2(const bf16_t* qkv, bf16_t* o, float* lse, int B, int N, int H, int hd, float scale, int nq,
+                       hipStream_t s) {
+  const size_t lds = (size_t)2 * NKT16 * 16 * HD * 2 + (size_t)NW * StripOut<HD>::BYTES;
+  auto kern = attn_fwd2_kernel<HD, NKT16, NW>;
+  if (lds > 64 * 1024) (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  static const int diag = [] {
+    const char* e = getenv("VIT_ATTN_DIAG");
+    return e ? atoi(e) : 0;
+  }();
+  hipLaunchKernelGGL(kern, dim3(B * H), dim3(NW * 64), lds, s, qkv, o, lse, N, H, hd, scale, nq, diag);
+  return hipGetLastError();
+}
+
+template <int HD, int NKT16>
+hipError_t launch_fwd_p(const bf16_t* qkv, bf16_t* o, float* lse, int B, int N, int H, int hd, float scale, int nq,
+                        hipStream_t s) {
+  const size_t lds = (size_t)4 * NKT16 * 16 * HD * 2 + (size_t)8 * StripOut<HD>::BYTES;
+  auto kern = attn_fwd_p_kernel<HD, NKT16>;
+  if (lds > 64 * 1024) (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  static const int ncu = [] {
+    int dev = 0, n = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+    return n > 0 ? n : 256;
+  }();
+  const int bh = B * H;
+  static const int diag = [] {
+    const char* e = getenv("VIT_ATTN_DIAG");
+    return e ? atoi(e) : 0;
+  }();
+  static const int grid_mul = [] {
+    const char* e = getenv("VIT_ATTN_FWD_GRID");  // workgroups per CU (diagnostics)
+    return e ? atoi(e) : 1;
+  }();
+  const int grid = ncu * grid_mul;
+  hipLaunchKernelGGL(kern, dim3(bh < grid ? bh : grid), dim3(512), lds, s, qkv, o, lse, bh, N, H, hd, scale, nq, diag);
+  return hipGetLastError();
+}
+
 template <int HD, int NKT>
 hipError_t launch_fwd(const bf16_t* qkv, bf16_t* o, float* lse, int B, int N, int H, int hd, float scale,
                       int nq, hipStream_t s) {
+  // VIT_ATTN_FWD_VARIANT (diagnostics): 0 persistent, 1 one-shot lean, 2 the round-1 kernel
+  static const int var = [] {
+    const char* e = getenv("VIT_ATTN_FWD_VARIANT");
+    return e ? atoi(e) : 0;
+  }();
+  const bool old = var == 2;
+  // persistent double-buffered form while two K/V image pairs fit the 160 KiB LDS
+  if (var == 0 && HD <= 64 && 4 * ((N + 15) / 16) * 16 * HD * 2 + 8 * StripOut<HD>::BYTES <= 160 * 1024) {
+    if ((N + 15) / 16 == NKT) return launch_fwd_p<HD, NKT>(qkv, o, lse, B, N, H, hd, scale, nq, s);
+    return launch_fwd_p<HD, NKT - 1>(qkv, o, lse, B, N, H, hd, scale, nq, s);
+  }
+  if (var == 3 && HD <= 64) {
+    if ((N + 15) / 16 == NKT) return launch_fwd2<HD, NKT, 8>(qkv, o, lse, B, N, H, hd, scale, nq, s);
+    return launch_fwd2<HD, NKT - 1, 8>(qkv, o, lse, B, N, H, hd, scale, nq, s);
+  }
+  if (!old && HD <= 64) {  // NKT = 2 * ceil(N / 32); the lean kernel takes ceil(N / 16) tiles
+    if ((N + 15) / 16 == NKT) return launch_fwd2<HD, NKT>(qkv, o, lse, B, N, H, hd, scale, nq, s);
+    return launch_fwd2<HD, NKT - 1>(qkv, o, lse, B, N, H, hd, scale, nq, s);
+  }
   static const int nw = [] {
     const char* e = getenv("VIT_ATTN_FWD_NW");
     return e ? atoi(e) : 4;
@@ -553,10 +1230,40 @@ hipError_t launch_bwd_nw(const bf16_t* qkv, const bf16_t* dout, const float* lse
   return hipGetLastError();
 }
 
+template <int HD, int NKT16>
+hipError_t launch_bwd2(const bf16_t* qkv, const bf16_t* dout, const float* lse, float* delta, bf16_t* dqkv,
+                       float* bias_partial, int B, int N, int H, int hd, float scale, int nq, hipStream_t s) {
+  constexpr int NP = NKT16 * 16;
+  const size_t lds1 = (size_t)2 * NP * HD * 2 + (size_t)4 * HD * 4 + (size_t)4 * StripOut<HD>::BYTES;
+  auto k1 = attn_bwd_dq_kernel<HD, NKT16, 4>;
+  if (lds1 > 64 * 1024) (void)hipFuncSetAttribute((const void*)k1, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds1);
+  hipLaunchKernelGGL(k1, dim3(B * H), dim3(256), lds1, s, qkv, dout, lse, dqkv, delta, bias_partial, N, H, hd, scale,
+                     nq);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  const size_t lds2 = (size_t)2 * NP * HD * 2 + (size_t)2 * NP * 4 + (size_t)4 * 2 * HD * 4 + (size_t)4 * StripOut<HD>::BYTES;
+  auto k2 = attn_bwd_dkdv_kernel<HD, NKT16, 4>;
+  if (lds2 > 64 * 1024) (void)hipFuncSetAttribute((const void*)k2, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds2);
+  hipLaunchKernelGGL(k2, dim3(B * H), dim3(256), lds2, s, qkv, dout, lse, delta, dqkv, bias_partial, N, H, hd, scale,
+                     nq);
+  return hipGetLastError();
+}
+
 template <int HD, int NKT>
 hipError_t launch_bwd(const bf16_t* qkv, const bf16_t* o, const bf16_t* dout, const float* lse, bf16_t* dqkv,
-                      float* bias_partial, int B, int N, int H, int hd, float scale, int nq, hipStream_t s) {
+                      float* bias_partial, int B, int N, int H, int hd, float scale, int nq, float* delta,
+                      hipStream_t s) {
   (void)o;
+  // VIT_ATTN_BWD_VARIANT (diagnostics): 0 = the lean two-kernel form when it applies, 2 = round-1 kernel
+  static const int var = [] {
+    const char* e = getenv("VIT_ATTN_BWD_VARIANT");
+    return e ? atoi(e) : 0;
+  }();
+  if (var == 0 && HD <= 64 && delta) {
+    if ((N + 15) / 16 == NKT) return launch_bwd2<HD, NKT>(qkv, dout, lse, delta, dqkv, bias_partial, B, N, H, hd,
+                                                         scale, nq, s);
+    return launch_bwd2<HD, NKT - 1>(qkv, dout, lse, delta, dqkv, bias_partial, B, N, H, hd, scale, nq, s);
+  }
   static const int nw = [] {
     const char* e = getenv("VIT_ATTN_BWD_NW");
     return e ? atoi(e) : 4;
@@ -581,10 +1288,10 @@ hipError_t dispatch_fwd(int nkt, const bf16_t* qkv, bf16_t* o, float* lse, int B
 template <int HD>
 hipError_t dispatch_bwd(int nkt, const bf16_t* qkv, const bf16_t* o, const bf16_t* dout, const float* lse,
                         bf16_t* dqkv, float* bias_partial, int B, int N, int H, int hd, float scale, int nq,
-                        hipStream_t s) {
+                        float* delta, hipStream_t s) {
   switch (nkt) {
 #define C(n) \
-  case n: return launch_bwd<HD, n>(qkv, o, dout, lse, dqkv, bias_partial, B, N, H, hd, scale, nq, s);
+  case n: return launch_bwd<HD, n>(qkv, o, dout, lse, dqkv, bias_partial, B, N, H, hd, scale, nq, delta, s);
     VIT_NKT_CASES(C)
 #undef C
   }
@@ -624,7 +1331,8 @@ extern "C" int64_t vit_attention_bias_rows(int64_t N, int32_t path) {
 }
 
 extern "C" int64_t vit_attention_workspace_elems(int64_t B, int64_t N, int64_t H, int32_t path) {
-  return resolve_path(path, N) == 1 ? 0 : B * H * N;
+  (void)path;  // both paths hand delta from their dQ kernel to their dK / dV kernel
+  return B * H * N;
 }
 
 extern "C" int vit_attention_fwd_ex(const void* qkv, void* o, float* lse, int64_t B, int64_t N, int64_t H, int64_t hd,
@@ -690,15 +1398,15 @@ extern "C" int vit_attention_bwd_ex(const void* qkv, const void* o, const void* 
   switch (image_width(hd)) {
     case 32:
       e = dispatch_bwd<32>(nkt, q, ob, d, lse, (bf16_t*)dqkv, bias_partial, (int)B, (int)N, (int)H, (int)hd, scale, nq,
-                           s);
+                           workspace, s);
       break;
     case 64:
       e = dispatch_bwd<64>(nkt, q, ob, d, lse, (bf16_t*)dqkv, bias_partial, (int)B, (int)N, (int)H, (int)hd, scale, nq,
-                           s);
+                           workspace, s);
       break;
     default:
       e = dispatch_bwd<96>(nkt, q, ob, d, lse, (bf16_t*)dqkv, bias_partial, (int)B, (int)N, (int)H, (int)hd, scale, nq,
-                           s);
+                           workspace, s);
       break;
   }
   return vit::check_hip(e, "vit_attention_bwd launch");

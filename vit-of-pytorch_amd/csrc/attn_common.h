@@ -7,6 +7,7 @@ namespace vit_attn {
 
 constexpr float LOG2E = 1.4426950408889634f;
 typedef unsigned v4u __attribute__((ext_vector_type(4)));
+typedef unsigned v2u __attribute__((ext_vector_type(2)));
 
 template <int HD>
 __device__ __forceinline__ int aswz(int row) {
@@ -117,5 +118,87 @@ __device__ __forceinline__ float sum16(float v) {
   v += __shfl_xor(v, 8, 64);
   return v;
 }
+
+// ---- explicit LDS address space (byte offsets from the dynamic LDS base) ----
+typedef __attribute__((address_space(3))) char lds_t;
+template <class T>
+__device__ __forceinline__ T lds_ld(const lds_t* p) {
+  return *reinterpret_cast<const __attribute__((address_space(3))) T*>(p);
+}
+template <class T>
+__device__ __forceinline__ void lds_st(lds_t* p, const T& v) {
+  *reinterpret_cast<__attribute__((address_space(3))) T*>(p) = v;
+}
+__device__ __forceinline__ v4s lds_tr(const lds_t* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16(reinterpret_cast<__attribute__((address_space(3))) v4s*>(
+      const_cast<lds_t*>(p)));
+}
+__device__ __forceinline__ v4f mfma16(const v4s& a, const v4s& b, const v4f& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, b, c, 0, 0, 0);
+}
+// max(a, b, c) in one v_max3_f32 (hipcc splits fmaxf chains into v_max_f32 pairs)
+__device__ __forceinline__ float max3f(float a, float b, float c) {
+  float r;
+  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+__device__ __forceinline__ v4s pack4(const v4f& a) {
+  v4s r;
+  r[0] = (short)f2bf(a[0]); r[1] = (short)f2bf(a[1]); r[2] = (short)f2bf(a[2]); r[3] = (short)f2bf(a[3]);
+  return r;
+}
+
+// Per-lane byte offsets into a [rows][HD] swizzled image (img_off), for
+//   row reads (16 rows x 32 k MFMA fragment, ds_read_b128):  row 16t + (lane & 15), chunk 4kk + (lane >> 4)
+//   transposed reads (ds_read_b64_tr_b16, rd_tr): rows 16t + 4g + q, columns 16dt + 4p .. (+ 8 B within the chunk)
+// A tile index t adds t * 16 * HD * 2 bytes (an immediate): the swizzle depends only on row bits 1..2.
+template <int HD>
+struct ImgLane {
+  int row[HD / 32 > 0 ? HD / 32 : 1];
+  int tr[HD / 16];
+  __device__ __forceinline__ explicit ImgLane(int lane) {
+    const int g = lane >> 4, i = lane & 15;
+#pragma unroll
+    for (int kk = 0; kk < HD / 32; ++kk) row[kk] = i * HD * 2 + (((kk * 4 + g) ^ aswz<HD>(i)) << 4);
+    const int q = i >> 2, p = i & 3, rr = 4 * g + q;
+#pragma unroll
+    for (int dt = 0; dt < HD / 16; ++dt) tr[dt] = rr * HD * 2 + (((dt * 2 + (p >> 1)) ^ aswz<HD>(rr)) << 4) + 8 * (p & 1);
+  }
+  static constexpr int TILE = 16 * HD * 2;
+};
+
+// ---- epilogue: a wave's 16-row x HD output strip, written as whole rows ----
+// The O^T / dQ^T / dK^T accumulators hold 4 consecutive columns (16dt + 4g ..) of one row (lane i) per
+// register quad, i.e. 8-B pieces of 16 rows per store instruction. Staging the strip through a
+// wave-private LDS tile ([16][HD] bf16, rows padded to HD*2 + 16 bytes: the 8-B writes of a 16-lane
+// group land on distinct banks) lets every lane store 16 contiguous bytes, each instruction covering
+// whole 2*HD-byte rows.
+template <int HD>
+struct StripOut {
+  static constexpr int LD = HD * 2 + 16;  // bytes per staged row
+  static constexpr int BYTES = 16 * LD;
+  // stage: acc[dt] * s (bf16) at row i, columns 16dt + 4g .. + 3
+  __device__ __forceinline__ static void stage(lds_t* buf, const v4f* acc, float s, int lane) {
+    const int g = lane >> 4, i = lane & 15;
+#pragma unroll
+    for (int dt = 0; dt < HD / 16; ++dt) {
+      v2u u;
+      u[0] = pack2bf(acc[dt][0] * s, acc[dt][1] * s);
+      u[1] = pack2bf(acc[dt][2] * s, acc[dt][3] * s);
+      lds_st(buf + i * LD + (dt * 16 + 4 * g) * 2, u);
+    }
+  }
+  // store rows [0, 16) of the staged strip to dst + r * ld (elements), rows < nrows, columns < hd
+  __device__ __forceinline__ static void store(const lds_t* buf, bf16_t* dst, long ld, int nrows, int hd, int lane) {
+    constexpr int CPR = HD / 8;              // 16-B chunks per row
+    constexpr int ROWS_PER = 64 / CPR;       // rows per wave-instruction
+#pragma unroll
+    for (int r0 = 0; r0 < 16; r0 += ROWS_PER) {
+      const int r = r0 + lane / CPR, ch = lane % CPR;
+      const v4u v = lds_ld<v4u>(buf + r * LD + ch * 16);
+      if (r < nrows && ch * 8 < hd) *reinterpret_cast<v4u*>(dst + (long)r * ld + ch * 8) = v;
+    }
+  }
+};
 
 }  // namespace vit_attn
