@@ -197,20 +197,22 @@ __global__ void __launch_bounds__(NW * 64, NW == 8 ? 2 : 3) attn_fwd2_kernel(con
     mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
     const float mc = mx * c;
+    float l = 0.f;  // f32 row sum of the unrounded P (the reference's normalisation)
 #pragma unroll
     for (int kt = 0; kt < NKT; ++kt)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) s[kt][r] = ex2(fmaf(s[kt][r], c, -mc));
-    // P V and the row sums of the bf16 P it uses: an all-ones A operand sums P^T over the keys on the
-    // matrix core (every row of lsum holds the query's sum), replacing a VALU add per score
-    const v8bf ones8 = __builtin_bit_cast(v8bf, v8s{0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80});
-    v4f acc[HD / 16], lsum = {0.f, 0.f, 0.f, 0.f};
+      for (int r = 0; r < 4; ++r) {
+        s[kt][r] = ex2(fmaf(s[kt][r], c, -mc));
+        l += s[kt][r];
+      }
+    l += __shfl_xor(l, 16, 64);
+    l += __shfl_xor(l, 32, 64);
+    v4f acc[HD / 16];
 #pragma unroll
     for (int dt = 0; dt < HD / 16; ++dt) acc[dt] = v4f{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int ks = 0; ks < NKT / 2; ++ks) {
       const v8bf pp = pack8(s[2 * ks], s[2 * ks + 1]);
-      lsum = mfma(ones8, pp, lsum);
 #pragma unroll
       for (int dt = 0; dt < HD / 16; ++dt) {
         v8s vt;
@@ -221,11 +223,9 @@ __global__ void __launch_bounds__(NW * 64, NW == 8 ? 2 : 3) attn_fwd2_kernel(con
     }
     if constexpr (NKT % 2 == 1) {
       const v4s pp = pack4(s[NKT - 1]);
-      lsum = mfma16(v4s{0x3F80, 0x3F80, 0x3F80, 0x3F80}, pp, lsum);
 #pragma unroll
       for (int dt = 0; dt < HD / 16; ++dt) acc[dt] = mfma16(lds_tr(Vi + (NKT - 1) * T + L.tr[dt]), pp, acc[dt]);
     }
-    const float l = lsum[0];
     const int q = qt * 16 + i;
     if (g == 0 && q < N && !(diag & 2)) lse[(long)bh * N + q] = mx * scale + logf(l);
     const float inv_l = 1.0f / l;
@@ -1188,10 +1188,11 @@ hipError_t launch_fwd_p(const bf16_t* qkv, bf16_t* o, float* lse, int B, int N, 
 template <int HD, int NKT>
 hipError_t launch_fwd(const bf16_t* qkv, bf16_t* o, float* lse, int B, int N, int H, int hd, float scale,
                       int nq, hipStream_t s) {
-  // VIT_ATTN_FWD_VARIANT (diagnostics): 0 persistent, 1 one-shot lean, 2 the round-1 kernel
+  // VIT_ATTN_FWD_VARIANT (diagnostics): 3 one-shot lean 8-wave (default), 1 one-shot lean 4-wave,
+  // 0 persistent double-buffered, 2 the round-1 kernel
   static const int var = [] {
     const char* e = getenv("VIT_ATTN_FWD_VARIANT");
-    return e ? atoi(e) : 0;
+    return e ? atoi(e) : 3;
   }();
   const bool old = var == 2;
   // persistent double-buffered form while two K/V image pairs fit the 160 KiB LDS
@@ -1254,10 +1255,11 @@ hipError_t launch_bwd(const bf16_t* qkv, const bf16_t* o, const bf16_t* dout, co
                       float* bias_partial, int B, int N, int H, int hd, float scale, int nq, float* delta,
                       hipStream_t s) {
   (void)o;
-  // VIT_ATTN_BWD_VARIANT (diagnostics): 0 = the lean two-kernel form when it applies, 2 = round-1 kernel
+  // VIT_ATTN_BWD_VARIANT: 2 = the single-kernel two-stage form (default: 272 us in the B/16 bs256 step
+  // against 294 us for the two-kernel form, profiles/r02), 0 = the lean two-kernel form
   static const int var = [] {
     const char* e = getenv("VIT_ATTN_BWD_VARIANT");
-    return e ? atoi(e) : 0;
+    return e ? atoi(e) : 2;
   }();
   if (var == 0 && HD <= 64 && delta) {
     if ((N + 15) / 16 == NKT) return launch_bwd2<HD, NKT>(qkv, dout, lse, delta, dqkv, bias_partial, B, N, H, hd,

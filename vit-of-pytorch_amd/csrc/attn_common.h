@@ -192,6 +192,9 @@ struct StripOut {
   __device__ __forceinline__ static void store(const lds_t* buf, bf16_t* dst, long ld, int nrows, int hd, int lane) {
     constexpr int CPR = HD / 8;              // 16-B chunks per row
     constexpr int ROWS_PER = 64 / CPR;       // rows per wave-instruction
+    // the staged 8-B writes and these 16-B reads have different types: keep the compiler from moving
+    // the reads above the writes (one wave's LDS operations then execute in order)
+    asm volatile("" ::: "memory");
 #pragma unroll
     for (int r0 = 0; r0 < 16; r0 += ROWS_PER) {
       const int r = r0 + lane / CPR, ch = lane % CPR;
