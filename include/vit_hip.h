@@ -194,6 +194,16 @@ int vit_attention_bwd_ex(const void* qkv, const void* o, const void* dout, const
                          float* bias_partial, int64_t B, int64_t N, int64_t H, int64_t hd, float scale,
                          int64_t q_rows, int32_t path, float* workspace, vit_stream_t stream);
 
+/* Ragged-query attention forward (Res-ViT inference, res-vit/model.py:494-529: per sample, queries =
+ * its active tokens, keys / values = all its tokens). Sample b's queries are rows [cu_q[b], cu_q[b+1])
+ * of q (bf16, row stride ldq, head h at columns h*hd), its keys rows [b*Nkv, (b+1)*Nkv) of k and v
+ * (bf16, strides ldk / ldv); o (bf16, stride ldo) rows match q's. cu_q: device int32 [B + 1],
+ * max_q >= every sample's query count. o = softmax((q k^T) / sqrt(hd)) v (scale = 1/sqrt(hd)).
+ * K/V-tiled online softmax, any Nkv; one launch for the whole batch. Forward only. */
+int vit_attention_fwd_varlen(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v, int64_t ldv,
+                             void* o, int64_t ldo, const int32_t* cu_q, int64_t B, int64_t max_q, int64_t Nkv,
+                             int64_t H, int64_t hd, float scale, vit_stream_t stream);
+
 /* ------------------------------------------------------------------------------------------
  * Patch embedding im2col (Conv2d k=s=P as a GEMM, src/model.py:179,197-200):
  * x f32 NCHW [B,3,img,img] -> out bf16 [B*N, Kpad], N = (img/P)^2 + 1, row b*N (cls) is 0,

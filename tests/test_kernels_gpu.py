@@ -430,3 +430,28 @@ def test_attention_query_rows_match_full(B, N, H, hd, path):
     assert torch.equal(g_f.view(B * N, 3, D)[:, 1:], g_r.view(B * N, 3, D)[:, 1:])   # dK, dV
     assert torch.equal(g_f.view(B * N, 3, D)[:, 0], g_r.view(B * N, 3, D)[:, 0])     # dQ (0 past row 0)
     assert torch.equal(b_f, b_r)
+
+
+@pytest.mark.parametrize("counts,Nkv,H,hd", [((5, 0, 17, 1), 17, 2, 32), ((197, 60, 3), 197, 3, 64),
+                                             ((70, 577), 577, 2, 64), ((100, 257), 257, 2, 80)])
+def test_attention_varlen_ragged_queries(counts, Nkv, H, hd):
+    """vit_attention_fwd_varlen (Res-ViT inference, res-vit/model.py:494-529): sample b's queries are its
+    own rows of a packed q (any count, 0 included), its keys / values all Nkv of its tokens."""
+    B = len(counts)
+    D = H * hd
+    total = sum(counts)
+    q = torch.randn(max(total, 1), D, device=DEV).bfloat16()
+    k = torch.randn(B * Nkv, D, device=DEV).bfloat16()
+    v = torch.randn(B * Nkv, D, device=DEV).bfloat16()
+    o = torch.full((max(total, 1), D), float("nan"), device=DEV, dtype=torch.bfloat16)
+    cu = torch.tensor([0] + list(torch.tensor(counts).cumsum(0)), device=DEV, dtype=torch.int32)
+    ops.attention_fwd_varlen(q, D, k, D, v, D, o, D, cu, B, max(counts), Nkv, H, hd, 1.0 / math.sqrt(hd))
+    for b in range(B):
+        s, e = int(cu[b]), int(cu[b + 1])
+        if s == e:
+            continue
+        qb = q[s:e].float().view(e - s, H, hd).transpose(0, 1)
+        kb = k[b * Nkv:(b + 1) * Nkv].float().view(Nkv, H, hd).transpose(0, 1)
+        vb = v[b * Nkv:(b + 1) * Nkv].float().view(Nkv, H, hd).transpose(0, 1)
+        ref = (torch.softmax(qb @ kb.transpose(-1, -2) / math.sqrt(hd), -1) @ vb).transpose(0, 1).reshape(e - s, D)
+        assert rel(o[s:e].float(), ref) < 1e-2, b

@@ -1,0 +1,62 @@
+"""Res-ViT host-side surface (vitmi.resvit vs reference res-vit/model.py, model_utils.py) on CPU: the
+router index tables and the constructor (module names, state_dict order, RNG draws) against
+tests/golden/resvit_tiny.npz, which tests/golden/make_resvit_golden.py wrote from the imported reference."""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from vitmi import resvit
+
+TINY = dict(dim=64, mlp_dim=128, n_layers=5, n_heads=2, n_kv_heads=2, norm_eps=1e-5, lora_rank=4,
+            dynamic_active_target=0.4, dynamic_start_layer=1, dynamic_router_hdim=32, dynamic_reserve_initials=1,
+            low_rank_dim=16, block_size=2, use_lora=True, use_reslr=True, image_size=(32, 32), patch_size=(8, 8),
+            num_classes=10, device="cpu")
+
+
+@pytest.fixture(scope="module")
+def golden(golden_dir):
+    return np.load(os.path.join(golden_dir, "resvit_tiny.npz"))
+
+
+def test_lra_index_tables_match_reference(golden):
+    ref = json.loads(str(golden["lra_masks_json"]))
+    for bs in (1, 2, 4):
+        mine = [list(map(list, t)) for t in resvit.get_indices_from_LRA_mask(bs)]
+        assert mine == ref[str(bs)], bs
+    with pytest.raises(ValueError):
+        resvit.get_indices_from_LRA_mask(3)
+
+
+def test_constructor_names_order_and_rng(golden):
+    torch.manual_seed(42)
+    m = resvit.Transformer(resvit.ModelArgs(**TINY))
+    sd = m.state_dict()
+    keys = [k[2:] for k in golden.files if k.startswith("p/")]
+    assert list(sd.keys()) == keys
+    # tensors the fixture's rescale leaves alone are the constructor's own draws: bit-identical
+    untouched = [k for k in keys if not any(s in k for s in (".attention.w", "lora_", "approximators", "router.out_conv.4",
+                                                              "norm", "pos_embedding", "classifier.weight"))]
+    assert len(untouched) > 20
+    for k in untouched:
+        assert torch.equal(sd[k], torch.from_numpy(golden["p/" + k])), k
+    # LoRA freezes the base weights (res-vit/model.py:573-584)
+    trainable = [n for n, p in m.named_parameters() if p.requires_grad]
+    assert trainable == [str(t) for t in golden["trainable"]]
+
+
+def test_repeat_kv():
+    x = torch.randn(2, 5, 3, 4)
+    r = resvit.repeat_kv(x, 2)
+    assert r.shape == (2, 5, 6, 4)
+    assert torch.equal(r[:, :, 0], x[:, :, 0]) and torch.equal(r[:, :, 1], x[:, :, 0]) and torch.equal(r[:, :, 5], x[:, :, 2])
+    assert resvit.repeat_kv(x, 1) is x
+
+
+def test_cpu_forward_refuses():
+    torch.manual_seed(42)
+    m = resvit.Transformer(resvit.ModelArgs(**TINY))
+    with pytest.raises(RuntimeError, match="MI355X HIP path only"):
+        m(torch.randn(1, 3, 32, 32), torch.tensor([1]))

@@ -1,0 +1,136 @@
+"""Res-ViT (vitmi.resvit) on the MI355X vs the reference res-vit/model.py, through the fixture
+tests/golden/resvit_tiny.npz written from the imported reference (tests/golden/make_resvit_golden.py).
+GPU only.
+
+Routing decisions are discrete: a token whose router logit margin is below bf16 noise could flip and
+send the whole comparison down another path. So the router is checked on its own (its logits from the
+reference's recorded router input, and every decision whose margin exceeds that noise), and the
+end-to-end checks replay the reference's recorded decisions (and, in training, its Gumbel draws).
+Tolerances (bf16 operands, f32 accumulation): logits relative 1e-2, losses 1e-3
+relative (router entropy / ratio loss 1e-2: small differences of nearly-saturated probabilities),
+every trainable gradient 3e-2 relative or 1e-3 of the global gradient norm when tiny.
+"""
+import math
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from test_resvit_cpu import TINY
+
+pytestmark = pytest.mark.gpu
+
+
+def rel(a, b):
+    a = torch.as_tensor(a).detach().double().cpu()
+    b = torch.as_tensor(b).double().cpu()
+    return float((a - b).norm() / b.norm().clamp_min(1e-30))
+
+
+@pytest.fixture(scope="module")
+def golden(golden_dir):
+    return np.load(os.path.join(golden_dir, "resvit_tiny.npz"))
+
+
+def build(golden):
+    from vitmi import resvit
+    torch.manual_seed(42)
+    m = resvit.Transformer(resvit.ModelArgs(**dict(TINY, device="cuda")))
+    m.load_state_dict({k[2:]: torch.from_numpy(golden[k]) for k in golden.files if k.startswith("p/")})
+    return m.cuda()
+
+
+def routers(m):
+    return [l.router for l in m.layers if hasattr(l, "router")]
+
+
+def replay(m, golden, tag):
+    """feed the reference's recorded decisions (and Gumbel draws) to the routers, in call order"""
+    for j, r in enumerate(routers(m)):
+        hard = torch.from_numpy(golden[f"{tag}/router{j}_hard"]).cuda()
+        r.hard_override = lambda logits, h=hard: h
+        if tag == "train":
+            g = torch.from_numpy(golden[f"train/gumbel{j}"]).cuda()
+            r.gumbel_noise = lambda logits, g=g: g
+
+
+@pytest.mark.parametrize("tag", ["eval", "train"])
+def test_router_matches_reference(golden, tag):
+    """each router on the reference's recorded input: logits within bf16 tolerance, and the same keep
+    decision for every token / layer whose reference logit margin exceeds 5% of the logit scale."""
+    m = build(golden)
+    m.train(tag == "train")
+    for j, r in enumerate(routers(m)):
+        x = torch.from_numpy(golden[f"{tag}/router{j}_x"]).cuda()
+        ref_logits = torch.from_numpy(golden[f"{tag}/router{j}_logits"])
+        if tag == "train":
+            g = torch.from_numpy(golden[f"train/gumbel{j}"]).cuda()
+            r.gumbel_noise = lambda logits, g=g: g
+        seen = {}
+        h = r.out_conv.register_forward_hook(lambda mod, i, o: seen.setdefault("logits", o.detach()))
+        with torch.no_grad():
+            hard, idx, ent, soft = r(x)
+        h.remove()
+        assert rel(seen["logits"], ref_logits) < 1e-2
+        ref_hard = torch.from_numpy(golden[f"{tag}/router{j}_hard"])
+        z = ref_logits.view(*ref_logits.shape[:2], -1, 2).double()
+        if tag == "train":
+            z = z + torch.from_numpy(golden[f"train/gumbel{j}"]).double()
+        margin = (z[..., 1] - z[..., 0]).abs()
+        sure = margin > 0.05 * float(z.abs().max())
+        sure[:, :1] = True  # the reserved cls token is forced to keep
+        assert int(sure.sum()) > 0.8 * sure.numel()
+        assert torch.equal(hard.cpu()[..., 1][sure], ref_hard[..., 1][sure]), (tag, j)
+
+
+def test_eval_ragged_forward_matches_reference(golden):
+    """inference: router argmax, ragged attention (active queries, all keys; one varlen launch), FFN,
+    approximators on the inactive tokens (res-vit/model.py:494-529)."""
+    m = build(golden).eval()
+    replay(m, golden, "eval")
+    x = torch.from_numpy(golden["x"]).cuda()
+    y = torch.from_numpy(golden["y"]).cuda()
+    with torch.no_grad():
+        c, a, d, ent, metric = m(x, y)
+    for k, v in m.routing_maps.items():
+        assert torch.equal(v.cpu(), torch.from_numpy(golden[f"eval/routing{k}"])), k
+    assert rel(m.logits, golden["eval/logits"]) < 1e-2
+    assert abs(float(c) - float(golden["eval/c_loss"])) <= 1e-3 * float(golden["eval/c_loss"])
+    assert abs(float(ent) - float(golden["eval/r_entropy"])) <= 1e-2 * abs(float(golden["eval/r_entropy"])) + 1e-6
+    assert abs(float(metric["non_low_rank_ratio"]) - float(golden["eval/active_ratio"])) < 1e-6
+
+
+def test_train_step_matches_reference(golden):
+    """training: teacher (every token) and student (routed) paths, Gumbel straight-through routing, LoRA
+    over frozen base weights; 10 c_loss + 10 a_loss + 1 d_loss (res-vit/train.py:56) and the gradient of
+    every trainable parameter."""
+    m = build(golden).train()
+    replay(m, golden, "train")
+    x = torch.from_numpy(golden["x"]).cuda()
+    y = torch.from_numpy(golden["y"]).cuda()
+    c, a, d, ent, metric = m(x, y)
+    (10.0 * c + 10.0 * a + 1.0 * d).backward()
+    assert rel(m.logits, golden["train/logits"]) < 1e-2
+    assert abs(float(c) - float(golden["train/c_loss"])) <= 1e-3 * float(golden["train/c_loss"])
+    assert abs(float(d) - float(golden["train/d_loss"])) <= 1e-2 * float(golden["train/d_loss"])
+    assert abs(float(a) - float(golden["train/a_loss"])) <= 1e-2 * float(golden["train/a_loss"]) + 1e-6
+    assert abs(float(ent) - float(golden["train/r_entropy"])) <= 1e-2 * abs(float(golden["train/r_entropy"])) + 1e-6
+    named = dict(m.named_parameters())
+    trainable = [str(t) for t in golden["trainable"]]
+    assert [n for n, p in m.named_parameters() if p.requires_grad] == trainable
+    tot = math.sqrt(sum(float(np.square(golden["grad/" + n].astype(np.float64)).sum()) for n in trainable))
+    bad = []
+    for n in trainable:
+        ref = torch.from_numpy(golden["grad/" + n])
+        mine = named[n].grad
+        mine = torch.zeros_like(ref) if mine is None else mine.detach().cpu()
+        gn = float(ref.double().norm())
+        if gn < 1e-3 * tot:
+            if float((mine.double() - ref.double()).norm()) > 1e-3 * tot:
+                bad.append((n, "abs"))
+        elif rel(mine, ref) > 3e-2:
+            bad.append((n, rel(mine, ref)))
+    assert not bad, bad
+    # frozen base weights receive no gradient (res-vit/model.py:573-584)
+    assert all(p.grad is None for n, p in m.named_parameters() if not p.requires_grad)

@@ -407,6 +407,99 @@ __global__ void __launch_bounds__(NW * 64) attn_bwd_dkdv_tiled_kernel(
   }
 }
 
+// ---- forward, ragged queries (Res-ViT inference, res-vit/model.py:494-529) ------------------------
+// Sample b's queries are rows [cu_q[b], cu_q[b+1]) of q (its active tokens, any count), its keys and
+// values rows [b * Nkv, (b+1) * Nkv) of k / v (all tokens). One launch replaces the reference's
+// per-sample loop of asymmetric attention calls; same online-softmax body as attn_fwd_tiled_kernel.
+template <int HD, int NW>
+__global__ void __launch_bounds__(NW * 64) attn_fwd_varlen_kernel(
+    const bf16_t* __restrict__ q, long ldq, const bf16_t* __restrict__ k, long ldk, const bf16_t* __restrict__ v,
+    long ldv, bf16_t* __restrict__ o, long ldo, const int* __restrict__ cu_q, int Nkv, int H, int hd, float scale) {
+  static_assert(NW * 16 == BLK, "one 16-query strip per wave");
+  constexpr int IMG = BLK * HD * 2;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int b = blockIdx.x / H, h = blockIdx.x % H;
+  const int qs = cu_q[b], nqb = cu_q[b + 1] - qs;
+  if ((int)blockIdx.y * BLK >= nqb) return;  // uniform over the workgroup
+  const bf16_t* qb = q + (long)qs * ldq + (long)h * hd;
+  const bf16_t* kb = k + (long)b * Nkv * ldk + (long)h * hd;
+  const bf16_t* vb = v + (long)b * Nkv * ldv + (long)h * hd;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int g = lane >> 4, i = lane & 15;
+  const int q0 = blockIdx.y * BLK + wave * 16;
+  v8bf qf[HD / 32];
+#pragma unroll
+  for (int kk = 0; kk < HD / 32; ++kk) qf[kk] = gl_row<HD>(qb, ldq, q0, kk, nqb, hd, lane);
+  const int nkb = (Nkv + BLK - 1) / BLK;
+  Stage2<HD, NW * 64> st;
+  st.issue(kb, ldk, vb, ldv, 0, Nkv, hd);
+  st.write(smem, smem + IMG);
+  __syncthreads();
+  const float c = scale * LOG2E;
+  float m = -INFINITY, l = 0.f;
+  v4f oacc[HD / 16];
+#pragma unroll
+  for (int dt = 0; dt < HD / 16; ++dt) oacc[dt] = v4f{0.f, 0.f, 0.f, 0.f};
+  for (int j = 0; j < nkb; ++j) {
+    if (j + 1 < nkb) st.issue(kb, ldk, vb, ldv, (j + 1) * BLK, Nkv, hd);
+    const char* Ki = smem + (j & 1) * 2 * IMG;
+    const char* Vi = Ki + IMG;
+    v4f s[4];
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt) {
+      s[kt] = v4f{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < HD / 32; ++kk) s[kt] = mfma(rd_row<HD>(Ki, kt * 16, kk, lane), qf[kk], s[kt]);
+    }
+    if ((j + 1) * BLK > Nkv) {
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (j * BLK + kt * 16 + 4 * g + r >= Nkv) s[kt][r] = -INFINITY;
+    }
+    float mx = -INFINITY;
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt) mx = fmaxf(mx, fmaxf(fmaxf(s[kt][0], s[kt][1]), fmaxf(s[kt][2], s[kt][3])));
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float mn = fmaxf(m, mx);
+    const float alpha = ex2((m - mn) * c);
+    m = mn;
+    const float mc = mn * c;
+    l *= alpha;
+#pragma unroll
+    for (int dt = 0; dt < HD / 16; ++dt) oacc[dt] *= alpha;
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float p = ex2(fmaf(s[kt][r], c, -mc));
+        s[kt][r] = p;
+        l += p;
+      }
+    const v8bf p01 = pack8(s[0], s[1]), p23 = pack8(s[2], s[3]);
+#pragma unroll
+    for (int dt = 0; dt < HD / 16; ++dt) {
+      oacc[dt] = mfma(rd_tr<HD>(Vi, 0, 1, dt * 16, lane), p01, oacc[dt]);
+      oacc[dt] = mfma(rd_tr<HD>(Vi, 2, 3, dt * 16, lane), p23, oacc[dt]);
+    }
+    if (j + 1 < nkb) st.write(smem + ((j + 1) & 1) * 2 * IMG, smem + ((j + 1) & 1) * 2 * IMG + IMG);
+    __syncthreads();
+  }
+  l += __shfl_xor(l, 16, 64);
+  l += __shfl_xor(l, 32, 64);
+  const int qq = q0 + i;
+  if (qq < nqb) {
+    const float inv_l = 1.0f / l;
+#pragma unroll
+    for (int dt = 0; dt < HD / 16; ++dt) {
+      const int d = dt * 16 + 4 * g;
+      if (d < hd) store4(o + (long)(qs + qq) * ldo + (long)h * hd + d, oacc[dt], inv_l);
+    }
+  }
+}
+
 constexpr int NWT = BLK / 16;  // 4 waves per workgroup
 
 template <int HD>
@@ -452,4 +545,40 @@ hipError_t vit_attn_tiled_bwd(const void* qkv, const void* dout, const float* ls
   if (hd <= 32) return launch_tiled_bwd<32>(q, d, lse, delta, (bf16_t*)dqkv, bias_partial, B, N, H, hd, scale, nq, s);
   if (hd <= 64) return launch_tiled_bwd<64>(q, d, lse, delta, (bf16_t*)dqkv, bias_partial, B, N, H, hd, scale, nq, s);
   return launch_tiled_bwd<96>(q, d, lse, delta, (bf16_t*)dqkv, bias_partial, B, N, H, hd, scale, nq, s);
+}
+
+hipError_t vit_attn_varlen_fwd(const void* q, long ldq, const void* k, long ldk, const void* v, long ldv, void* o,
+                               long ldo, const int* cu_q, int B, int max_q, int Nkv, int H, int hd, float scale,
+                               hipStream_t s) {
+  const dim3 grid(B * H, (max_q + BLK - 1) / BLK);
+  const auto* qq = (const bf16_t*)q;
+  const auto* kk = (const bf16_t*)k;
+  const auto* vv = (const bf16_t*)v;
+  auto* oo = (bf16_t*)o;
+  if (hd <= 32)
+    hipLaunchKernelGGL((attn_fwd_varlen_kernel<32, NWT>), grid, dim3(NWT * 64), (size_t)4 * BLK * 32 * 2, s, qq, ldq, kk,
+                       ldk, vv, ldv, oo, ldo, cu_q, Nkv, H, hd, scale);
+  else if (hd <= 64)
+    hipLaunchKernelGGL((attn_fwd_varlen_kernel<64, NWT>), grid, dim3(NWT * 64), (size_t)4 * BLK * 64 * 2, s, qq, ldq, kk,
+                       ldk, vv, ldv, oo, ldo, cu_q, Nkv, H, hd, scale);
+  else
+    hipLaunchKernelGGL((attn_fwd_varlen_kernel<96, NWT>), grid, dim3(NWT * 64), (size_t)4 * BLK * 96 * 2, s, qq, ldq, kk,
+                       ldk, vv, ldv, oo, ldo, cu_q, Nkv, H, hd, scale);
+  return hipGetLastError();
+}
+
+extern "C" int vit_attention_fwd_varlen(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v,
+                                        int64_t ldv, void* o, int64_t ldo, const int32_t* cu_q, int64_t B,
+                                        int64_t max_q, int64_t Nkv, int64_t H, int64_t hd, float scale,
+                                        vit_stream_t stream) {
+  VIT_CHECK_ARG(q && k && v && o && cu_q && B >= 1 && H >= 1 && Nkv >= 1 && max_q >= 0,
+                "vit_attention_fwd_varlen: bad args");
+  VIT_CHECK_ARG(hd >= 16 && hd <= 96 && hd % 16 == 0, "vit_attention_fwd_varlen: head_dim %lld unsupported",
+                (long long)hd);
+  VIT_CHECK_ARG(ldq % 8 == 0 && ldk % 8 == 0 && ldv % 8 == 0 && ldo % 4 == 0,
+                "vit_attention_fwd_varlen: row strides must keep 16-B (q/k/v) and 8-B (o) alignment");
+  if (max_q == 0) return VIT_OK;
+  return vit::check_hip(vit_attn_varlen_fwd(q, ldq, k, ldk, v, ldv, o, ldo, cu_q, (int)B, (int)max_q, (int)Nkv,
+                                            (int)H, (int)hd, scale, (hipStream_t)stream),
+                        "vit_attention_fwd_varlen launch");
 }

@@ -91,6 +91,8 @@ _SIGS = {
     "vit_dropout_apply_f32": (c_i32, [ctypes.POINTER(Dropout), c_vp, c_vp, c_i64, c_i64, c_vp]),
     "vit_add_bcast_f32": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_i64, c_vp]),
     "vit_unpack_bf16_f32": (c_i32, [c_vp, c_i64, c_i64, c_i64, c_vp, c_i64, c_vp]),
+    "vit_attention_fwd_varlen": (c_i32, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_i64, c_i64,
+                                         c_i64, c_i64, c_f32, c_vp]),
 }
 
 EXPORTED = tuple(_SIGS)

@@ -330,3 +330,54 @@ def attention(q, k, v):
         raise ValueError(f"attention: q, k, v must share a [b, n, H, hd] shape, got {tuple(q.shape)}, "
                          f"{tuple(k.shape)}, {tuple(v.shape)}")
     return HipAttention.apply(q, k, v)
+
+
+def attention_ragged(q, k, v, cu_q, max_q):
+    """Ragged-query attention forward (Res-ViT inference, res-vit/model.py:494-529): q [total, H, hd]
+    holds every sample's active query tokens back to back (sample b at rows cu_q[b] .. cu_q[b+1]), k / v
+    [B, Nkv, H, hd] all of each sample's tokens; returns [total, H, hd] f32. One varlen kernel launch
+    (vit_attention_fwd_varlen) for the batch. Forward only (the reference uses it under no_grad)."""
+    _gpu(q, k, v, cu_q)
+    if torch.is_grad_enabled() and any(t.requires_grad for t in (q, k, v)):
+        raise NotImplementedError("ragged attention is the inference path (res-vit/model.py:494-529); it has no "
+                                  "backward")
+    total, h, hd = q.shape
+    b, nkv = k.shape[0], k.shape[1]
+    d = h * hd
+    qb = torch.empty(max(total, 1), d, device=q.device, dtype=BF16)
+    kb = torch.empty(b * nkv, d, device=q.device, dtype=BF16)
+    vb = torch.empty(b * nkv, d, device=q.device, dtype=BF16)
+    if total:
+        ops.cast_bf16(_f32(q).reshape(-1), qb, total * d)
+    ops.cast_bf16(_f32(k).reshape(-1), kb, b * nkv * d)
+    ops.cast_bf16(_f32(v).reshape(-1), vb, b * nkv * d)
+    ob = torch.empty(max(total, 1), d, device=q.device, dtype=BF16)
+    ops.attention_fwd_varlen(qb, d, kb, d, vb, d, ob, d, cu_q.to(torch.int32).contiguous(), b, int(max_q), nkv, h, hd,
+                             1.0 / math.sqrt(hd))
+    out = torch.empty(total, h, hd, device=q.device, dtype=F32)
+    if total:
+        ops.unpack_bf16_f32(ob, d, total, d, out, d)
+    return out
+
+
+def patch_embed(x, weight, bias, patch):
+    """nn.Conv2d(3, D, kernel = stride = patch) on images x [B, 3, H, W] as im2col (vit_im2col_f32) + the
+    bf16 MFMA GEMM with bias, returned token-major [B, (H/P)(W/P), D] (the reference's
+    rearrange(conv(x), 'b c h w -> b (h w) c'); res-vit/model.py:629-630, src/model.py:197-200).
+    Gradients reach weight and bias (the images are inputs)."""
+    _gpu(x, weight, bias)
+    if x.requires_grad:
+        raise NotImplementedError("patch_embed: no gradient with respect to the input images")
+    b, c, hh, ww = x.shape
+    if c != 3 or hh != ww:
+        raise ValueError(f"patch_embed expects square 3-channel images, got {tuple(x.shape)}")
+    g = hh // patch
+    n = g * g
+    k = 3 * patch * patch
+    kpad = _rup(k, 64)
+    cols = torch.empty(b * (n + 1), kpad, device=x.device, dtype=F32)
+    ops.im2col_f32(_f32(x), cols, b, hh, patch, kpad)
+    rows = cols.view(b, n + 1, kpad)[:, 1:, :k].reshape(b * n, k)  # drop the cls rows im2col leaves zero
+    d = weight.shape[0]
+    y = HipLinear.apply(rows, weight.reshape(d, k), bias, False)
+    return y.view(b, n, d)

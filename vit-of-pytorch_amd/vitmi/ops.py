@@ -276,3 +276,13 @@ def unpack_bf16_f32(inp, ldi, rows, cols, out, ldo):
     _chk(inp, BF16, "inp")
     _chk(out, F32, "out")
     check(lib().vit_unpack_bf16_f32(_p(inp), ldi, rows, cols, _p(out), ldo, _stream()), "vit_unpack_bf16_f32")
+
+
+def attention_fwd_varlen(q, ldq, k, ldk, v, ldv, o, ldo, cu_q, B, max_q, Nkv, H, hd, scale):
+    """ragged-query attention forward (vit_attention_fwd_varlen): bf16 q / k / v / o row views, cu_q
+    int32 [B + 1] on the device."""
+    for t, n in ((q, "q"), (k, "k"), (v, "v"), (o, "o")):
+        _chk(t, BF16, n)
+    _chk(cu_q, torch.int32, "cu_q")
+    check(lib().vit_attention_fwd_varlen(_p(q), ldq, _p(k), ldk, _p(v), ldv, _p(o), ldo, _p(cu_q), B, max_q, Nkv, H,
+                                         hd, scale, _stream()), "vit_attention_fwd_varlen")
