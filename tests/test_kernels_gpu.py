@@ -246,8 +246,9 @@ def test_attention(B, N, H, hd, path):
     assert rel(mv, gv) < 2e-2
 
 
-def test_im2col_and_embed_grad():
-    B, img, P, D = 2, 32, 8, 64
+@pytest.mark.parametrize("B,img,P,D", [(2, 32, 8, 64), (3, 224, 16, 768), (2, 224, 14, 1280), (2, 64, 32, 1024)])
+def test_im2col_and_embed_grad(B, img, P, D):
+    """vector paths (P % 8 == 0, D % 4 == 0) and the scalar fallback (P = 14)"""
     g = img // P
     N = g * g + 1
     K = 3 * P * P

@@ -52,15 +52,99 @@ __global__ void dropout_mask_kernel(DropDev drop, long row0, long rows, int cols
   if (r >= rows || c >= cols) return;
   out[r * ld + c] = drop.thr ? drop_mult1(drop, row0 + r, c) : 1.0f;
 }
-// dcls = dpos[0]; dconv_bias = sum_{n>=1} dpos[n]
-__global__ void cls_bias_grad_kernel(const float* __restrict__ dpos, int N, int D, float* __restrict__ dcls,
-                                     float* __restrict__ dbias) {
-  const int d = blockIdx.x * blockDim.x + threadIdx.x;
-  if (d >= D) return;
+
+// Vector forms of the two embedding kernels above (the common shapes: P % 8 == 0, D % 4 == 0).
+// im2col: one thread per 8 consecutive patch columns (8 adjacent pixels of one image row: two
+// 16-B loads, one 16-B bf16 store); the division chain runs once per 8 outputs instead of per output.
+template <typename OUT>
+__global__ void im2col8_kernel(const float* __restrict__ x, OUT* __restrict__ out, int B, int img, int P) {
+  const int g = img / P, N = g * g + 1, K8 = 3 * P * P / 8;
+  const long total = (long)B * N * K8;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int c8 = (int)(i % K8);
+    const long row = i / K8;
+    const int t = (int)(row % N), b = (int)(row / N);
+    float4 lo = make_float4(0.f, 0.f, 0.f, 0.f), hi = lo;
+    if (t > 0) {
+      const int patch = t - 1, py = patch / g, px = patch % g;
+      const int col = c8 * 8, c = col / (P * P), rem = col % (P * P), ky = rem / P, kx = rem % P;
+      const float4* src =
+          reinterpret_cast<const float4*>(x + (((long)b * 3 + c) * img + (py * P + ky)) * img + (px * P + kx));
+      lo = src[0];
+      hi = src[1];
+    }
+    if constexpr (sizeof(OUT) == 2) {
+      uint4 v;
+      v.x = (uint32_t)f2bf(lo.x) | ((uint32_t)f2bf(lo.y) << 16);
+      v.y = (uint32_t)f2bf(lo.z) | ((uint32_t)f2bf(lo.w) << 16);
+      v.z = (uint32_t)f2bf(hi.x) | ((uint32_t)f2bf(hi.y) << 16);
+      v.w = (uint32_t)f2bf(hi.z) | ((uint32_t)f2bf(hi.w) << 16);
+      reinterpret_cast<uint4*>(out)[i] = v;
+    } else {
+      reinterpret_cast<float4*>(out)[2 * i] = lo;
+      reinterpret_cast<float4*>(out)[2 * i + 1] = hi;
+    }
+  }
+}
+
+// dpos[n][d] = sum_b dh0[(b*N+n)*D + d]: workgroup (n, column slice) = 8 image groups x C4 float4
+// columns, the 8 partial rows summed through LDS. gridDim.y slices keep > 256 workgroups in flight.
+__global__ void __launch_bounds__(768) pos_grad4_kernel(const float* __restrict__ dh0, int B, int N, int D,
+                                                        float* __restrict__ dpos, DropDev drop) {
+  __shared__ float4 red[8][96];
+  const int C4 = D / 4 / gridDim.y;
+  const int n = blockIdx.x, c = threadIdx.x % C4, grp = threadIdx.x / C4;
+  const int d = (blockIdx.y * C4 + c) * 4;
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  const float* base = dh0 + (long)n * D + d;
+  const long bstride = (long)N * D;
+#pragma unroll 4
+  for (int b = grp; b < B; b += 8) {
+    float4 v = *reinterpret_cast<const float4*>(base + b * bstride);
+    if (drop.thr) {
+      const long r = (long)b * N + n;
+      v.x *= drop_mult1(drop, r, d);
+      v.y *= drop_mult1(drop, r, d + 1);
+      v.z *= drop_mult1(drop, r, d + 2);
+      v.w *= drop_mult1(drop, r, d + 3);
+    }
+    s.x += v.x;
+    s.y += v.y;
+    s.z += v.z;
+    s.w += v.w;
+  }
+  red[grp][c] = s;
+  __syncthreads();
+  if (grp == 0) {
+#pragma unroll
+    for (int k = 1; k < 8; ++k) {
+      s.x += red[k][c].x;
+      s.y += red[k][c].y;
+      s.z += red[k][c].z;
+      s.w += red[k][c].w;
+    }
+    *reinterpret_cast<float4*>(dpos + (long)n * D + d) = s;
+  }
+}
+
+// dcls = dpos[0]; dconv_bias = sum_{n>=1} dpos[n]: 16 columns x 16 row lanes per workgroup
+__global__ void __launch_bounds__(256) cls_bias_grad16_kernel(const float* __restrict__ dpos, int N, int D,
+                                                              float* __restrict__ dcls, float* __restrict__ dbias) {
+  __shared__ float red[16][17];
+  const int c = threadIdx.x & 15, r = threadIdx.x >> 4;
+  const int d = blockIdx.x * 16 + c;
   float s = 0.f;
-  for (int n = 1; n < N; ++n) s += dpos[(long)n * D + d];
-  dcls[d] = dpos[d];
-  dbias[d] = s;
+  if (d < D)
+    for (int n = 1 + r; n < N; n += 16) s += dpos[(long)n * D + d];
+  red[r][c] = s;
+  __syncthreads();
+  if (r == 0 && d < D) {
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) t += red[k][c];
+    dbias[d] = t;
+    dcls[d] = dpos[d];
+  }
 }
 
 // ---- column sums --------------------------------------------------------------------------------
@@ -143,58 +227,89 @@ __global__ void colsum_final_kernel(const float* __restrict__ partial, int chunk
 }
 
 // ---- f32 GEMM: classifier head of the bf16 step, and every projection of the fp32 (exact) forward.
-// 64 x 64 tile per 256-thread workgroup, 4 x 4 outputs per thread, k-tiles of 16 staged in LDS
-// (f32 operands, f32 accumulation: the reference's fp32 arithmetic, no bf16 rounding anywhere).
+// Exact f32 on the matrix core (v_mfma_f32_16x16x4_f32: f32 operands, f32 accumulation; no bf16
+// rounding anywhere). 32 x 32 output tile per 256-thread workgroup; the four waves split the K loop
+// (k-tiles of 16, wave w takes tiles w, w+4, ...) so narrow problems still fill the chip (the head:
+// 256 x 1000 x 768 = 256 workgroups), and their partial tiles are summed through LDS at the end.
+// Each wave stages its own k-tile (A 32x16, B 16x32) through a private LDS image with coalesced
+// loads in either operand layout; rows padded to 48 floats so the fragment reads are conflict-free.
+constexpr int GF_LD = 48;
 __global__ void __launch_bounds__(256) gemm_f32_kernel(int M, int N, int K, const float* __restrict__ A, long lda,
                                                        int at, const float* __restrict__ B, long ldb, int bt,
                                                        float* __restrict__ C, long ldc, const float* __restrict__ bias,
                                                        int accumulate) {
-  __shared__ float As[16][68], Bs[16][68];  // [k][m], [k][n]
-  const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
-  const int m0 = blockIdx.y * 64, n0 = blockIdx.x * 64;
-  float acc[4][4];
+  __shared__ float smem[4 * 2 * 16 * GF_LD];  // per wave: As[k][m], Bs[k][n]; reused for the reduction
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int m0 = blockIdx.y * 32, n0 = blockIdx.x * 32;
+  float* As = smem + wave * 2 * 16 * GF_LD;
+  float* Bs = As + 16 * GF_LD;
+  v4f acc[2][2];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = 0.f;
-  for (int k0 = 0; k0 < K; k0 += 16) {
+    for (int j = 0; j < 2; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+  const int nkt = (K + 15) / 16;
+  for (int kt = wave; kt < nkt; kt += 4) {
+    const int k0 = kt * 16;
+    float av[8], bv[8];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int idx = tid + e * 256;
+    for (int e = 0; e < 8; ++e) {
+      const int idx = lane + e * 64;
       int m, k;
-      if (at) { k = idx >> 6; m = idx & 63; } else { m = idx >> 4; k = idx & 15; }
+      if (at) { k = idx >> 5; m = idx & 31; } else { m = idx >> 4; k = idx & 15; }
       const int gm = m0 + m, gk = k0 + k;
-      As[k][m] = (gm < M && gk < K) ? (at ? A[(long)gk * lda + gm] : A[(long)gm * lda + gk]) : 0.f;
+      av[e] = (gm < M && gk < K) ? (at ? A[(long)gk * lda + gm] : A[(long)gm * lda + gk]) : 0.f;
       int n, kb;
-      if (bt) { n = idx >> 4; kb = idx & 15; } else { kb = idx >> 6; n = idx & 63; }
+      if (bt) { n = idx >> 4; kb = idx & 15; } else { kb = idx >> 5; n = idx & 31; }
       const int gn = n0 + n, gkb = k0 + kb;
-      Bs[kb][n] = (gn < N && gkb < K) ? (bt ? B[(long)gn * ldb + gkb] : B[(long)gkb * ldb + gn]) : 0.f;
+      bv[e] = (gn < N && gkb < K) ? (bt ? B[(long)gn * ldb + gkb] : B[(long)gkb * ldb + gn]) : 0.f;
     }
-    __syncthreads();
 #pragma unroll
-    for (int k = 0; k < 16; ++k) {
-      const float4 a = *reinterpret_cast<const float4*>(&As[k][ty * 4]);
-      const float4 b = *reinterpret_cast<const float4*>(&Bs[k][tx * 4]);
-      const float av[4] = {a.x, a.y, a.z, a.w}, bv[4] = {b.x, b.y, b.z, b.w};
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = fmaf(av[i], bv[j], acc[i][j]);
+    for (int e = 0; e < 8; ++e) {
+      const int idx = lane + e * 64;
+      if (at) As[(idx >> 5) * GF_LD + (idx & 31)] = av[e]; else As[(idx & 15) * GF_LD + (idx >> 4)] = av[e];
+      if (bt) Bs[(idx & 15) * GF_LD + (idx >> 4)] = bv[e]; else Bs[(idx >> 5) * GF_LD + (idx & 31)] = bv[e];
     }
-    __syncthreads();
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const int k = ks * 4 + (lane >> 4);
+      float a[2], b[2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        a[t] = As[k * GF_LD + t * 16 + (lane & 15)];
+        b[t] = Bs[k * GF_LD + t * 16 + (lane & 15)];
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
   }
+  // sum the four waves' partial tiles: red[w][row][col], row stride 33
+  __syncthreads();
+  float* red = smem;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int m = m0 + ty * 4 + i;
-    if (m >= M) continue;
+  for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int n = n0 + tx * 4 + j;
-      if (n >= N) continue;
-      const float v = acc[i][j] + (bias ? bias[n] : 0.f);
-      float* dst = C + (long)m * ldc + n;
-      *dst = accumulate ? *dst + v : v;
-    }
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        red[wave * 32 * 33 + (i * 16 + 4 * (lane >> 4) + r) * 33 + j * 16 + (lane & 15)] = acc[i][j][r];
+  __syncthreads();
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int idx = threadIdx.x + e * 256, row = idx >> 5, col = idx & 31;
+    const int m = m0 + row, n = n0 + col;
+    if (m >= M || n >= N) continue;
+    float v = red[row * 33 + col] + red[32 * 33 + row * 33 + col] + red[2 * 32 * 33 + row * 33 + col] +
+              red[3 * 32 * 33 + row * 33 + col];
+    if (bias) v += bias[n];
+    float* dst = C + (long)m * ldc + n;
+    *dst = accumulate ? *dst + v : v;
   }
 }
 
@@ -309,8 +424,12 @@ extern "C" int vit_im2col(const float* x, void* out, int64_t B, int64_t img, int
                           vit_stream_t stream) {
   VIT_CHECK_ARG(x && out && B > 0 && P > 0 && img >= P && Kpad >= 3 * P * P, "vit_im2col: bad args");
   const int64_t g = img / P, N = g * g + 1;
-  hipLaunchKernelGGL(im2col_kernel<bf16_t>, dim3(grid_for(B * N * Kpad)), dim3(256), 0, (hipStream_t)stream, x, (bf16_t*)out,
-                     (int)B, (int)img, (int)P, (int)Kpad);
+  if (P % 8 == 0 && img % 4 == 0 && Kpad == 3 * P * P && (uintptr_t)x % 16 == 0 && (uintptr_t)out % 16 == 0)
+    hipLaunchKernelGGL(im2col8_kernel<bf16_t>, dim3(grid_for(B * N * Kpad / 8)), dim3(256), 0, (hipStream_t)stream, x,
+                       (bf16_t*)out, (int)B, (int)img, (int)P);
+  else
+    hipLaunchKernelGGL(im2col_kernel<bf16_t>, dim3(grid_for(B * N * Kpad)), dim3(256), 0, (hipStream_t)stream, x,
+                       (bf16_t*)out, (int)B, (int)img, (int)P, (int)Kpad);
   VIT_LAUNCH_CHECK("vit_im2col");
 }
 
@@ -318,9 +437,21 @@ extern "C" int vit_embed_grad(const float* dh0, int64_t B, int64_t N, int64_t D,
                               float* dconv_bias, const vit_dropout* dropout, vit_stream_t stream) {
   VIT_CHECK_ARG(dh0 && dpos && dcls && dconv_bias && B > 0 && N > 0 && D > 0, "vit_embed_grad: bad args");
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(pos_grad_kernel, dim3((unsigned)((D + 255) / 256), (unsigned)N), dim3(256), 0, s, dh0, (int)B,
-                     (int)N, (int)D, dpos, make_drop(dropout));
-  hipLaunchKernelGGL(cls_bias_grad_kernel, dim3((unsigned)((D + 255) / 256)), dim3(256), 0, s, dpos, (int)N, (int)D,
+  int ys = 0;
+  if (D % 4 == 0 && ((uintptr_t)dh0 % 16) == 0 && ((uintptr_t)dpos % 16) == 0) {
+    // column slices of at most 96 float4 columns, at least 2 when the rows alone leave CUs idle
+    const int d4 = (int)(D / 4);
+    for (int y = (d4 + 95) / 96; y <= d4; ++y)
+      if (d4 % y == 0) { ys = y; break; }
+    if (ys == 1 && N < 256 && d4 % 2 == 0) ys = 2;
+  }
+  if (ys > 0)
+    hipLaunchKernelGGL(pos_grad4_kernel, dim3((unsigned)N, (unsigned)ys), dim3((unsigned)(8 * (D / 4 / ys))), 0, s, dh0,
+                       (int)B, (int)N, (int)D, dpos, make_drop(dropout));
+  else
+    hipLaunchKernelGGL(pos_grad_kernel, dim3((unsigned)((D + 255) / 256), (unsigned)N), dim3(256), 0, s, dh0, (int)B,
+                       (int)N, (int)D, dpos, make_drop(dropout));
+  hipLaunchKernelGGL(cls_bias_grad16_kernel, dim3((unsigned)((D + 15) / 16)), dim3(256), 0, s, dpos, (int)N, (int)D,
                      dcls, dconv_bias);
   VIT_LAUNCH_CHECK("vit_embed_grad");
 }
@@ -393,7 +524,7 @@ extern "C" int vit_gemm_f32(int64_t M, int64_t N, int64_t K, const float* A, int
                             int32_t accumulate, vit_stream_t stream) {
   VIT_CHECK_ARG(A && B && C && M >= 0 && N >= 0 && K >= 0, "vit_gemm_f32: bad args");
   if (M == 0 || N == 0) return VIT_OK;
-  dim3 grid((unsigned)((N + 63) / 64), (unsigned)((M + 63) / 64)), block(256);
+  dim3 grid((unsigned)((N + 31) / 32), (unsigned)((M + 31) / 32)), block(256);
   hipLaunchKernelGGL(gemm_f32_kernel, grid, block, 0, (hipStream_t)stream, (int)M, (int)N, (int)K, A, (long)lda,
                      (int)a_trans, B, (long)ldb, (int)b_trans, C, (long)ldc, bias, (int)accumulate);
   VIT_LAUNCH_CHECK("vit_gemm_f32");
@@ -541,8 +672,12 @@ extern "C" int vit_im2col_f32(const float* x, float* out, int64_t B, int64_t img
                               vit_stream_t stream) {
   VIT_CHECK_ARG(x && out && B > 0 && P > 0 && img >= P && Kpad >= 3 * P * P, "vit_im2col_f32: bad args");
   const int64_t g = img / P, N = g * g + 1;
-  hipLaunchKernelGGL(im2col_kernel<float>, dim3(grid_for(B * N * Kpad)), dim3(256), 0, (hipStream_t)stream, x, out,
-                     (int)B, (int)img, (int)P, (int)Kpad);
+  if (P % 8 == 0 && img % 4 == 0 && Kpad == 3 * P * P && (uintptr_t)x % 16 == 0 && (uintptr_t)out % 16 == 0)
+    hipLaunchKernelGGL(im2col8_kernel<float>, dim3(grid_for(B * N * Kpad / 8)), dim3(256), 0, (hipStream_t)stream, x,
+                       out, (int)B, (int)img, (int)P);
+  else
+    hipLaunchKernelGGL(im2col_kernel<float>, dim3(grid_for(B * N * Kpad)), dim3(256), 0, (hipStream_t)stream, x, out,
+                       (int)B, (int)img, (int)P, (int)Kpad);
   VIT_LAUNCH_CHECK("vit_im2col_f32");
 }
 
