@@ -213,7 +213,9 @@ ATTN_CASES = [(2, 197, 12, 64, 0), (3, 17, 2, 32, 0), (2, 50, 4, 64, 0), (1, 5, 
               # K/V-tiled path (ops.ATTN_TILED): forced at ViT-224 sizes, and the 384-px sequences it exists for
               # (B/16, L/16 @384: 577 tokens; H/14 @384: 730 tokens, hd 80)
               (2, 197, 3, 64, 2), (2, 257, 2, 80, 2), (3, 17, 2, 32, 2), (1, 65, 2, 48, 2), (2, 33, 2, 96, 2),
-              (2, 577, 3, 64, 0), (1, 730, 2, 80, 0), (1, 321, 2, 64, 0)]
+              (2, 577, 3, 64, 0), (1, 730, 2, 80, 0), (1, 321, 2, 64, 0),
+              # more (image, head) items than CUs: the persistent backward's workgroups walk several items
+              (24, 197, 12, 64, 0), (23, 50, 12, 64, 0)]
 
 
 @pytest.mark.parametrize("B,N,H,hd,path", ATTN_CASES)
@@ -403,7 +405,7 @@ def test_gemm_wave_split_rows(epi, K):
 
 
 @pytest.mark.parametrize("B,N,H,hd,path", [(2, 197, 3, 64, 0), (2, 257, 2, 80, 0), (1, 50, 2, 32, 0),
-                                           (2, 197, 3, 64, 2), (1, 577, 2, 80, 0)])
+                                           (2, 197, 3, 64, 2), (1, 577, 2, 80, 0), (24, 197, 12, 64, 0)])
 def test_attention_query_rows_match_full(B, N, H, hd, path):
     """q_rows = 1 (the last layer's cls query): o / lse of the first 32-query pair equal the full
     run; with dO zero past row 0, dK / dV / bias partials are bit-identical to the full backward and

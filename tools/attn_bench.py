@@ -43,8 +43,9 @@ def run(B, N, H, hd, path):
     us = bench(lambda: ops.attention_fwd(qkv, o, lse, B, N, H, hd, hd ** -0.5, path=path))
     print(f"B{B} N{N} H{H} hd{hd} path{path} fwd {us:7.1f} us {fl / us / 1e6:6.1f} TF/s {by_f / us / 1e6:5.2f} TB/s",
           flush=True)
+    nq = int(os.environ.get("ATTN_QROWS", N))  # q_rows (1: the pruned last layer's cls query pair)
     us = bench(lambda: ops.attention_bwd(qkv, o, do, lse, dqkv, B, N, H, hd, hd ** -0.5, bias_partial=bp, path=path,
-                                         workspace=ws))
+                                         workspace=ws, q_rows=nq))
     print(f"B{B} N{N} H{H} hd{hd} path{path} bwd {us:7.1f} us {2.5 * fl / us / 1e6:6.1f} TF/s "
           f"{by_b / us / 1e6:5.2f} TB/s", flush=True)
 

@@ -999,7 +999,8 @@ __global__ void __launch_bounds__(NW * 64, 2) attn_bwd_kernel(const bf16_t* __re
 
   // ---- stage 2: dK and dV, key-tile pairs ----
   if (!(stages & 2)) return;  // diagnostic timing of stage 1 alone (VIT_ATTN_BWD_STAGES)
-  load_images<HD, NP, NW * 64>(ImA, base, rs, ImB, dob, D, N, hd);  // Q, dO
+  // Q, dO: only the query pairs stage 2 visits (rows past nqa read as zeros without a memory access)
+  load_images<HD, NP, NW * 64>(ImA, base, rs, ImB, dob, D, min(N, 32 * npair_q), hd);
   __syncthreads();
   // the last query pair may hold one wholly padded 16-row tile (N % 32 in 1..16): its S / dP
   // products are skipped (P = dS = 0 there)
@@ -1135,6 +1136,304 @@ __global__ void __launch_bounds__(NW * 64, 2) attn_bwd_kernel(const bf16_t* __re
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// Persistent backward (HD <= 64, N <= 224): one 512-thread workgroup per CU walks the (image, head)
+// items. Seven compute waves run the two stages of attn_bwd_kernel above (stage 1: 16-query strips,
+// exact delta = sum_j P dP and dQ; stage 2: one 32-key pair per wave, dK / dV); the eighth wave is a
+// loader that moves the images the compute waves need NEXT into LDS by LDS-DMA while they work:
+// Q / dO of the current item during stage 1, K / V of the next item during stage 2. No image load
+// sits on the critical path (the one-shot kernel's load -> sync -> compute phases cost ~200 us of
+// its ~300 us in the B/16 step: the q_rows = 1 layer, almost no math, took 200 us), and the compute
+// waves' own vmcnt waits (their Q / dO strip rows) never cover the DMA, which the loader alone
+// waits for. Outputs leave through wave-private LDS strips as whole 128-B rows (StripOut).
+template <int HD, int NKT>
+__global__ void __launch_bounds__(512, 1) attn_bwd_p_kernel(const bf16_t* __restrict__ qkv,
+                                                            const bf16_t* __restrict__ dout,
+                                                            const float* __restrict__ lse, bf16_t* __restrict__ dqkv,
+                                                            float* __restrict__ bias_partial, int B, int N, int H,
+                                                            int hd, float scale, int nq) {
+  constexpr int NP = NKT * 16, IMG = NP * HD * 2, NCW = 7;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* ImK = smem;
+  char* ImV = smem + IMG;
+  char* ImQ = smem + 2 * IMG;
+  char* ImO = smem + 3 * IMG;
+  float* lse_s0 = reinterpret_cast<float*>(smem + 4 * IMG);  // [2][NP], by item parity
+  float* dlt_s = lse_s0 + 2 * NP;                             // [NP]
+  float* bsum0 = dlt_s + NP;                                  // [2][NCW][3][HD], by item parity
+  lds_t* strips = (lds_t*)(bsum0 + 2 * NCW * 3 * HD);         // [NCW] StripOut buffers
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const bool loader = wave == NCW;
+  const int g = lane >> 4, i = lane & 15;
+  const int D = H * hd;
+  const long rs = 3L * D;
+  const float c = scale * LOG2E;
+  const int items = B * H;
+  const int nqt = (N + 15) / 16, npair = (N + 31) / 32;
+  const int nqa = min(N, (nq + 31) / 32 * 32);
+  const int npair_q = (nqa + 31) / 32;
+  const bool last_half = (2 * npair - 1) * 16 >= N;
+  lds_t* so = strips + (wave < NCW ? wave : 0) * StripOut<HD>::BYTES;
+
+  // loader: rows [0, rows_img) of a [N][hd] slice (row stride ld) into a swizzled image; rows >= N and
+  // columns >= hd land as zeros (out of the descriptor's range). One 1-KiB LDS-DMA per RPI rows:
+  // lane L fills image row r0 + L / CPR at chunk position L % CPR, i.e. source chunk (L % CPR) ^ swizzle.
+  auto dma = [&](char* img, const bf16_t* src, long ld, int rows_img) {
+    constexpr int CPR = HD / 8, RPI = 64 / CPR;
+    const __amdgpu_buffer_rsrc_t rsc = make_rsrc(src, (uint32_t)(((long)(N - 1) * ld + hd) * 2));
+    const int rl = lane / CPR, pc = lane % CPR;
+    for (int r0 = 0; r0 < rows_img; r0 += RPI) {
+      const int r = r0 + rl;
+      const int ch = pc ^ aswz<HD>(r);
+      const int off = (r < N && ch * 8 < hd) ? (int)(((long)r * ld + ch * 8) * 2) : 0x7ffffff0;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsc, LDS_PTR(void, img + r0 * HD * 2), 16, off, 0, 0, 0);
+    }
+  };
+  auto load_lse = [&](int it, float* dst) {
+    for (int r = lane; r < NP; r += 64) dst[r] = r < N ? lse[(long)it * N + r] * LOG2E : INFINITY;
+  };
+  auto kv_base = [&](int it) { return qkv + (long)(it / H) * N * rs + (long)(it % H) * hd; };
+
+  const int it0 = blockIdx.x;
+  if (loader && it0 < items) {
+    const bf16_t* base = kv_base(it0);
+    dma(ImK, base + D, rs, NP);
+    dma(ImV, base + 2 * D, rs, NP);
+    load_lse(it0, lse_s0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+
+  int par = 0;
+  for (int it = it0; it < items; it += gridDim.x, par ^= 1) {
+    const int b = it / H, h = it % H;
+    const bf16_t* base = kv_base(it);
+    const bf16_t* dob = dout + (long)b * N * D + (long)h * hd;
+    bf16_t* dq_base = dqkv + (long)b * N * rs + (long)h * hd;
+    const float* lse_s = lse_s0 + par * NP;
+    float* bsum = bsum0 + par * NCW * 3 * HD;
+
+    // ---- phase 1: stage 1 on K / V images; the loader brings Q / dO ----
+    if (loader) {
+      dma(ImQ, base, rs, 32 * npair_q);
+      dma(ImO, dob, D, 32 * npair_q);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+      if (i == 0) {
+#pragma unroll
+        for (int dt = 0; dt < HD / 16; ++dt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) bsum[(wave * 3 + 0) * HD + dt * 16 + 4 * g + r] = 0.f;
+      }
+      v8bf qn[HD / 32], dn[HD / 32];  // next strip's Q / dO rows, requested one strip ahead
+#pragma unroll
+      for (int kk = 0; kk < HD / 32; ++kk) {
+        qn[kk] = gl_row<HD>(base, rs, wave * 16, kk, N, hd, lane);
+        dn[kk] = gl_row<HD>(dob, D, wave * 16, kk, N, hd, lane);
+      }
+      for (int qt = wave; qt < nqt; qt += NCW) {
+        if (qt * 16 >= nqa) {  // no gradient reaches these queries: dQ = 0, delta = 0
+          if (g == 0) dlt_s[qt * 16 + i] = 0.f;
+          v4f z[HD / 16];
+#pragma unroll
+          for (int dt = 0; dt < HD / 16; ++dt) z[dt] = v4f{0.f, 0.f, 0.f, 0.f};
+          StripOut<HD>::stage(so, z, 1.0f, lane);
+          StripOut<HD>::store(so, dq_base + (long)qt * 16 * rs, rs, N - qt * 16, hd, lane);
+          continue;
+        }
+        v8bf qf[HD / 32], df[HD / 32];
+#pragma unroll
+        for (int kk = 0; kk < HD / 32; ++kk) {
+          qf[kk] = qn[kk];
+          df[kk] = dn[kk];
+          qn[kk] = gl_row<HD>(base, rs, (qt + NCW) * 16, kk, N, hd, lane);
+          dn[kk] = gl_row<HD>(dob, D, (qt + NCW) * 16, kk, N, hd, lane);
+        }
+        const float ls = lse_s[qt * 16 + i];
+        v4f P[NKT], DP[NKT];
+        float dl = 0.f;
+#pragma unroll
+        for (int kt = 0; kt < NKT; ++kt) {
+          if (kt == NKT - 1 && kt * 16 >= N) {  // a wholly padded last key tile
+            P[kt] = DP[kt] = v4f{0.f, 0.f, 0.f, 0.f};
+            continue;
+          }
+          v4f st = {0.f, 0.f, 0.f, 0.f}, dpt = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int kk = 0; kk < HD / 32; ++kk) {
+            st = mfma(rd_row<HD>(ImK, kt * 16, kk, lane), qf[kk], st);
+            dpt = mfma(rd_row<HD>(ImV, kt * 16, kk, lane), df[kk], dpt);
+          }
+          const bool full = (kt + 1) * 16 <= N;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float pv = ex2(st[r] * c - ls);
+            if (!full && kt * 16 + 4 * g + r >= N) pv = 0.f;
+            P[kt][r] = pv;
+            dl += pv * dpt[r];
+          }
+          DP[kt] = dpt;
+        }
+        dl += __shfl_xor(dl, 16, 64);
+        dl += __shfl_xor(dl, 32, 64);
+        const int q = qt * 16 + i;
+        if (q >= N) dl = 0.f;
+        if (g == 0) dlt_s[q] = dl;
+        v4f dq[HD / 16];
+#pragma unroll
+        for (int dt = 0; dt < HD / 16; ++dt) dq[dt] = v4f{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < NKT / 2; ++ks) {
+          v4f d0, d1;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            d0[r] = P[2 * ks][r] * (DP[2 * ks][r] - dl);
+            d1[r] = P[2 * ks + 1][r] * (DP[2 * ks + 1][r] - dl);
+          }
+          const v8bf bD = pack8(d0, d1);
+#pragma unroll
+          for (int dt = 0; dt < HD / 16; ++dt)
+            dq[dt] = mfma(rd_tr<HD>(ImK, 2 * ks, 2 * ks + 1, dt * 16, lane), bD, dq[dt]);
+        }
+        StripOut<HD>::stage(so, dq, scale, lane);
+        StripOut<HD>::store(so, dq_base + (long)qt * 16 * rs, rs, N - qt * 16, hd, lane);
+        if (bias_partial) {  // the strip's dQ column sums (padded queries: dS = 0) into the wave's slot
+#pragma unroll
+          for (int dt = 0; dt < HD / 16; ++dt)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const float v = sum16(dq[dt][r]);
+              if (i == 0) bsum[(wave * 3 + 0) * HD + dt * 16 + 4 * g + r] += v * scale;
+            }
+        }
+      }
+    }
+    __syncthreads();  // Q / dO images landed; delta complete; K / V images read by stage 1
+
+    // ---- phase 2: each compute wave takes its key pair's K / V rows into registers ----
+    const int kp = wave;
+    const bool has_kp = !loader && kp < npair;
+    v8bf kf[2][HD / 32], vf[2][HD / 32];
+    if (has_kp) {
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int kk = 0; kk < HD / 32; ++kk) {
+          kf[t][kk] = rd_row<HD>(ImK, (2 * kp + t) * 16, kk, lane);
+          vf[t][kk] = rd_row<HD>(ImV, (2 * kp + t) * 16, kk, lane);
+        }
+    }
+    __syncthreads();  // K / V images free for the next item
+
+    // ---- phase 3: stage 2 on Q / dO images; the loader brings the next item's K / V ----
+    if (loader) {
+      const int nxt = it + gridDim.x;
+      if (nxt < items) {
+        const bf16_t* nb = kv_base(nxt);
+        dma(ImK, nb + D, rs, NP);
+        dma(ImV, nb + 2 * D, rs, NP);
+        load_lse(nxt, lse_s0 + (par ^ 1) * NP);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+      if (i == 0) {
+#pragma unroll
+        for (int dt = 0; dt < HD / 16; ++dt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            bsum[(wave * 3 + 1) * HD + dt * 16 + 4 * g + r] = bsum[(wave * 3 + 2) * HD + dt * 16 + 4 * g + r] = 0.f;
+      }
+      if (has_kp) {
+        v4f dv[2][HD / 16], dk[2][HD / 16];
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int dt = 0; dt < HD / 16; ++dt) dv[t][dt] = dk[t][dt] = v4f{0.f, 0.f, 0.f, 0.f};
+        for (int qs = 0; qs < npair_q; ++qs) {
+          v4f P[2][2], DS[2][2];  // [key tile][query tile]
+#pragma unroll
+          for (int u = 0; u < 2; ++u) {
+            const int qt = 2 * qs + u;
+            if (u == 1 && last_half && qs == npair - 1) {
+              P[0][1] = P[1][1] = DS[0][1] = DS[1][1] = v4f{0.f, 0.f, 0.f, 0.f};
+              continue;
+            }
+            v8bf qr[HD / 32], orow[HD / 32];
+#pragma unroll
+            for (int kk = 0; kk < HD / 32; ++kk) {
+              qr[kk] = rd_row<HD>(ImQ, qt * 16, kk, lane);
+              orow[kk] = rd_row<HD>(ImO, qt * 16, kk, lane);
+            }
+            const v4f lq = *reinterpret_cast<const v4f*>(lse_s + qt * 16 + 4 * g);
+            const v4f dq4 = *reinterpret_cast<const v4f*>(dlt_s + qt * 16 + 4 * g);
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+              v4f sv = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+              for (int kk = 0; kk < HD / 32; ++kk) {
+                sv = mfma(qr[kk], kf[t][kk], sv);
+                dp = mfma(orow[kk], vf[t][kk], dp);
+              }
+              const bool kvalid = (2 * kp + t) * 16 + i < N;
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                const float pp = kvalid ? ex2(sv[r] * c - lq[r]) : 0.f;
+                P[t][u][r] = pp;
+                DS[t][u][r] = pp * (dp[r] - dq4[r]);
+              }
+            }
+          }
+          const v8bf bP0 = pack8(P[0][0], P[0][1]), bP1 = pack8(P[1][0], P[1][1]);
+          const v8bf bD0 = pack8(DS[0][0], DS[0][1]), bD1 = pack8(DS[1][0], DS[1][1]);
+#pragma unroll
+          for (int dt = 0; dt < HD / 16; ++dt) {
+            const v8bf ot = rd_tr<HD>(ImO, 2 * qs, 2 * qs + 1, dt * 16, lane);
+            const v8bf qtr = rd_tr<HD>(ImQ, 2 * qs, 2 * qs + 1, dt * 16, lane);
+            dv[0][dt] = mfma(ot, bP0, dv[0][dt]);
+            dv[1][dt] = mfma(ot, bP1, dv[1][dt]);
+            dk[0][dt] = mfma(qtr, bD0, dk[0][dt]);
+            dk[1][dt] = mfma(qtr, bD1, dk[1][dt]);
+          }
+        }
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          const int k0 = (2 * kp + t) * 16;
+          if (k0 < N) {
+            StripOut<HD>::stage(so, dk[t], scale, lane);
+            StripOut<HD>::store(so, dq_base + (long)k0 * rs + D, rs, N - k0, hd, lane);
+            StripOut<HD>::stage(so, dv[t], 1.0f, lane);
+            StripOut<HD>::store(so, dq_base + (long)k0 * rs + 2 * D, rs, N - k0, hd, lane);
+          }
+        }
+        if (bias_partial) {  // invalid keys hold exact zeros (P = 0)
+#pragma unroll
+          for (int dt = 0; dt < HD / 16; ++dt)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const float a = sum16(dk[0][dt][r] + dk[1][dt][r]), v = sum16(dv[0][dt][r] + dv[1][dt][r]);
+              if (i == 0) {
+                bsum[(wave * 3 + 1) * HD + dt * 16 + 4 * g + r] = a * scale;
+                bsum[(wave * 3 + 2) * HD + dt * 16 + 4 * g + r] = v;
+              }
+            }
+        }
+      }
+    }
+    __syncthreads();  // item done: Q / dO images and delta free; next K / V and lse landed
+    if (loader && bias_partial) {
+      for (int e = lane; e < 3 * HD; e += 64) {
+        const int z = e / HD, d = e % HD;
+        if (d >= hd) continue;
+        float acc = 0.f;
+#pragma unroll
+        for (int w = 0; w < NCW; ++w) acc += bsum[(w * 3 + z) * HD + d];
+        bias_partial[(long)b * 3 * D + z * D + h * hd + d] = acc;
+      }
+    }
+  }
+}
+
 template <int HD, int NKT, int NW>
 hipError_t launch_fwd_nw(const bf16_t* qkv, bf16_t* o, float* lse, int B, int N, int H, int hd, float scale,
                          int nq, hipStream_t s) {
@@ -1231,6 +1530,26 @@ hipError_t launch_bwd_nw(const bf16_t* qkv, const bf16_t* dout, const float* lse
   return hipGetLastError();
 }
 
+template <int HD, int NKT>
+hipError_t launch_bwd_p(const bf16_t* qkv, const bf16_t* dout, const float* lse, bf16_t* dqkv, float* bias_partial,
+                        int B, int N, int H, int hd, float scale, int nq, hipStream_t s) {
+  constexpr int NP = NKT * 16;
+  const size_t lds = (size_t)4 * NP * HD * 2 + (size_t)3 * NP * 4 + (size_t)2 * 7 * 3 * HD * 4 +
+                     (size_t)7 * StripOut<HD>::BYTES;
+  auto kern = attn_bwd_p_kernel<HD, NKT>;
+  (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  static const int ncu = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      return 256;
+    return n;
+  }();
+  const int items = B * H;
+  hipLaunchKernelGGL(kern, dim3(items < ncu ? items : ncu), dim3(512), lds, s, qkv, dout, lse, dqkv, bias_partial, B, N,
+                     H, hd, scale, nq);
+  return hipGetLastError();
+}
+
 template <int HD, int NKT16>
 hipError_t launch_bwd2(const bf16_t* qkv, const bf16_t* dout, const float* lse, float* delta, bf16_t* dqkv,
                        float* bias_partial, int B, int N, int H, int hd, float scale, int nq, hipStream_t s) {
@@ -1256,11 +1575,14 @@ hipError_t launch_bwd(const bf16_t* qkv, const bf16_t* o, const bf16_t* dout, co
                       hipStream_t s) {
   (void)o;
   // VIT_ATTN_BWD_VARIANT: 2 = the single-kernel two-stage form (default: 272 us in the B/16 bs256 step
-  // against 294 us for the two-kernel form, profiles/r02), 0 = the lean two-kernel form
+  // against 294 us for the two-kernel form), 0 = the lean two-kernel form, 3 = the persistent
+  // loader-wave form (HD <= 64, N <= 224; measured slower: 424 vs 341 us standalone at B/16 bs256,
+  // 274 vs 209 us at q_rows = 1, profiles/r02/attn_bwd_variants.txt)
   static const int var = [] {
     const char* e = getenv("VIT_ATTN_BWD_VARIANT");
     return e ? atoi(e) : 2;
   }();
+  if (var == 3 && HD <= 64 && NKT <= 14) return launch_bwd_p<HD, NKT>(qkv, dout, lse, dqkv, bias_partial, B, N, H, hd, scale, nq, s);
   if (var == 0 && HD <= 64 && delta) {
     if ((N + 15) / 16 == NKT) return launch_bwd2<HD, NKT>(qkv, dout, lse, delta, dqkv, bias_partial, B, N, H, hd,
                                                          scale, nq, s);

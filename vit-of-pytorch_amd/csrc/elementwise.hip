@@ -249,27 +249,32 @@ __global__ void __launch_bounds__(256) gemm_f32_kernel(int M, int N, int K, cons
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
   const int nkt = (K + 15) / 16;
-  for (int kt = wave; kt < nkt; kt += 4) {
+  // the wave's next k-tile is loaded into registers while the current one is multiplied
+  auto load = [&](int kt, float* av, float* bv) {
     const int k0 = kt * 16;
-    float av[8], bv[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       const int idx = lane + e * 64;
       int m, k;
       if (at) { k = idx >> 5; m = idx & 31; } else { m = idx >> 4; k = idx & 15; }
       const int gm = m0 + m, gk = k0 + k;
-      av[e] = (gm < M && gk < K) ? (at ? A[(long)gk * lda + gm] : A[(long)gm * lda + gk]) : 0.f;
+      av[e] = (kt < nkt && gm < M && gk < K) ? (at ? A[(long)gk * lda + gm] : A[(long)gm * lda + gk]) : 0.f;
       int n, kb;
       if (bt) { n = idx >> 4; kb = idx & 15; } else { kb = idx >> 5; n = idx & 31; }
       const int gn = n0 + n, gkb = k0 + kb;
-      bv[e] = (gn < N && gkb < K) ? (bt ? B[(long)gn * ldb + gkb] : B[(long)gkb * ldb + gn]) : 0.f;
+      bv[e] = (kt < nkt && gn < N && gkb < K) ? (bt ? B[(long)gn * ldb + gkb] : B[(long)gkb * ldb + gn]) : 0.f;
     }
+  };
+  float av[8], bv[8];
+  load(wave, av, bv);
+  for (int kt = wave; kt < nkt; kt += 4) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       const int idx = lane + e * 64;
       if (at) As[(idx >> 5) * GF_LD + (idx & 31)] = av[e]; else As[(idx & 15) * GF_LD + (idx >> 4)] = av[e];
       if (bt) Bs[(idx & 15) * GF_LD + (idx >> 4)] = bv[e]; else Bs[(idx >> 5) * GF_LD + (idx & 31)] = bv[e];
     }
+    load(kt + 4, av, bv);
     __builtin_amdgcn_wave_barrier();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll

@@ -33,6 +33,10 @@ def _rup(x, m):
     return (x + m - 1) // m * m
 
 
+# workgroups a split-K weight gradient aims for (one per CU); VIT_WGRAD_TARGET for tuning sweeps
+_WGRAD_TARGET = int(os.environ.get("VIT_WGRAD_TARGET", "256"))
+
+
 @dataclass(frozen=True)
 class ArchConfig:
     image_size: int = 224
@@ -315,7 +319,7 @@ class ViTEngine:
         split (tools/gemm_bench.py: fc1/fc2 wgrad at split 7 = 36 x 7 = 252 workgroups)."""
         tiles = ((M + 255) // 256) * ((N + 255) // 256) * z
         nkt = K // 64
-        return max(1, min(round(256 / tiles), nkt // 8, 32))
+        return max(1, min(round(_WGRAD_TARGET / tiles), nkt // 8, 32))
 
     def _workspace(self, numel):
         if self._ws is None or self._ws.numel() < numel:
