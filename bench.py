@@ -128,6 +128,8 @@ def main():
     ap.add_argument("--num-classes", type=int, default=1000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
+    ap.add_argument("--grad-compress", choices=["none", "bf16"], default="none",
+                    help="N>1: all-reduce the gradient buckets in bf16 (vitmi.dist compress='bf16')")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -159,7 +161,9 @@ def main():
     x = torch.randn(b, 3, args.image_size, args.image_size, device=dev, generator=g)
     y = torch.randint(0, args.num_classes, (b,), device=dev, generator=g)
     mom_buf = torch.zeros_like(eng.flat)
-    reducer = GradAllReducer(eng, average=False).attach() if world > 1 else None  # CE pre-scaled by 1/(b*world)
+    compress = None if args.grad_compress == "none" else args.grad_compress
+    reducer = (GradAllReducer(eng, average=False, compress=compress).attach()  # CE pre-scaled by 1/(b*world)
+               if world > 1 else None)
     total_steps = args.warmup + args.steps
     # OneCycleLR schedule scalars as configured by reference src/train.py:159-163 (lr .03, 500 warmup/15000)
     from torch.optim.lr_scheduler import OneCycleLR
@@ -239,7 +243,8 @@ def main():
                                f"{'RCCL all-reduce+' if world > 1 else ''}SGD-momentum/OneCycleLR)",
                    "model": f"ViT-{args.arch.upper()}", "image_size": args.image_size, "per_gpu_batch": b,
                    "global_batch": b * world, "seq_len": cfg.tokens, "num_classes": args.num_classes,
-                   "parallelism": f"dp{world}"},
+                   "parallelism": f"dp{world}",
+                   **({"grad_allreduce_dtype": "bf16"} if compress and world > 1 else {})},
         "roofline": {"bound": "mfma", "kernel": "gemm fc1 fwd (bias + GELU + GELU' epilogue), "
                                                 f"M={T} N={cfg.mlp_dim} K={cfg.emb_dim}",
                      "achieved": round(fc1_tflops, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",

@@ -36,13 +36,13 @@ class _FakeEngine:
                 self.grad_ready_hook(self.grad, name, s, e)
 
 
-def _worker(rank, world, port, sizes, average, q):
+def _worker(rank, world, port, sizes, average, q, compress=None):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from vitmi.dist import GradAllReducer
     eng = _FakeEngine(sizes)
-    red = GradAllReducer(eng, min_bucket_elems=50, average=average).attach()
+    red = GradAllReducer(eng, min_bucket_elems=50, average=average, compress=compress).attach()
     for _ in range(2):  # two steps: buckets re-used
         eng.backward(rank)
         red.finish()
@@ -59,14 +59,14 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("average", [True, False])
-def test_grad_allreduce_gloo_world2(average):
+@pytest.mark.parametrize("average,compress", [(True, None), (False, None), (True, "bf16")])
+def test_grad_allreduce_gloo_world2(average, compress):
     world = 2
     sizes = [10, 100, 100, 100, 37]  # head (coalesced with layer2: below min_bucket), layers, embed
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, sizes, average, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, sizes, average, q, compress)) for r in range(world)]
     for p in procs:
         p.start()
     res = dict(q.get(timeout=120) for _ in range(world))
@@ -76,6 +76,8 @@ def test_grad_allreduce_gloo_world2(average):
     n = sum(sizes)
     base = torch.arange(n, dtype=torch.float32)
     expect = base * (1 + 2) / (world if average else 1)
+    if compress == "bf16":  # each rank's bucket and the sum rounded to bf16
+        expect = ((base.bfloat16().float() + (base * 2).bfloat16().float()).bfloat16().float()) / world
     for r in range(world):
         assert torch.allclose(res[r], expect), r
     assert torch.equal(res[0], res[1])  # replicas bit-identical

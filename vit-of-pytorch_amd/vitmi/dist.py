@@ -13,6 +13,12 @@ cross entropy yields the global-batch mean gradient of the reference's DataParal
 the gathered batch). With average=False the buckets are summed (the caller pre-scales the loss by
 1/(b*world), as bench.py does). Replicas stay bit-identical because every rank applies the same SGD
 update to the same all-reduced gradient.
+
+compress="bf16" halves the exchanged bytes (ViT-L/16: 1.22 GB of f32 gradients per step, ViT-H/14:
+2.53 GB, at ~153 GB/s per xGMI link): each bucket is cast to bf16 on the exchange stream (HIP cast
+kernel), all-reduced in bf16 and widened back into the f32 gradient buffer (HIP unpack kernel) before
+the optimizer reads it. The sum is rounded to bf16 at every ring step (relative error ~2^-9 x ranks),
+the trade the reference's DataParallel never offered; off by default.
 """
 from __future__ import annotations
 
@@ -21,8 +27,13 @@ import torch.distributed as dist
 
 
 class GradAllReducer:
-    def __init__(self, engine, group=None, min_bucket_elems=1 << 20, average=True):
+    def __init__(self, engine, group=None, min_bucket_elems=1 << 20, average=True, compress=None):
+        if compress not in (None, "bf16"):
+            raise ValueError(f"compress must be None or 'bf16', got {compress!r}")
         self.engine = engine
+        self.compress = compress
+        self._stage = None  # bf16 staging copy of the flat gradient buffer (compress="bf16")
+        self._widen = []    # (f32 slice, bf16 slice) pairs still to be widened (CPU / async path)
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.average = average
@@ -44,6 +55,11 @@ class GradAllReducer:
         self.engine.grad_ready_hook = None
         self.engine.grad_ready_finish = None
 
+    def _staging(self, buf, start, end):
+        if self._stage is None or self._stage.numel() < buf.numel():
+            self._stage = torch.empty(buf.numel(), device=buf.device, dtype=torch.bfloat16)
+        return self._stage[start:end]
+
     def _launch(self, buf, start, end, events=()):
         t = buf[start:end]
         op = dist.ReduceOp.AVG if self.native_avg else dist.ReduceOp.SUM
@@ -57,8 +73,20 @@ class GradAllReducer:
             for ev in events:  # the bucket's producers (main and side streams of the engine)
                 self.stream.wait_event(ev)
             with torch.cuda.stream(self.stream):
-                dist.all_reduce(t, op=op, group=self.group)
+                if self.compress:
+                    from . import ops
+                    tb = self._staging(buf, start, end)
+                    ops.cast_bf16(t, tb, end - start)
+                    dist.all_reduce(tb, op=op, group=self.group)
+                    ops.unpack_bf16_f32(tb, end - start, 1, end - start, t, end - start)
+                else:
+                    dist.all_reduce(t, op=op, group=self.group)
         else:
+            if self.compress:
+                tb = self._staging(buf, start, end)
+                tb.copy_(t)
+                self._widen.append((t, tb))
+                t = tb
             self._works.append(dist.all_reduce(t, op=op, group=self.group, async_op=True))
 
     def hook(self, buf, name, start, end, events=()):
@@ -82,6 +110,9 @@ class GradAllReducer:
             for w in self._works:
                 w.wait()
             self._works = []
+            for t, tb in self._widen:
+                t.copy_(tb)
+            self._widen = []
         for t in self._to_scale:
             t.mul_(1.0 / self.world)
         self._to_scale = []
