@@ -1,7 +1,8 @@
 """Generate tests/golden/resvit_tiny.npz from the reference Res-ViT itself (res-vit/model.py).
 
 Run HERE (the container that has /root/reference mounted):
-    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_resvit_golden.py
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_resvit_golden.py          # resvit_tiny.npz
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_resvit_golden.py --b16    # resvit_b16.npz
 
 Imports the reference's own `res-vit/model.py` (+ `model_utils.py`; einops is installed) and runs its
 `Transformer` on a tiny configuration with every Res-ViT feature on (use_lora, use_reslr, two blocks of
@@ -18,6 +19,13 @@ end-to-end comparison (a decision whose logit margin is below bf16 noise would o
 Weights: the reference constructor under torch.manual_seed(42), then a deterministic well-conditioned
 rescale (the parity protocol of SURVEY.md §8c, extended to the Res-ViT modules; see tame()). Data only;
 no reference source is copied. The GPU box never runs this script.
+
+--b16: BASELINE config C5's model, Res-ViT-B/16 @224 with the res-vit/config.py training defaults
+(LoRA rank 8 + residual low-rank paths, router from layer 2, active target 0.6, block size 1, 100
+classes), batch 2. Too large to store its weights, so the fixture holds per-tensor fingerprints
+(f64 sum and sum of squares) of the seed-42 + tame() parameters, the eval / train outputs, every
+router call's hard decisions and Gumbel draws (for replay), and per-parameter gradient norms; the
+inputs are regenerated from a seeded CPU generator (INPUT_SEED).
 """
 import importlib.util
 import json
@@ -37,6 +45,21 @@ CFG = dict(dim=64, mlp_dim=128, n_layers=5, n_heads=2, n_kv_heads=2, norm_eps=1e
            low_rank_dim=16, block_size=2, use_lora=True, use_reslr=True, image_size=(32, 32), patch_size=(8, 8),
            num_classes=10, device="cpu")
 BS = 3
+
+# Res-ViT-B/16 @224, res-vit/config.py get_train_config defaults (use_lora / use_reslr on)
+B16 = dict(dim=768, mlp_dim=3072, n_layers=12, n_heads=12, n_kv_heads=12, norm_eps=1e-5, lora_rank=8,
+           dynamic_active_target=0.6, dynamic_start_layer=2, dynamic_router_hdim=512, dynamic_reserve_initials=1,
+           low_rank_dim=256, block_size=1, use_lora=True, use_reslr=True, image_size=(224, 224),
+           patch_size=(16, 16), num_classes=100, device="cpu")
+B16_BS = 2
+INPUT_SEED = 7
+
+
+def b16_inputs():
+    g = torch.Generator().manual_seed(INPUT_SEED)
+    x = torch.randn(B16_BS, 3, 224, 224, generator=g)
+    y = torch.randint(0, B16["num_classes"], (B16_BS,), generator=g)
+    return x, y
 
 
 def load_ref():
@@ -175,5 +198,46 @@ def main():
           f"a {float(ta):.4f} d {float(td):.6f}")
 
 
+def main_b16():
+    mod = load_ref()
+    torch.manual_seed(42)
+    model = mod.Transformer(mod.ModelArgs(**B16))
+    tame(model)
+    out = {"cfg_json": np.array(json.dumps({k: v for k, v in B16.items() if k != "device"}))}
+    for k, v in model.state_dict().items():
+        t = v.detach().double()
+        out["fp/" + k] = np.array([float(t.sum()), float((t * t).sum())])
+    x, y = b16_inputs()
+    (c, a, d, ent, metric), rec_e = run_eval(model, x, y)
+    out["eval/logits"] = model.logits.clone().numpy()
+    out["eval/c_loss"] = np.float64(c)
+    out["eval/r_entropy"] = np.float64(ent)
+    out["eval/active_ratio"] = np.float64(metric["non_low_rank_ratio"])
+    for k, v in model.routing_maps.items():
+        out[f"eval/routing{k}"] = v.numpy()
+    for j, i in enumerate(range(0, len(rec_e), 2)):
+        out[f"eval/router{j}_hard"] = rec_e[i + 1]["hard"].numpy()
+    (tc, ta, td, tent, tmetric), noise, rec_t = run_train(mod, model, x, y, 11)
+    out["train/logits"] = model.logits.detach().numpy()
+    for k, v in (("c_loss", tc), ("a_loss", ta), ("d_loss", td), ("r_entropy", tent)):
+        out[f"train/{k}"] = np.float64(v.detach())
+    for i, n_ in enumerate(noise):
+        out[f"train/gumbel{i}"] = n_.numpy()
+    for j, i in enumerate(range(0, len(rec_t), 2)):
+        out[f"train/router{j}_hard"] = rec_t[i + 1]["hard"].numpy()
+    out["trainable"] = np.array([n for n, p in model.named_parameters() if p.requires_grad])
+    for n, p in model.named_parameters():
+        if p.requires_grad:
+            gr = p.grad if p.grad is not None else torch.zeros_like(p)
+            out["gnorm/" + n] = np.float64(gr.double().norm())
+    dst = os.path.join(HERE, "resvit_b16.npz")
+    np.savez_compressed(dst, **out)
+    print(f"wrote {dst}: eval active ratio {float(out['eval/active_ratio']):.3f}; train losses c {float(tc):.4f} "
+          f"a {float(ta):.4f} d {float(td):.6f}; {len(noise)} router calls")
+
+
 if __name__ == "__main__":
-    main()
+    if "--b16" in sys.argv[1:]:
+        main_b16()
+    else:
+        main()

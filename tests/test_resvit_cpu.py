@@ -60,3 +60,20 @@ def test_cpu_forward_refuses():
     m = resvit.Transformer(resvit.ModelArgs(**TINY))
     with pytest.raises(RuntimeError, match="MI355X HIP path only"):
         m(torch.randn(1, 3, 32, 32), torch.tensor([1]))
+
+
+def test_b16_constructor_and_rescale_match_reference_fingerprints(golden_dir):
+    """Res-ViT-B/16 (BASELINE C5's model): the seed-42 constructor followed by the fixture rescale
+    reproduces the reference's tensors (per-tensor f64 sum and sum of squares, tests/golden/resvit_b16.npz)."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
+    from make_resvit_golden import B16, tame
+    g = np.load(os.path.join(golden_dir, "resvit_b16.npz"))
+    torch.manual_seed(42)
+    m = resvit.Transformer(resvit.ModelArgs(**B16))
+    tame(m)
+    sd = m.state_dict()
+    assert sorted(k[3:] for k in g.files if k.startswith("fp/")) == sorted(sd.keys())
+    for k, v in sd.items():
+        t = v.double()
+        assert float(t.sum()) == float(g["fp/" + k][0]) and float((t * t).sum()) == float(g["fp/" + k][1]), k

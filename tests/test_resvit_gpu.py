@@ -134,3 +134,72 @@ def test_train_step_matches_reference(golden):
     assert not bad, bad
     # frozen base weights receive no gradient (res-vit/model.py:573-584)
     assert all(p.grad is None for n, p in m.named_parameters() if not p.requires_grad)
+
+
+# ---- Res-ViT-B/16 @224 (BASELINE config C5's model, res-vit/config.py defaults), batch 2 ----
+@pytest.fixture(scope="module")
+def golden_b16(golden_dir):
+    return np.load(os.path.join(golden_dir, "resvit_b16.npz"))
+
+
+def build_b16(golden_b16):
+    """seed-42 constructor + the fixture's deterministic rescale, checked against the reference's
+    per-tensor fingerprints (f64 sum and sum of squares) before use"""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
+    from make_resvit_golden import B16, b16_inputs, tame  # our generator script: data only, no reference code
+    from vitmi import resvit
+    torch.manual_seed(42)
+    m = resvit.Transformer(resvit.ModelArgs(**B16))
+    tame(m)
+    for k, v in m.state_dict().items():
+        t = v.detach().double()
+        ref = golden_b16["fp/" + k]
+        assert abs(float(t.sum()) - ref[0]) <= 1e-9 * max(1.0, abs(ref[1])) ** 0.5 + 1e-12 * abs(ref[0]), k
+        assert abs(float((t * t).sum()) - ref[1]) <= 1e-9 * abs(ref[1]) + 1e-12, k
+    x, y = b16_inputs()
+    return m.cuda(), x.cuda(), y.cuda()
+
+
+def test_b16_eval_ragged_forward_matches_reference(golden_b16):
+    """Res-ViT-B/16 inference: 10 routers, ragged attention over the kept tokens of each image."""
+    m, x, y = build_b16(golden_b16)
+    m.eval()
+    replay(m, golden_b16, "eval")
+    with torch.no_grad():
+        c, a, d, ent, metric = m(x, y)
+    for k, v in m.routing_maps.items():
+        assert torch.equal(v.cpu(), torch.from_numpy(golden_b16[f"eval/routing{k}"])), k
+    assert rel(m.logits, golden_b16["eval/logits"]) < 1e-2
+    assert abs(float(c) - float(golden_b16["eval/c_loss"])) <= 1e-3 * float(golden_b16["eval/c_loss"])
+    assert abs(float(metric["non_low_rank_ratio"]) - float(golden_b16["eval/active_ratio"])) < 1e-6
+
+
+def test_b16_train_step_matches_reference(golden_b16):
+    """Res-ViT-B/16 training step (teacher + routed student, LoRA over frozen bases): losses and the
+    norm of every trainable parameter's gradient."""
+    m, x, y = build_b16(golden_b16)
+    m.train()
+    replay(m, golden_b16, "train")
+    c, a, d, ent, metric = m(x, y)
+    (10.0 * c + 10.0 * a + 1.0 * d).backward()
+    assert rel(m.logits, golden_b16["train/logits"]) < 1e-2
+    assert abs(float(c) - float(golden_b16["train/c_loss"])) <= 1e-3 * float(golden_b16["train/c_loss"])
+    assert abs(float(d) - float(golden_b16["train/d_loss"])) <= 1e-2 * float(golden_b16["train/d_loss"])
+    assert abs(float(a) - float(golden_b16["train/a_loss"])) <= 1e-2 * float(golden_b16["train/a_loss"]) + 1e-6
+    named = dict(m.named_parameters())
+    trainable = [str(t) for t in golden_b16["trainable"]]
+    assert [n for n, p in m.named_parameters() if p.requires_grad] == trainable
+    tot = math.sqrt(sum(float(golden_b16["gnorm/" + n]) ** 2 for n in trainable))
+    bad = []
+    for n in trainable:
+        ref = float(golden_b16["gnorm/" + n])
+        g = named[n].grad
+        mine = 0.0 if g is None else float(g.double().norm())
+        if ref < 1e-3 * tot:
+            if abs(mine - ref) > 1e-3 * tot:
+                bad.append((n, "abs", mine, ref))
+        elif abs(mine - ref) > 3e-2 * ref:
+            bad.append((n, mine, ref))
+    assert not bad, bad
+    assert all(p.grad is None for n, p in m.named_parameters() if not p.requires_grad)

@@ -923,11 +923,11 @@ int pick_tile(const vit_gemm_args* a) {
   //    it loses to the plain ping-pong, so those keep config 5 / 3.
   const bool ak = a->a_layout == VIT_K_CONTIG, bk = a->b_layout == VIT_K_CONTIG;
   if (a->epilogue == VIT_EPI_SPLITK && a->M >= 256 && a->N >= 256) {
-    static const int env_sk = [] {  // tuning override for the split-K weight gradients (5, 7, 8)
+    static const int env_sk = [] {  // tuning override for the split-K weight gradients (5 .. 8)
       const char* e = getenv("VIT_GEMM_SPLITK_CFG");
       return e ? atoi(e) : 5;
     }();
-    return env_sk == 7 || env_sk == 8 ? env_sk : 5;
+    return env_sk == 6 || env_sk == 7 || env_sk == 8 ? env_sk : 5;
   }
   if (a->M >= 1024 && a->N >= 256) {
     // (short-K f32 residual outputs keep 2 workgroups per CU; the aux-reading epilogues run on the
