@@ -933,7 +933,14 @@ int pick_tile(const vit_gemm_args* a) {
     // (short-K f32 residual outputs keep 2 workgroups per CU; the aux-reading epilogues run on the
     // half-tile kernel since their operand is prefetched a staging pass ahead: fc2 dgrad x GELU'
     // 286 us vs 356 us on 256x128)
-    if (ak && bk && !(a->epilogue == VIT_EPI_BIAS_RESID_F32 && a->K < 2048)) return 9;
+    // (short-K f32 residual outputs — the out-projection — also run here: 7418 vs 7385 img/s over
+    // the 256x128 two-workgroup kernel, profiles/r02/gemm_epilogue_diag.txt; VIT_GEMM_RESID_PP2=0
+    // restores that)
+    static const int env_rs = [] {
+      const char* e = getenv("VIT_GEMM_RESID_PP2");
+      return e ? atoi(e) : 1;
+    }();
+    if (ak && bk && (env_rs || !(a->epilogue == VIT_EPI_BIAS_RESID_F32 && a->K < 2048))) return 9;
     if (a->N >= 2048 && a->epilogue != VIT_EPI_GELU_BWD && a->epilogue != VIT_EPI_MUL_BF16) return 5;
     if (!bk && a->K >= 3072) return 5;
     return 3;
