@@ -135,11 +135,14 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if os.environ.get("VITMI_SHARE_GPU"):  # functional rehearsal of the N>1 path on fewer GPUs (gloo)
+        local %= max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group(os.environ.get("VITMI_DIST_BACKEND", "nccl"), device_id=dev)
+        backend = os.environ.get("VITMI_DIST_BACKEND", "nccl")
+        dist.init_process_group(backend, **({"device_id": dev} if backend == "nccl" else {}))
 
     from vitmi import ops
     from vitmi.dist import GradAllReducer
