@@ -45,16 +45,16 @@ def train_flops_per_image(a, image_size, num_classes):
 
 
 def pmc_traffic(kernel_tag="gemm_pp2_kernel<true, true, 8>"):
-    """HBM bytes per launch of the roofline kernel from the newest committed rocprofv3 PMC passes
+    """HBM bytes per launch of a roofline kernel from the newest committed rocprofv3 PMC passes
     (tools/prof.sh: FETCH_SIZE and WRITE_SIZE in separate passes, FETCH_SIZE doubled per the gfx950
     correction of MI355X_MICROARCH.md). None when no pass of that kernel is committed."""
     import glob
     import re
 
-    def version(path):  # profiles/rNN/fc1_traffic_vK.json: newest round, then newest pass
-        m = re.search(r"r(\d+)[/\\]fc1_traffic_v(\d+)", path)
+    def version(path):  # profiles/rNN/<kernel>_traffic_vK.json: newest round, then newest pass
+        m = re.search(r"r(\d+)[/\\]\w*?_traffic_v(\d+)", path)
         return (int(m.group(1)), int(m.group(2))) if m else (-1, -1)
-    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*", "fc1_traffic*.json")), key=version)
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*", "*_traffic_v*.json")), key=version)
     for path in reversed(files):
         try:
             d = json.load(open(path))
@@ -76,21 +76,39 @@ def _cpu_model():
     return "unknown"
 
 
+def _cpu_share():
+    """host cores this process may actually use: the affinity mask, capped by a cgroup CPU quota
+    (cpu.max) and by OMP_NUM_THREADS when the launcher sets it (a GPU box shares its host: the mask
+    lists every core of the machine, the quota grants ~16)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, int(int(quota) / int(period))))
+    except (OSError, ValueError):
+        pass
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return n
+
+
 def cpu_baseline(arch, image_size, num_classes, seconds_budget=20.0):
     """Time the CPU oracle (restatement of reference src/train.py:train_epoch's step) on the host, on
     every core this process may run on, under both init protocols: the tamed rescale
     (the parity protocol) and the reference's own std-1 init (slower on CPU: saturated softmax ->
     subnormal floats). `value` is the reference-init rate, the reference's own configuration."""
     from oracle.vit_oracle import OneCycle, ViTConfig, init_params, loss_and_grads, sgd_step, tame_params
-    try:
-        cores = len(os.sched_getaffinity(0))
-    except AttributeError:
-        cores = os.cpu_count() or 1
+    cores = _cpu_share()
     torch.set_num_threads(cores)
     cfg = ViTConfig(image_size=image_size, num_classes=num_classes, **arch)
     sched = OneCycle(0.03, 15000, 500 / 15000)
     rates = {}
     for proto, bs in (("reference", 4), ("tamed", 8)):  # (CPU img/s is nearly batch-independent)
+        print(f"cpu_baseline: {proto} init, batch {bs}, {cores} threads", file=sys.stderr, flush=True)
         g = torch.Generator().manual_seed(0)
         x = torch.randn(bs, 3, image_size, image_size, generator=g)
         y = torch.randint(0, num_classes, (bs,), generator=g)
@@ -198,14 +216,16 @@ def main():
     for k in range(args.warmup):
         step(k)
     barrier()
-    eng.probe = []
+    probes = ([], [])
     t0 = time.perf_counter()
     for k in range(args.warmup, total_steps):
+        if k == total_steps - 1:  # HIP events around the roofline kernels' launches of the last timed step
+            eng.probe, eng.probe_wgrad = probes  # (each event record costs the stream ~10 us of idle)
         step(k)
     barrier()
     dt = time.perf_counter() - t0
-    probe = eng.probe
-    eng.probe = None
+    probe, probe_w = probes
+    eng.probe = eng.probe_wgrad = None
     if world > 1:
         import torch.distributed as dist
         t = torch.tensor([dt], device=dev)
@@ -215,6 +235,12 @@ def main():
     T = b * cfg.tokens
     fc1_flop = 2.0 * T * cfg.emb_dim * cfg.mlp_dim
     fc1_tflops = fc1_flop / (fc1_ms * 1e-3) / 1e12
+    # the step's dominant kernel by time: the split-K weight-gradient GEMM (gemm_pp_kernel; ~22% of the
+    # step), every launch of the timed steps; achieved = its algorithmic FLOPs / its own time
+    wg_ms = [s_.elapsed_time(e_) for s_, e_, _ in probe_w]
+    wg_flop = sum(f_ for _, _, f_ in probe_w)
+    wg_tflops = wg_flop / (sum(wg_ms) * 1e-3) / 1e12 if wg_ms else 0.0
+    wg_avg_ms = sum(wg_ms) / max(1, len(wg_ms))
     imgs = args.steps * b * world
     value = imgs / dt
     fpi = train_flops_per_image(arch, args.image_size, args.num_classes)
@@ -227,6 +253,7 @@ def main():
     fpe = fpi - ((3 * 2 * (N_ - 1) * (D_ * D_ + 2 * D_ * M_) + 3 * 4 * (N_ - q_kept) * N_ * D_)
                  if eng.prune_last else 0)
     traffic = pmc_traffic() if args.arch == "b16" and b == 256 else None
+    traffic_w = pmc_traffic("gemm_pp_kernel<256, 64, 2, false, false, 7>") if args.arch == "b16" and b == 256 else None
     step_tflops_per_gpu = value / world * fpi / 1e12
     out = {
         "metric": "images/sec training step, ViT-B/16 224px bf16, 1/2/4/8 MI355X" if args.arch == "b16" and
@@ -248,7 +275,15 @@ def main():
                    "global_batch": b * world, "seq_len": cfg.tokens, "num_classes": args.num_classes,
                    "parallelism": f"dp{world}",
                    **({"grad_allreduce_dtype": "bf16"} if compress and world > 1 else {})},
-        "roofline": {"bound": "mfma", "kernel": "gemm fc1 fwd (bias + GELU + GELU' epilogue), "
+        "roofline": {"bound": "mfma", "kernel": "split-K weight-gradient GEMM gemm_pp_kernel (the step's dominant "
+                                                f"kernel): {len(wg_ms)} launches per step (HIP events, last timed step), "
+                                                f"K = tokens = {T}",
+                     "achieved": round(wg_tflops, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+                     "frac": round(wg_tflops / PEAK_BF16_TFLOPS, 4), "traffic": (traffic_w or {}).get("bytes"),
+                     "traffic_detail": traffic_w,
+                     "algorithmic_flop_per_launch": round(wg_flop / max(1, len(wg_ms))),
+                     "avg_launch_ms": round(wg_avg_ms, 4), "launches": len(wg_ms)},
+        "roofline_fc1_fwd": {"bound": "mfma", "kernel": "gemm fc1 fwd (bias + GELU + GELU' epilogue), "
                                                 f"M={T} N={cfg.mlp_dim} K={cfg.emb_dim}",
                      "achieved": round(fc1_tflops, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                      "frac": round(fc1_tflops / PEAK_BF16_TFLOPS, 4), "traffic": (traffic or {}).get("bytes"),

@@ -241,6 +241,7 @@ class ViTEngine:
         self._pruned = False
         self._side = None
         self.probe = None  # list: (start, end) HIP events around every fc1 forward GEMM launch
+        self.probe_wgrad = None  # list: (start, end, flop) around every split-K weight-gradient GEMM launch
         # dropout (nn.Dropout of PositionEmbs / EncoderBlock / MlpBlock, reference src/model.py:19-20,
         # 46-49, 124-125): counter-based Philox masks keyed by (seed, per-forward offset, site, row,
         # col), regenerated by the backward instead of stored. Seeded from torch's initial seed.
@@ -330,8 +331,15 @@ class ViTEngine:
         """out[z] (f32, [M][N], ld ldo) = sum_t A[t][m] B[t][n]  (both operands K-major)."""
         s = self._splitk(M, N, K, batch)
         ws = self._workspace(batch * s * M * N)
+        if self.probe_wgrad is not None:  # bench.py's roofline kernel: events on the stream it runs on
+            ev0 = torch.cuda.Event(enable_timing=True)
+            ev0.record()
         ops.gemm(A, B, ws, M, N, K, a_layout=MN_CONTIG, b_layout=MN_CONTIG, lda=lda, ldb=ldb, ldc=N,
                  epilogue=EPI_SPLITK, batch=batch, b_bs=b_bs, split_k=s)
+        if self.probe_wgrad is not None:
+            ev1 = torch.cuda.Event(enable_timing=True)
+            ev1.record()
+            self.probe_wgrad.append((ev0, ev1, 2.0 * M * N * K * batch))
         ops.splitk_reduce(ws, batch, s, M, N, out, ldo, out_bs)
 
     # ---- forward -------------------------------------------------------------------------------
