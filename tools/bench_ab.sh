@@ -1,0 +1,7 @@
+#!/bin/bash
+set -e
+export TMPDIR=/tmp
+for i in 1 2; do
+timeout -k 10 200 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline > gpurun_out/b_new_$i.log 2>&1
+tail -1 gpurun_out/b_new_$i.log | cut -c1-140
+done

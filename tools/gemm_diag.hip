@@ -4,6 +4,16 @@
 //   tools/gemm_diag M N K tile [epi] [wg] [a_layout b_layout]
 #include "../vit-of-pytorch_amd/csrc/capi.hip"
 #include "../vit-of-pytorch_amd/csrc/gemm.hip"
+#include "../vit-of-pytorch_amd/csrc/gemm_e0.hip"
+#include "../vit-of-pytorch_amd/csrc/gemm_e1.hip"
+#include "../vit-of-pytorch_amd/csrc/gemm_e2.hip"
+#include "../vit-of-pytorch_amd/csrc/gemm_e3.hip"
+#include "../vit-of-pytorch_amd/csrc/gemm_e4.hip"
+#include "../vit-of-pytorch_amd/csrc/gemm_e5.hip"
+#include "../vit-of-pytorch_amd/csrc/gemm_e6.hip"
+#include "../vit-of-pytorch_amd/csrc/gemm_e7.hip"
+#include "../vit-of-pytorch_amd/csrc/gemm_e8.hip"
+#include "../vit-of-pytorch_amd/csrc/gemm_e9.hip"
 
 #include <stdio.h>
 #include <stdlib.h>
