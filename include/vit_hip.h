@@ -139,7 +139,9 @@ int vit_splitk_reduce(const float* ws, int64_t batch, int64_t split, int64_t M, 
  *      be NULL); optional bf16 copy of dx_out. Per-block partial sums [nblk][3*D] of
  *      (dy*xhat, dy, dx_out) go to `partial` (>= vit_layernorm_bwd_partial_rows(rows) rows of 3*D);
  *      when non-NULL, dgamma_dbeta[0:D] = dgamma, [D:2D] = dbeta, and dx_colsum[0:D] = column sums of
- *      dx_out (= the bias gradient of the linear layer feeding this residual stream).
+ *      dx_out (= the bias gradient of the linear layer feeding this residual stream). With both NULL
+ *      only the partials are written: nblk = vit_layernorm_bwd_blocks(rows) rows, which a caller can
+ *      reduce later (vit_colsum3 over [nblk][3*D], e.g. on another stream).
  *      dx_dropout (optional): the bf16 copy and dx_colsum carry dx_out * mult (the gradient of the
  *      dropout-ed branch that fed the residual stream); dx itself stays unmasked.
  * ---------------------------------------------------------------------------------------- */
@@ -147,6 +149,7 @@ int vit_layernorm_fwd(const float* x, int64_t ldx, const float* gamma, const flo
                       void* y, int64_t ldy, int32_t y_f32, float* mean, float* rstd,
                       int64_t rows, int64_t D, float eps, vit_stream_t stream);
 int64_t vit_layernorm_bwd_partial_rows(int64_t rows);
+int64_t vit_layernorm_bwd_blocks(int64_t rows);
 int vit_layernorm_bwd(const void* dy, int64_t lddy, int32_t dy_f32, const float* x, int64_t ldx,
                       const float* mean, const float* rstd, const float* gamma,
                       const float* dres, int64_t lddres, float* dx, int64_t lddx,

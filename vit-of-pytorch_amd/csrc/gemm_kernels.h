@@ -696,6 +696,12 @@ __global__ void __launch_bounds__(WM* WN * 64, (gemm_min_waves<BM, BN, BK, STAGE
   constexpr int CPR = BN / 8;
   static_assert(NT % CPR == 0, "a thread keeps one 8-column chunk across the epilogue loop");
   float csum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  constexpr int AWB = AuxPre<EPI>::W > 0 ? AuxPre<EPI>::W : 1;
+  const bool fast = EpiOut<EPI>::FAST && p.vec && m0 + BM <= p.M && n0 + BN <= p.N;
+  float bv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if constexpr (EpiOut<EPI>::BIAS) {
+    if (fast && p.bias) ld8f(p.bias + z * p.bias_bs + n0 + (threadIdx.x % CPR) * 8, bv);
+  }
 #pragma unroll
   for (int pass = 0; pass < NPASS; ++pass) {
     if (NPASS == 1 || wm / (WM / NPASS) == pass) {
@@ -708,6 +714,38 @@ __global__ void __launch_bounds__(WM* WN * 64, (gemm_min_waves<BM, BN, BK, STAGE
             cs[(wm0 - pass * PASS_ROWS + i * 16 + 4 * g + r) * LDC + wn0 + j * 16 + c] = acc[i][j][r];
     }
     __syncthreads();
+    if (fast) {
+      // whole in-range tile: this thread's 8-column chunk is fixed (NT % CPR == 0); every aux chunk
+      // of the pass is requested before the first store and the store words stay live (epi_prep8)
+      constexpr int ITB = PASS_ROWS * CPR / NT;
+      static_assert(ITB * NT == PASS_ROWS * CPR, "whole chunks per thread");
+      const int ch = threadIdx.x % CPR, n = n0 + ch * 8;
+      uint4 ax[ITB][AWB], ob[ITB][EpiOut<EPI>::W];
+      if constexpr (AuxPre<EPI>::W > 0) {
+#pragma unroll
+        for (int it = 0; it < ITB; ++it)
+          AuxPre<EPI>::fetch(p, m0 + pass * PASS_ROWS + (threadIdx.x + it * NT) / CPR, n, ax[it]);
+      }
+#pragma unroll
+      for (int it = 0; it < ITB; ++it) {
+        const int row = (threadIdx.x + it * NT) / CPR;
+        float v[8], u[8];
+        ld8f(cs + row * LDC + ch * 8, v);
+        if constexpr (AuxPre<EPI>::W > 0) AuxPre<EPI>::unpack(ax[it], u);
+        epi_prep8<EPI>(p, m0 + pass * PASS_ROWS + row, n, v, u, bv, ob[it]);
+        if (p.col_partial) {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) csum[k] += v[k];
+        }
+      }
+#pragma unroll
+      for (int it = 0; it < ITB; ++it)
+        epi_put8<EPI>(p, z, split_idx, m0 + pass * PASS_ROWS + (threadIdx.x + it * NT) / CPR, n, ob[it]);
+#pragma unroll
+      for (int it = 0; it < ITB; ++it)
+#pragma unroll
+        for (int w = 0; w < EpiOut<EPI>::W; ++w) keep_live(ob[it][w]);
+    } else
 #pragma unroll 2
     for (int e = threadIdx.x; e < PASS_ROWS * CPR; e += NT) {
       const int row = e / CPR, ch = e % CPR;

@@ -220,6 +220,9 @@ static int64_t ln_bwd_blocks(int64_t rows) {
   return b < 1 ? 1 : b;
 }
 
+// rows of block partials the backward writes (the rows a deferred vit_colsum3 of them reduces)
+extern "C" int64_t vit_layernorm_bwd_blocks(int64_t rows) { return ln_bwd_blocks(rows); }
+
 // rows of 3*D floats the `partial` workspace must hold (block partials + their column reduction)
 extern "C" int64_t vit_layernorm_bwd_partial_rows(int64_t rows) {
   const int64_t nb = ln_bwd_blocks(rows);

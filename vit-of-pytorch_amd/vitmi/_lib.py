@@ -54,6 +54,7 @@ _SIGS = {
     "vit_splitk_reduce": (c_i32, [c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_i64, c_i64, c_i32, c_vp]),
     "vit_layernorm_fwd": (c_i32, [c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_i32, c_vp, c_vp, c_i64, c_i64, c_f32, c_vp]),
     "vit_layernorm_bwd_partial_rows": (c_i64, [c_i64]),
+    "vit_layernorm_bwd_blocks": (c_i64, [c_i64]),
     "vit_layernorm_bwd": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_i64,
                                   c_vp, c_i64, c_vp, c_vp, c_vp, c_i32, c_i64, c_i64, ctypes.POINTER(Dropout),
                                   c_vp]),

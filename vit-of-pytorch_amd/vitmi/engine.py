@@ -165,13 +165,18 @@ class _Acts:
         self.dlncls = z(b, D, dt=f)
         self.dlogits = z(b, cfg.num_classes, dt=f)
         self.row_stats = z(b, 3, dt=f)
+        # bias-gradient partial sums: written on the compute stream, reduced on the engine's bias stream
+        # (ViTEngine.backward), so each kind is double-buffered
         self.lnpart = z(ops.layernorm_bwd_partial_rows(T), 3 * D, dt=f)
+        self.lnparts = [self.lnpart, z(ops.layernorm_bwd_partial_rows(T), 3 * D, dt=f)]
         self.colpart = z(ops.colsum_partial_rows(T), max(3 * D, M, cfg.num_classes), dt=f)
-        self.gelu_part = z(-(-T // 128), M, dt=f)   # per-M-tile column sums of dU (fc1 bias grad)
+        self.gelu_parts = [z(-(-T // 128), M, dt=f) for _ in range(2)]  # per-M-tile column sums of dU (fc1 bias)
+        self.gelu_part = self.gelu_parts[0]
         # column sums of dq|dk|dv (q/k/v bias grads): per image (LDS-resident attention, N <= 320) or per
         # image and 64-row block (K/V-tiled attention, longer sequences)
         self.attn_bias_rows = ops.attention_bias_rows(N)
-        self.qkv_bpart = z(b * self.attn_bias_rows, 3 * D, dt=f)
+        self.qkv_bparts = [z(b * self.attn_bias_rows, 3 * D, dt=f) for _ in range(2)]
+        self.qkv_bpart = self.qkv_bparts[0]
         nws = ops.attention_workspace_elems(b, N, H)
         self.attn_ws = z(nws, dt=f) if nws else None
         # last encoder layer on the cls rows only (ViTEngine.prune_last): compact operands, rows
@@ -181,6 +186,58 @@ class _Acts:
         self.c_o, self.c_ln2, self.c_dh, self.c_dh2, self.c_dyln = (z(bp, D) for _ in range(5))
         self.c_g, self.c_gp, self.c_dg = (z(bp, M) for _ in range(3))
         self.c_mu2, self.c_rs2 = z(b, dt=f), z(b, dt=f)
+
+
+class _BiasReducer:
+    """The bias-gradient column reductions of one backward, on the engine's bias stream.
+
+    The compute stream writes per-block partial sums (LayerNorm backward: [nblk][dgamma | dbeta | dx];
+    the fc2-dgrad GEMM epilogue: per-tile dU column sums; the attention backward: per-image dq|dk|dv
+    sums); reduce() runs their vit_colsum / vit_colsum3 on the bias stream after everything issued so
+    far on the compute stream, and buf() hands out the two buffers of each kind alternately, making the
+    compute stream wait for the reduction that last read a buffer before it is written again."""
+
+    def __init__(self, eng, a, main):
+        if eng._bias_st is None:
+            eng._bias_st = torch.cuda.Stream(device=eng.dev)
+        self.stream = eng._bias_st
+        self.main = main
+        self.a = a
+        self.D = eng.cfg.emb_dim
+        self.done = {}   # (kind, index) -> event after the last reduction that read that buffer
+        self.nxt = {}
+
+    def buf(self, kind, bufs):
+        i = self.nxt.get(kind, 0)
+        self.nxt[kind] = i ^ 1
+        ev = self.done.pop((kind, i), None)
+        if ev is not None:
+            self.main.wait_event(ev)
+        return bufs[i], (kind, i)
+
+    def reduce(self, key, fn):
+        ev = torch.cuda.Event()
+        ev.record(self.main)
+        self.stream.wait_event(ev)
+        with torch.cuda.stream(self.stream):
+            fn()
+        if key is not None:
+            d = torch.cuda.Event()
+            d.record(self.stream)
+            self.done[key] = d
+
+    def ln_bwd(self, dy, lddy, x, ldx, mean, rstd, gamma, dx, lddx, rows, dgamma_dbeta, dx_colsum, **kw):
+        """LayerNorm backward on the compute stream; dgamma | dbeta (and the column sums of dx, the
+        bias gradient of the layer feeding the residual stream) reduced on the bias stream."""
+        part, key = self.buf("ln", self.a.lnparts)
+        D = self.D
+        ops.layernorm_bwd(dy, lddy, x, ldx, mean, rstd, gamma, dx, lddx, part, rows, D, **kw)
+        nblk = ops.layernorm_bwd_blocks(rows)
+        self.reduce(key, lambda: ops.colsum3(part, nblk, D, 3 * D, self.a.colpart, dgamma_dbeta, dgamma_dbeta[D:],
+                                             dx_colsum))
+
+    def finish(self):
+        self.main.wait_stream(self.stream)
 
 
 class ViTEngine:
@@ -240,6 +297,10 @@ class ViTEngine:
         self.prune_last = os.environ.get("VITMI_PRUNE_LAST", "1") != "0"
         self._pruned = False
         self._side = None
+        # bias-gradient column reductions (vit_colsum / vit_colsum3 over per-block partial sums: ~100
+        # launches of ~5 us per B/16 step) run on their own stream: nothing on the compute stream waits
+        # for them, so they fill the tails of the GEMM launches instead of sitting between them
+        self._bias_st = None
         self.probe = None  # list: (start, end) HIP events around every fc1 forward GEMM launch
         self.probe_wgrad = None  # list: (start, end, flop) around every split-K weight-gradient GEMM launch
         # dropout (nn.Dropout of PositionEmbs / EncoderBlock / MlpBlock, reference src/model.py:19-20,
@@ -439,7 +500,7 @@ class ViTEngine:
         ops.gemm(a.c_g, mv[ln("mlp.fc2.weight"):], a.h[i + 1], b, D, M, a_layout=K_CONTIG, b_layout=K_CONTIG,
                  lda=M, ldb=M, ldc=S, epilogue=EPI_BIAS_RESID_F32, bias=f[ln("mlp.fc2.bias"):], aux=a.hm[i], ldaux=S)
 
-    def _backward_last_cls(self, a, i, b, g, on_side):
+    def _backward_last_cls(self, a, i, b, g, on_side, bias):
         """Backward of _forward_last_cls: the gradient reaching the last layer's output is non-zero on
         the cls rows only (a.c_dh, from the final LayerNorm backward), so fc2 / fc1 (data and weight
         gradients), LayerNorm 2 and the out-projection run on those b rows (weight-gradient K = the
@@ -452,17 +513,17 @@ class ViTEngine:
         gv = lambda name: g[self.off(self.lname(i, name)):]
         bp = a.bp
         on_side(lambda: self._wgrad(a.c_dh, D, a.c_g, M, D, M, bp, gv("mlp.fc2.weight"), M))
+        gpart, gkey = bias.buf("gelu", a.gelu_parts)
         kw = dict(a_layout=K_CONTIG, b_layout=K_CONTIG, lda=D, ldb=D, ldc=M, epilogue=EPI_MUL_BF16, aux=a.c_gp,
-                  ldaux=M, col_partial=a.gelu_part)
+                  ldaux=M, col_partial=gpart)
         ops.gemm(a.c_dh, self.w2t[i], a.c_dg, b, M, D, **kw)
         tiles_m = -(-b // ops.gemm_tile_rows(a.c_dh, self.w2t[i], a.c_dg, b, M, D, **kw))
-        ops.colsum(a.gelu_part, tiles_m, M, M, a.colpart, gv("mlp.fc1.bias"))
+        bias.reduce(gkey, lambda: ops.colsum(gpart, tiles_m, M, M, a.colpart, gv("mlp.fc1.bias")))
         on_side(lambda: self._wgrad(a.c_dg, M, a.c_ln2, D, M, D, bp, gv("mlp.fc1.weight"), D))
         ops.gemm(a.c_dg, self.w1t[i], a.c_dyln, b, D, M, a_layout=K_CONTIG, b_layout=K_CONTIG, lda=M, ldb=M, ldc=D,
                  epilogue=EPI_BF16)
-        ops.layernorm_bwd(a.c_dyln, D, a.hm[i], S, a.c_mu2, a.c_rs2, f[self.off(self.lname(i, "norm2.weight")):],
-                          a.dh, S, a.lnpart, b, D, dres=a.dh, lddres=S, dx_bf16=a.c_dh2, lddxb=D,
-                          dgamma_dbeta=gv("norm2.weight"), dx_colsum=gv("attn.out.bias"))
+        bias.ln_bwd(a.c_dyln, D, a.hm[i], S, a.c_mu2, a.c_rs2, f[self.off(self.lname(i, "norm2.weight")):], a.dh, S, b,
+                    gv("norm2.weight"), gv("attn.out.bias"), dres=a.dh, lddres=S, dx_bf16=a.c_dh2, lddxb=D)
         on_side(lambda: self._wgrad(a.c_o, D, a.c_dh2, D, D, D, bp, gv("attn.out.weight"), D))
         a.dO.zero_()
         ops.gemm(a.c_dh2, mv[self.off(self.lname(i, "attn.out.weight")):], a.dO, b, D, D, a_layout=K_CONTIG,
@@ -577,16 +638,16 @@ class ViTEngine:
             if not hook:
                 return
             evs = []
-            if overlap:
-                for st in (main, side):
-                    ev = torch.cuda.Event()
-                    ev.record(st)
-                    evs.append(ev)
+            for st in ((main, side) if overlap else (main,)) + (bias.stream,):
+                ev = torch.cuda.Event()
+                ev.record(st)
+                evs.append(ev)
             hook(g, *bucket, evs)
 
+        bias = _BiasReducer(self, a, main)
         # classifier head (f32): dWc = dl^T lncls, dbc = colsum(dl), dlncls = dl Wc
         ops.gemm_f32(C, D, b, dl, C, True, a.lncls, D, False, gv("classifier.weight"), D)
-        ops.colsum(dl, b, C, C, a.colpart, gv("classifier.bias"))
+        bias.reduce(None, lambda: ops.colsum(dl, b, C, C, a.colpart, gv("classifier.bias")))
         ops.gemm_f32(b, D, C, dl, C, False, f[self.off("classifier.weight"):], D, False, a.dlncls, D)
         # final LN backward on cls rows -> residual grad (zero elsewhere)
         # (its dx column sum is the last layer's fc2 bias gradient: only the cls rows are non-zero)
@@ -595,10 +656,10 @@ class ViTEngine:
         a.dh.zero_()
         if not pruned:
             a.dhb[wb].zero_()
-        ops.layernorm_bwd(a.dlncls, D, a.h[L], N * D, a.muf, a.rsf, f[self.off("transformer.norm.weight"):], a.dh,
-                          N * D, a.lnpart, b, D, dx_bf16=a.c_dh if pruned else a.dhb[wb], lddxb=D if pruned else N * D,
-                          dgamma_dbeta=gv("transformer.norm.weight"),
-                          dx_colsum=gv(self.lname(L - 1, "mlp.fc2.bias")), dx_dropout=dd(3 + 3 * (L - 1), N))
+        bias.ln_bwd(a.dlncls, D, a.h[L], N * D, a.muf, a.rsf, f[self.off("transformer.norm.weight"):], a.dh, N * D, b,
+                    gv("transformer.norm.weight"), gv(self.lname(L - 1, "mlp.fc2.bias")),
+                    dx_bf16=a.c_dh if pruned else a.dhb[wb], lddxb=D if pruned else N * D,
+                    dx_dropout=dd(3 + 3 * (L - 1), N))
         fire(self.layout.buckets[0])
         scale = 1.0 / math.sqrt(hd)
         for i in reversed(range(L)):
@@ -606,7 +667,7 @@ class ViTEngine:
             li = i & 1
             if pruned and i == L - 1:
                 # MLP, LayerNorm 2 and out-projection backward on the cls rows; dO = 0 elsewhere
-                self._backward_last_cls(a, i, b, g, on_side)
+                self._backward_last_cls(a, i, b, g, on_side, bias)
                 wb ^= 1
             else:
                 dhb = a.dhb[wb]
@@ -616,11 +677,12 @@ class ViTEngine:
                 release("dhb", wb)
                 dg = a.dg[li]
                 acquire("dg", li)
+                gpart, gkey = bias.buf("gelu", a.gelu_parts)
                 kw = dict(a_layout=K_CONTIG, b_layout=K_CONTIG, lda=D, ldb=D, ldc=M, epilogue=EPI_MUL_BF16, aux=a.gp[i],
-                          ldaux=M, col_partial=a.gelu_part)
+                          ldaux=M, col_partial=gpart)
                 ops.gemm(dhb, self.w2t[i], dg, T, M, D, **kw)
                 tiles_m = -(-T // ops.gemm_tile_rows(dhb, self.w2t[i], dg, T, M, D, **kw))
-                ops.colsum(a.gelu_part, tiles_m, M, M, a.colpart, gv(self.lname(i, "mlp.fc1.bias")))
+                bias.reduce(gkey, lambda: ops.colsum(gpart, tiles_m, M, M, a.colpart, gv(self.lname(i, "mlp.fc1.bias"))))
                 on_side(lambda: self._wgrad(dg, M, a.ln2[i], D, M, D, a.Tp, gv(self.lname(i, "mlp.fc1.weight")), D))
                 release("dg", li)
                 ops.gemm(dg, self.w1t[i], a.dyln, T, D, M, a_layout=K_CONTIG, b_layout=K_CONTIG, lda=M,
@@ -628,10 +690,9 @@ class ViTEngine:
                 wb ^= 1
                 acquire("dhb", wb)
                 dhb = a.dhb[wb]
-                ops.layernorm_bwd(a.dyln, D, a.hm[i], D, a.mu2[i], a.rs2[i], f[ln("norm2.weight"):], a.dh, D, a.lnpart, T,
-                                  D, dres=a.dh, lddres=D, dx_bf16=dhb, lddxb=D,
-                                  dgamma_dbeta=gv(self.lname(i, "norm2.weight")),
-                                  dx_colsum=gv(self.lname(i, "attn.out.bias")), dx_dropout=dd(1 + 3 * i))
+                bias.ln_bwd(a.dyln, D, a.hm[i], D, a.mu2[i], a.rs2[i], f[ln("norm2.weight"):], a.dh, D, T,
+                            gv(self.lname(i, "norm2.weight")), gv(self.lname(i, "attn.out.bias")),
+                            dres=a.dh, lddres=D, dx_bf16=dhb, lddxb=D, dx_dropout=dd(1 + 3 * i))
                 # ---- attention: hm = h + out(attn(ln1(h))) ----
                 on_side(lambda: self._wgrad(a.o[i], D, dhb, D, D, D, a.Tp, gv(self.lname(i, "attn.out.weight")), D))
                 release("dhb", wb)
@@ -639,12 +700,14 @@ class ViTEngine:
                          ldb=D, ldc=D, epilogue=EPI_BF16)
             dqkv = a.dqkv[li]
             acquire("dqkv", li)
-            ops.attention_bwd(a.qkv[i], a.o[i], a.dO, a.lse[i], dqkv, b, N, H, hd, scale, bias_partial=a.qkv_bpart,
+            qpart, qkey = bias.buf("qkv", a.qkv_bparts)
+            ops.attention_bwd(a.qkv[i], a.o[i], a.dO, a.lse[i], dqkv, b, N, H, hd, scale, bias_partial=qpart,
                               q_rows=1 if pruned and i == L - 1 else None, workspace=a.attn_ws)
             qo = ln("attn.query.weight")
             zs = ln("attn.key.weight") - qo
             qb = ln("attn.query.bias")
-            ops.colsum3(a.qkv_bpart, b * a.attn_bias_rows, D, 3 * D, a.colpart, g[qb:], g[qb + zs:], g[qb + 2 * zs:])
+            bias.reduce(qkey, lambda: ops.colsum3(qpart, b * a.attn_bias_rows, D, 3 * D, a.colpart, g[qb:], g[qb + zs:],
+                                                  g[qb + 2 * zs:]))
             on_side(lambda: self._wgrad(a.ln1[i], D, dqkv, 3 * D, D, D, a.Tp, g[qo:], D, batch=3, b_bs=D,
                                         out_bs=zs))
             release("dqkv", li)
@@ -652,11 +715,10 @@ class ViTEngine:
                      ldb=3 * D, ldc=D, epilogue=EPI_BF16)
             wb ^= 1
             acquire("dhb", wb)
-            ops.layernorm_bwd(a.dyln, D, a.h[i], D, a.mu1[i], a.rs1[i], f[ln("norm1.weight"):], a.dh, D, a.lnpart, T,
-                              D, dres=a.dh, lddres=D, dx_bf16=a.dhb[wb], lddxb=D,
-                              dgamma_dbeta=gv(self.lname(i, "norm1.weight")),
-                              dx_colsum=gv(self.lname(i - 1, "mlp.fc2.bias")) if i > 0 else None,
-                              dx_dropout=dd(3 + 3 * (i - 1)) if i > 0 else dd(0))
+            bias.ln_bwd(a.dyln, D, a.h[i], D, a.mu1[i], a.rs1[i], f[ln("norm1.weight"):], a.dh, D, T,
+                        gv(self.lname(i, "norm1.weight")), gv(self.lname(i - 1, "mlp.fc2.bias")) if i > 0 else None,
+                        dres=a.dh, lddres=D, dx_bf16=a.dhb[wb], lddxb=D,
+                        dx_dropout=dd(3 + 3 * (i - 1)) if i > 0 else dd(0))
             fire(self.layout.buckets[L - i])
         # ---- embedding: conv weight grad (wgrad over patches), bias / pos / cls ----
         dhb = a.dhb[wb]
@@ -665,6 +727,7 @@ class ViTEngine:
         ops.embed_grad(a.dh, b, N, D, gv("transformer.pos_embedding.pos_embedding"), gv("cls_token"),
                        gv("embedding.bias"), dropout=dd(0))
         fire(self.layout.buckets[-1])
+        bias.finish()
         if overlap:
             main.wait_stream(side)
         return g

@@ -104,6 +104,11 @@ def layernorm_bwd_partial_rows(rows):
     return int(lib().vit_layernorm_bwd_partial_rows(rows))
 
 
+def layernorm_bwd_blocks(rows):
+    """rows of block partials [nblk][3*D] a layernorm_bwd without dgamma/dx_colsum leaves to reduce."""
+    return int(lib().vit_layernorm_bwd_blocks(rows))
+
+
 def layernorm_bwd(dy, lddy, x, ldx, mean, rstd, gamma, dx, lddx, partial, rows, D, *, dres=None, lddres=0,
                   dx_bf16=None, lddxb=0, dgamma_dbeta=None, dx_colsum=None, accumulate=False, dx_dropout=None):
     check(lib().vit_layernorm_bwd(_p(dy), lddy, int(dy.dtype == F32), _p(x), ldx, _p(mean), _p(rstd), _p(gamma),
