@@ -8,7 +8,7 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/ktr
 S=$(find $O/ktrace -name "*kernel_stats.csv" | head -1)
 T=$(find $O/ktrace -name "*kernel_trace.csv" | head -1)
 python3 tools/prof_summary.py $S 13 > $O/kernel_summary.txt
-python3 tools/trace_step.py $T > $O/step_timeline.txt
+python3 tools/trace_step.py $T 1 $O/step_launches.txt > $O/step_timeline.txt
 cp $S $O/kernel_stats.csv
 rm -rf $O/ktrace
 tail -1 $O/ktrace.log | cut -c1-120

@@ -13,7 +13,7 @@ step "ktrace" timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format
 S=$(find $O/ktrace -name "*kernel_stats.csv" | head -1)
 T=$(find $O/ktrace -name "*kernel_trace.csv" | head -1)
 python3 tools/prof_summary.py $S 13 > $O/kernel_summary.txt
-python3 tools/trace_step.py $T > $O/step_timeline.txt
+python3 tools/trace_step.py $T 1 $O/step_launches.txt > $O/step_timeline.txt
 cp $S $O/kernel_stats.csv
 step "pmc mfma" timeout -k 10 -s KILL 300 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_BUSY_CYCLES --output-format csv -d $O/pmc_mfma -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > $O/pmc_mfma.log 2>&1
 step "pmc fetch" timeout -k 10 -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > $O/pmc_fetch.log 2>&1

@@ -4,7 +4,7 @@
 Splits the trace into steps at the SGD kernel, takes the last step, and reports per stream:
 busy time (union of kernel intervals), and per kernel class the summed duration, plus the step's
 wall span and the time during which NO kernel runs (launch gaps / host waits).
-usage: trace_step.py run_kernel_trace.csv [step_index_from_end=1]
+usage: trace_step.py run_kernel_trace.csv [step_index_from_end=1] [launch_list_out]
 """
 import csv
 import re
@@ -63,6 +63,11 @@ def main():
             c[1] += 1
         for name, (d, n) in sorted(cls.items(), key=lambda x: -x[1][0]):
             print(f"   {d / 1e3:9.1f} us  {n:4d}x  {d / n / 1e3:8.1f} avg  {name}")
+    if len(sys.argv) > 3:  # the step's launches in issue order: start offset, duration, queue, kernel
+        with open(sys.argv[3], "w") as f:
+            for r in step:
+                s0, e0 = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+                f.write(f"{(s0 - t0) / 1e3:9.1f} {(e0 - s0) / 1e3:8.1f} q{r['Queue_Id']} {short(r['Kernel_Name'])}\n")
 
 
 if __name__ == "__main__":

@@ -855,11 +855,16 @@ __global__ void __launch_bounds__(NW * 64, 2) attn_bwd_kernel(const bf16_t* __re
         for (int dt = 0; dt < HD / 16; ++dt) dq[dt] = mfma(rd_tr<HD>(ImA, 2 * ks, 2 * ks + 1, dt * 16, lane), bD, dq[dt]);
       }
       if (q < N) {
+        uint2 pk[HD / 16];
+#pragma unroll
+        for (int dt = 0; dt < HD / 16; ++dt) pk[dt] = pack4bf(dq[dt], scale);
 #pragma unroll
         for (int dt = 0; dt < HD / 16; ++dt) {
           const int d = dt * 16 + 4 * g;
-          if (d < hd) store4(dq_base + (long)q * rs + d, dq[dt], scale);
+          if (d < hd) *reinterpret_cast<uint2*>(dq_base + (long)q * rs + d) = pk[dt];
         }
+#pragma unroll
+        for (int dt = 0; dt < HD / 16; ++dt) keep_live2(pk[dt]);
       }
       if (bias_partial) {
 #pragma unroll
@@ -1079,6 +1084,14 @@ __global__ void __launch_bounds__(NW * 64, 2) attn_bwd_kernel(const bf16_t* __re
         dk[1][dt] = mfma(qt, bD1, dk[1][dt]);
       }
     }
+    uint2 pk[2][HD / 16], pv[2][HD / 16];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int dt = 0; dt < HD / 16; ++dt) {
+        pk[t][dt] = pack4bf(dk[t][dt], scale);
+        pv[t][dt] = pack4bf(dv[t][dt], 1.0f);
+      }
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
       const int key = (2 * kp + t) * 16 + i;
@@ -1087,8 +1100,8 @@ __global__ void __launch_bounds__(NW * 64, 2) attn_bwd_kernel(const bf16_t* __re
         for (int dt = 0; dt < HD / 16; ++dt) {
           const int d = dt * 16 + 4 * g;
           if (d < hd) {
-            store4(dq_base + (long)key * rs + D + d, dk[t][dt], scale);
-            store4(dq_base + (long)key * rs + 2 * D + d, dv[t][dt], 1.0f);
+            *reinterpret_cast<uint2*>(dq_base + (long)key * rs + D + d) = pk[t][dt];
+            *reinterpret_cast<uint2*>(dq_base + (long)key * rs + 2 * D + d) = pv[t][dt];
           }
         }
       }
@@ -1102,6 +1115,13 @@ __global__ void __launch_bounds__(NW * 64, 2) attn_bwd_kernel(const bf16_t* __re
           }
       }
     }
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int dt = 0; dt < HD / 16; ++dt) {
+        keep_live2(pk[t][dt]);
+        keep_live2(pv[t][dt]);
+      }
   }
 
   if (bias_partial) {

@@ -99,6 +99,19 @@ __device__ __forceinline__ void store4(bf16_t* dst, const v4f& v, float s) {
   *reinterpret_cast<uint2*>(dst) = u;
 }
 
+// A row of HD/16 accumulator fragments (columns 16dt + 4g .. +3), packed to bf16 before any of its
+// stores is issued. hipcc protects the source registers of an outstanding store with an
+// `s_waitcnt vmcnt` before they are overwritten (and vmcnt retires in order), so store4 calls that
+// reuse one temporary serialize on the store round trip; packing every fragment first, storing them,
+// and keeping the packed words live (keep_live2) lets the stores of a row overlap.
+__device__ __forceinline__ uint2 pack4bf(const v4f& v, float s) {
+  uint2 u;
+  u.x = pack2bf(v[0] * s, v[1] * s);
+  u.y = pack2bf(v[2] * s, v[3] * s);
+  return u;
+}
+__device__ __forceinline__ void keep_live2(const uint2& u) { asm volatile("" ::"v"(u.x), "v"(u.y)); }
+
 // Global row fragment (16 rows x 32 k, MFMA operand layout) straight to registers: lane (g, i) gets
 // row r0 + i, columns kk*32 + 8g .. +7; rows >= N and columns >= hd read as zero.
 template <int HD>
