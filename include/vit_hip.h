@@ -274,6 +274,11 @@ int vit_cast_pad_rows(const float* in, int64_t rows, int64_t cols, void* out, in
  * Packs q/k/v LinearGeneral weights [D][H,hd] (src/model.py:73-75) into one [D][3D] operand. */
 int vit_pack_cols(const float* in, int64_t zstride, int64_t ldi, int64_t rows, int64_t cols, int64_t Z,
                   void* out, int64_t ldo, int32_t out_bf16, vit_stream_t stream);
+/* vit_pack_cols over `batch` matrix sets (one per encoder layer): set z reads in + z*in_batch_stride
+ * (floats, may be negative) and writes out + z*out_batch_stride (elements). One launch for all layers. */
+int vit_pack_cols_batched(const float* in, int64_t in_batch_stride, int64_t zstride, int64_t ldi, int64_t rows,
+                          int64_t cols, int64_t Z, void* out, int64_t out_batch_stride, int64_t ldo,
+                          int32_t out_bf16, int64_t batch, vit_stream_t stream);
 /* out bf16 [cols][ldo] <- transpose of in f32 [rows][ldi]: out[c*ldo + r] = bf16(in[r*ldi + c]), for
  * batch matrices z at in + z*in_batch_stride, out + z*out_batch_stride (strides may be negative).
  * K-contiguous weight copies for the dgrad / projection GEMMs (fc1/fc2 weights src/model.py:31-32,

@@ -583,7 +583,9 @@ extern "C" int vit_axpby(const float* x, float* y, int64_t n, float a, float b, 
 namespace {
 template <bool BF16OUT>
 __global__ void pack_cols_kernel(const float* __restrict__ in, long zstride, long ldi, int rows, int cols, int Z,
-                                 void* __restrict__ out, long ldo) {
+                                 void* __restrict__ out, long ldo, long in_bs = 0, long out_bs = 0) {
+  in += (long)blockIdx.y * in_bs;  // batch (blockIdx.y): one matrix set per encoder layer
+  out = (char*)out + (long)blockIdx.y * out_bs * (BF16OUT ? 2 : 4);
   const long total = (long)rows * Z * cols;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
     const long r = i / ((long)Z * cols);
@@ -610,6 +612,25 @@ extern "C" int vit_pack_cols(const float* in, int64_t zstride, int64_t ldi, int6
     hipLaunchKernelGGL(pack_cols_kernel<false>, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, in,
                        (long)zstride, (long)ldi, (int)rows, (int)cols, (int)Z, out, (long)ldo);
   VIT_LAUNCH_CHECK("vit_pack_cols");
+}
+
+extern "C" int vit_pack_cols_batched(const float* in, int64_t in_batch_stride, int64_t zstride, int64_t ldi,
+                                     int64_t rows, int64_t cols, int64_t Z, void* out, int64_t out_batch_stride,
+                                     int64_t ldo, int32_t out_bf16, int64_t batch, vit_stream_t stream) {
+  VIT_CHECK_ARG(in && out && rows >= 0 && cols >= 0 && Z >= 1 && ldo >= Z * cols && batch >= 1 && batch < 65536,
+                "vit_pack_cols_batched: bad args");
+  const long total = rows * Z * cols;
+  if (total == 0) return VIT_OK;
+  long gx = (total + 255) / 256;
+  if (gx > 1024) gx = 1024;
+  const dim3 grid((unsigned)gx, (unsigned)batch);
+  if (out_bf16)
+    hipLaunchKernelGGL(pack_cols_kernel<true>, grid, dim3(256), 0, (hipStream_t)stream, in, (long)zstride, (long)ldi,
+                       (int)rows, (int)cols, (int)Z, out, (long)ldo, (long)in_batch_stride, (long)out_batch_stride);
+  else
+    hipLaunchKernelGGL(pack_cols_kernel<false>, grid, dim3(256), 0, (hipStream_t)stream, in, (long)zstride, (long)ldi,
+                       (int)rows, (int)cols, (int)Z, out, (long)ldo, (long)in_batch_stride, (long)out_batch_stride);
+  VIT_LAUNCH_CHECK("vit_pack_cols_batched");
 }
 
 // ---- transposed bf16 weight copies: out[c*ldo + r] = bf16(in[r*ldi + c]) ---------------------------

@@ -82,6 +82,8 @@ _SIGS = {
     "vit_cast_pad_rows": (c_i32, [c_vp, c_i64, c_i64, c_vp, c_i64, c_vp]),
     "vit_axpby": (c_i32, [c_vp, c_vp, c_i64, c_f32, c_f32, c_vp]),
     "vit_pack_cols": (c_i32, [c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp, c_i64, c_i32, c_vp]),
+    "vit_pack_cols_batched": (c_i32, [c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp, c_i64, c_i64, c_i32, c_i64,
+                                      c_vp]),
     "vit_transpose_f32_bf16": (c_i32, [c_vp, c_i64, c_i64, c_i64, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp]),
     "vit_colsum3": (c_i32, [c_vp, c_i32, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_i32, c_vp]),
     "vit_im2col_f32": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp]),

@@ -337,18 +337,14 @@ class ViTEngine:
         D = cfg.emb_dim
         if full:
             ops.cast_bf16(self.flat, self.mirror, self.layout.numel)
-        for i in range(cfg.num_layers):
-            qo = self.off(self.lname(i, "attn.query.weight"))
-            zs = self.off(self.lname(i, "attn.key.weight")) - qo
-            ops.pack_cols(self.flat[qo:], zs, D, D, D, 3, self.wqkv[i], 3 * D)
-            bo = self.off(self.lname(i, "attn.query.bias"))
-            ops.pack_cols(self.flat[bo:], zs, D, 1, D, 3, self.bqkv[i], 3 * D)
-        # K-contiguous copies, one launch per weight kind over all layers (layers sit at a constant
-        # stride in the flat buffer, layer L-1 first)
+        # q|k|v packing and K-contiguous copies, one launch per weight kind over all layers (layers sit
+        # at a constant stride in the flat buffer, layer L-1 first)
         M, L = cfg.mlp_dim, cfg.num_layers
         lst = self.layer_stride
         o0 = lambda s: self.off(self.lname(0, s))
         zs = self.off(self.lname(0, "attn.key.weight")) - o0("attn.query.weight")
+        ops.pack_cols_batched(self.flat[o0("attn.query.weight"):], -lst, zs, D, D, D, 3, self.wqkv, D * 3 * D, 3 * D, L)
+        ops.pack_cols_batched(self.flat[o0("attn.query.bias"):], -lst, zs, D, 1, D, 3, self.bqkv, 3 * D, 3 * D, L)
         for z in range(3):
             ops.transpose_bf16(self.flat[o0("attn.query.weight") + z * zs:], D, D, D, self.wqkvt[0, z * D:], D,
                                batch=L, in_bs=-lst, out_bs=3 * D * D)

@@ -229,6 +229,12 @@ def pack_cols(inp, zstride, ldi, rows, cols, Z, out, ldo):
           "vit_pack_cols")
 
 
+def pack_cols_batched(inp, in_bs, zstride, ldi, rows, cols, Z, out, out_bs, ldo, batch):
+    """pack_cols for `batch` layers at strides in_bs (floats, may be negative) / out_bs (elements)."""
+    check(lib().vit_pack_cols_batched(_p(inp), in_bs, zstride, ldi, rows, cols, Z, _p(out), out_bs, ldo,
+                                      int(out.dtype == BF16), batch, _stream()), "vit_pack_cols_batched")
+
+
 def transpose_bf16(inp, rows, cols, ldi, out, ldo, batch=1, in_bs=0, out_bs=0):
     """out[z][c*ldo + r] = bf16(inp[z][r*ldi + c]) (K-contiguous weight copies; z strides may be negative)."""
     _chk(out, BF16, "out")
