@@ -332,10 +332,13 @@ def test_colsum_ce_gemm_f32_sgd():
 
 
 @pytest.mark.parametrize("rows,cols", [(768, 3072), (3072, 768), (100, 70), (64, 64)])
-def test_transpose_bf16(rows, cols):
+@pytest.mark.parametrize("aligned", [False, True])
+def test_transpose_bf16(rows, cols, aligned):
+    # aligned: ldo a multiple of 8 (the 16-B store path; rows 100 also takes its row-tail path)
+    ldo = (rows + 7) // 8 * 8 if aligned else rows + 3
     x = torch.randn(rows, cols + 5, device=DEV)
-    out = torch.full((cols, rows + 3), float("nan"), device=DEV).bfloat16()
-    ops.transpose_bf16(x, rows, cols, cols + 5, out, rows + 3)
+    out = torch.full((cols, ldo), float("nan"), device=DEV).bfloat16()
+    ops.transpose_bf16(x, rows, cols, cols + 5, out, ldo)
     assert torch.equal(out[:, :rows], x[:, :cols].t().bfloat16())
 
 

@@ -640,7 +640,7 @@ extern "C" int vit_pack_cols_batched(const float* in, int64_t in_batch_stride, i
 namespace {
 __global__ void __launch_bounds__(256) transpose_f32_bf16_kernel(const float* __restrict__ in, long ldi, int rows,
                                                                  int cols, bf16_t* __restrict__ out, long ldo,
-                                                                 long in_bs, long out_bs) {
+                                                                 long in_bs, long out_bs, int vec) {
   __shared__ float tile[64][65];
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
   const int c0 = blockIdx.x * 64, r0 = blockIdx.y * 64;
@@ -652,10 +652,20 @@ __global__ void __launch_bounds__(256) transpose_f32_bf16_kernel(const float* __
     tile[ty + 4 * k][tx] = (r < rows && c < cols) ? in[(long)r * ldi + c] : 0.f;
   }
   __syncthreads();
+  // each thread: 16 consecutive outputs of one output row (two 16-B stores; 2-B stores per lane made
+  // this kernel store-instruction-bound)
+  const int oc = threadIdx.x >> 2, seg = (threadIdx.x & 3) * 16;
+  const int c = c0 + oc;
+  if (c >= cols) return;
+  bf16_t* o = out + (long)c * ldo + r0 + seg;
+  if (vec && r0 + seg + 16 <= rows) {
+    unsigned w[8];
 #pragma unroll
-  for (int k = 0; k < 16; ++k) {
-    const int c = c0 + ty + 4 * k, r = r0 + tx;  // output row c, column r
-    if (c < cols && r < rows) out[(long)c * ldo + r] = f2bf(tile[tx][ty + 4 * k]);
+    for (int j = 0; j < 8; ++j) w[j] = pack2bf(tile[seg + 2 * j][oc], tile[seg + 2 * j + 1][oc]);
+    *reinterpret_cast<uint4*>(o) = make_uint4(w[0], w[1], w[2], w[3]);
+    *reinterpret_cast<uint4*>(o + 8) = make_uint4(w[4], w[5], w[6], w[7]);
+  } else {
+    for (int j = 0; j < 16 && r0 + seg + j < rows; ++j) o[j] = f2bf(tile[seg + j][oc]);
   }
 }
 }  // namespace
@@ -667,8 +677,9 @@ extern "C" int vit_transpose_f32_bf16(const float* in, int64_t rows, int64_t col
                 "vit_transpose_f32_bf16: bad args");
   if (rows == 0 || cols == 0) return VIT_OK;
   dim3 grid((unsigned)((cols + 63) / 64), (unsigned)((rows + 63) / 64), (unsigned)batch);
+  const int vec = ldo % 8 == 0 && out_batch_stride % 8 == 0 && (uintptr_t)out % 16 == 0;
   hipLaunchKernelGGL(transpose_f32_bf16_kernel, grid, dim3(256), 0, (hipStream_t)stream, in, (long)ldi, (int)rows,
-                     (int)cols, (bf16_t*)out, (long)ldo, (long)in_batch_stride, (long)out_batch_stride);
+                     (int)cols, (bf16_t*)out, (long)ldo, (long)in_batch_stride, (long)out_batch_stride, vec);
   VIT_LAUNCH_CHECK("vit_transpose_f32_bf16");
 }
 
