@@ -1000,6 +1000,23 @@ __global__ void __launch_bounds__(NW * 64, 2) attn_bwd_kernel(const bf16_t* __re
         if (i == 0) bsum[(wave * 3 + 0) * HD + dt * 16 + 4 * g + r] = v * scale;
       }
   }
+  // stage 2's first key pair per wave (kp = wave) takes its K / V rows from the stage-1 images before
+  // they are overwritten (rows past N are the images' zero padding): K and V of those pairs are read
+  // from HBM once instead of twice; later pairs are requested from HBM one pair ahead as before
+  v8bf kn[2][HD / 32], vn[2][HD / 32];  // next pair's K / V rows
+  asm volatile("" ::: "memory");
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int kk = 0; kk < HD / 32; ++kk) {
+      if (stages & 4) {  // diagnostic (VIT_ATTN_BWD_STAGES bit 2): the first pair from HBM as well
+        kn[t][kk] = gl_row<HD>(base + D, rs, (2 * wave + t) * 16, kk, N, hd, lane);
+        vn[t][kk] = gl_row<HD>(base + 2 * D, rs, (2 * wave + t) * 16, kk, N, hd, lane);
+      } else {
+        kn[t][kk] = wave < npair ? rd_row<HD>(ImA, (2 * wave + t) * 16, kk, lane) : v8bf{};
+        vn[t][kk] = wave < npair ? rd_row<HD>(ImB, (2 * wave + t) * 16, kk, lane) : v8bf{};
+      }
+    }
   __syncthreads();  // K / V images no longer read; delta complete
 
   // ---- stage 2: dK and dV, key-tile pairs ----
@@ -1010,14 +1027,6 @@ __global__ void __launch_bounds__(NW * 64, 2) attn_bwd_kernel(const bf16_t* __re
   // the last query pair may hold one wholly padded 16-row tile (N % 32 in 1..16): its S / dP
   // products are skipped (P = dS = 0 there)
   const bool last_half = (2 * npair - 1) * 16 >= N;
-  v8bf kn[2][HD / 32], vn[2][HD / 32];  // next pair's K / V rows, requested one pair ahead
-#pragma unroll
-  for (int t = 0; t < 2; ++t)
-#pragma unroll
-    for (int kk = 0; kk < HD / 32; ++kk) {
-      kn[t][kk] = gl_row<HD>(base + D, rs, (2 * wave + t) * 16, kk, N, hd, lane);
-      vn[t][kk] = gl_row<HD>(base + 2 * D, rs, (2 * wave + t) * 16, kk, N, hd, lane);
-    }
   for (int kp = wave; kp < npair; kp += NW) {
     v8bf kf[2][HD / 32], vf[2][HD / 32];
 #pragma unroll

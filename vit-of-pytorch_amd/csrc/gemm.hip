@@ -40,7 +40,7 @@ int pick_tile(const vit_gemm_args* a) {
       const char* e = getenv("VIT_GEMM_SPLITK_CFG");
       return e ? atoi(e) : 5;
     }();
-    return env_sk == 6 || env_sk == 7 || env_sk == 8 ? env_sk : 5;
+    return env_sk == 6 || env_sk == 7 || env_sk == 8 || env_sk == 9 ? env_sk : 5;
   }
   if (a->M >= 1024 && a->N >= 256) {
     // (short-K f32 residual outputs keep 2 workgroups per CU; the aux-reading epilogues run on the
@@ -230,7 +230,7 @@ extern "C" int vit_gemm_bf16(const vit_gemm_args* a, vit_stream_t stream) {
           const char* e = getenv("VIT_GEMM_REM_CFG");
           return e ? atoi(e) : 0;
         }();
-        if (e == hipSuccess) e = run(rem_cfg >= 0 && rem_cfg <= 4 ? rem_cfg : 0, g2);
+        if (e == hipSuccess) e = run(rem_cfg >= 0 && rem_cfg <= 9 && rem_cfg != 1 ? rem_cfg : 0, g2);
         return vit::check_hip(e, "vit_gemm_bf16 launch");
       }
     }
