@@ -824,11 +824,14 @@ __global__ void __launch_bounds__(NW * 64, 2) attn_bwd_kernel(const bf16_t* __re
           st = mfma(rd_row<HD>(ImA, kt * 16, kk, lane), qf[kk], st);
           dpt = mfma(rd_row<HD>(ImB, kt * 16, kk, lane), df[kk], dpt);
         }
-        const bool full = (kt + 1) * 16 <= N;  // wave-uniform: only the last tiles hold padded keys
+        // Padded keys (rows N.. of the zero-filled K / V images) need no mask here: their dP = dO V^T
+        // is 0, so they add nothing to delta, and their dS only meets the zero K rows in dQ = dS K.
+        // The exponent is clamped at 0 so that P stays finite for them whatever the query's LSE (a
+        // real key's exponent is <= 0 up to rounding: LSE >= every score). The per-(tile, row) masks
+        // this replaces were spilled SGPR lane masks: 2 v_readlane + 2 v_cndmask per element.
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          float pv = ex2(st[r] * c - ls);
-          if (!full && kt * 16 + 4 * g + r >= N) pv = 0.f;
+          const float pv = ex2(fminf(st[r] * c - ls, 0.f));
           P[kt][r] = pv;
           dl += pv * dpt[r];
         }

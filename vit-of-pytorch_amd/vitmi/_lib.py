@@ -9,7 +9,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libvit_hip.so")
+# VITMI_LIB: an alternate build of the same library (A/B timing of kernel variants in one process tree)
+LIB_PATH = os.environ.get("VITMI_LIB") or os.path.join(_HERE, "libvit_hip.so")
 
 c_i64 = ctypes.c_int64
 c_i32 = ctypes.c_int32
