@@ -811,7 +811,7 @@ __global__ void __launch_bounds__(NW * 64, 2) attn_bwd_kernel(const bf16_t* __re
       }
       const float ls = lse_s[qt * 16 + i];
       v4f P[NKT], DP[NKT];
-      float dl = 0.f;
+      float dlr[4] = {0.f, 0.f, 0.f, 0.f};  // four independent chains (one fma chain per row r)
 #pragma unroll
       for (int kt = 0; kt < NKT; ++kt) {
         if (kt == NKT - 1 && kt * 16 >= N) {  // a wholly padded last key tile (N % 32 in 1..16)
@@ -833,10 +833,11 @@ __global__ void __launch_bounds__(NW * 64, 2) attn_bwd_kernel(const bf16_t* __re
         for (int r = 0; r < 4; ++r) {
           const float pv = ex2(fminf(st[r] * c - ls, 0.f));
           P[kt][r] = pv;
-          dl += pv * dpt[r];
+          dlr[r] += pv * dpt[r];
         }
         DP[kt] = dpt;
       }
+      float dl = (dlr[0] + dlr[1]) + (dlr[2] + dlr[3]);
       dl += __shfl_xor(dl, 16, 64);
       dl += __shfl_xor(dl, 32, 64);
       const int q = qt * 16 + i;
