@@ -8,7 +8,9 @@
 namespace {
 
 // NV = float4 chunks per lane (D <= NV * 256).
-template <int NV>
+// FULL: D == NV * 256, every chunk in range: no per-chunk guards, so a row's loads (and the gamma /
+// beta loads) issue back to back instead of one guarded load and its wait at a time
+template <int NV, bool FULL>
 __global__ void __launch_bounds__(256) ln_fwd_kernel(const float* __restrict__ x, long ldx, const float* __restrict__ gamma,
                                                      const float* __restrict__ beta, void* __restrict__ y, long ldy,
                                                      int y_f32, float* __restrict__ mean, float* __restrict__ rstd,
@@ -17,12 +19,20 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(const float* __restrict__ x
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
   const float* xr = x + (long)row * ldx;
-  float4 v[NV];
+  float4 v[NV], gmv[NV], btv[NV];
   float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {  // gamma / beta requested with the row, not after its reductions
+    const int c = (k * 64 + lane) * 4;
+    if (FULL || c < D) {
+      gmv[k] = *reinterpret_cast<const float4*>(gamma + c);
+      btv[k] = *reinterpret_cast<const float4*>(beta + c);
+    }
+  }
 #pragma unroll
   for (int k = 0; k < NV; ++k) {
     const int c = (k * 64 + lane) * 4;
-    if (c < D) {
+    if (FULL || c < D) {
       v[k] = *reinterpret_cast<const float4*>(xr + c);
       s += v[k].x + v[k].y + v[k].z + v[k].w;
     } else {
@@ -34,7 +44,7 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(const float* __restrict__ x
 #pragma unroll
   for (int k = 0; k < NV; ++k) {
     const int c = (k * 64 + lane) * 4;
-    if (c < D) {
+    if (FULL || c < D) {
       const float a = v[k].x - mu, b = v[k].y - mu, cc = v[k].z - mu, d = v[k].w - mu;
       ss += a * a + b * b + cc * cc + d * d;
     }
@@ -48,9 +58,8 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(const float* __restrict__ x
 #pragma unroll
   for (int k = 0; k < NV; ++k) {
     const int c = (k * 64 + lane) * 4;
-    if (c < D) {
-      const float4 gm = *reinterpret_cast<const float4*>(gamma + c);
-      const float4 bt = *reinterpret_cast<const float4*>(beta + c);
+    if (FULL || c < D) {
+      const float4 gm = gmv[k], bt = btv[k];
       const float o0 = (v[k].x - mu) * rs * gm.x + bt.x;
       const float o1 = (v[k].y - mu) * rs * gm.y + bt.y;
       const float o2 = (v[k].z - mu) * rs * gm.z + bt.z;
@@ -72,7 +81,7 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(const float* __restrict__ x
 // at 1024 blocks, +0.3% step; VIT_LN_BWD_BLOCKS overrides).
 constexpr int LN_BWD_MAX_BLOCKS = 512;
 
-template <int NV>
+template <int NV, bool FULL>
 __global__ void __launch_bounds__(256) ln_bwd_kernel(const void* __restrict__ dy, long lddy, int dy_f32,
                                                      const float* __restrict__ x, long ldx, const float* __restrict__ mean,
                                                      const float* __restrict__ rstd, const float* __restrict__ gamma,
@@ -89,7 +98,7 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const void* __restrict__ dy
     pb[k] = make_float4(0.f, 0.f, 0.f, 0.f);
     ps[k] = make_float4(0.f, 0.f, 0.f, 0.f);
     const int c = (k * 64 + lane) * 4;
-    gm[k] = c < D ? *reinterpret_cast<const float4*>(gamma + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+    gm[k] = FULL || c < D ? *reinterpret_cast<const float4*>(gamma + c) : make_float4(0.f, 0.f, 0.f, 0.f);
   }
   // rows are software-pipelined: the next row's loads (dy, x, residual grad, stats) are issued
   // before this row's math and stores, so each wave keeps two rows of HBM reads in flight
@@ -99,7 +108,7 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const void* __restrict__ dy
 #pragma unroll
     for (int k = 0; k < NV; ++k) {
       const int c = (k * 64 + lane) * 4;
-      if (c < D) {
+      if (FULL || c < D) {
         if (dy_f32) {
           d4[k] = *reinterpret_cast<const float4*>((const float*)dy + (long)row * lddy + c);
         } else {
@@ -138,7 +147,7 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const void* __restrict__ dy
 #pragma unroll
     for (int k = 0; k < NV; ++k) {
       const int c = (k * 64 + lane) * 4;
-      if (c < D) {
+      if (FULL || c < D) {
         float4 o;
         o.x = rs * (g[k].x - m1 - xh[k].x * m2) + r4[k].x;
         o.y = rs * (g[k].y - m1 - xh[k].y * m2) + r4[k].y;
@@ -202,8 +211,15 @@ extern "C" int vit_layernorm_fwd(const float* x, int64_t ldx, const float* gamma
   dim3 grid((unsigned)((rows + 3) / 4)), block(256);
   hipStream_t s = (hipStream_t)stream;
   switch (nv_for(D)) {
-#define C(n) \
-  case n: hipLaunchKernelGGL(ln_fwd_kernel<n>, grid, block, 0, s, x, (long)ldx, gamma, beta, y, (long)ldy, (int)y_f32, mean, rstd, (int)rows, (int)D, eps); break;
+#define C(n)                                                                                                        \
+  case n:                                                                                                           \
+    if (D == n * 256)                                                                                               \
+      hipLaunchKernelGGL((ln_fwd_kernel<n, true>), grid, block, 0, s, x, (long)ldx, gamma, beta, y, (long)ldy,       \
+                         (int)y_f32, mean, rstd, (int)rows, (int)D, eps);                                           \
+    else                                                                                                            \
+      hipLaunchKernelGGL((ln_fwd_kernel<n, false>), grid, block, 0, s, x, (long)ldx, gamma, beta, y, (long)ldy,      \
+                         (int)y_f32, mean, rstd, (int)rows, (int)D, eps);                                           \
+    break;
     C(1) C(2) C(3) C(4) C(5) C(6) C(7) C(8)
 #undef C
   }
@@ -243,9 +259,14 @@ extern "C" int vit_layernorm_bwd(const void* dy, int64_t lddy, int32_t dy_f32, c
   switch (nv_for(D)) {
 #define C(n)                                                                                                        \
   case n:                                                                                                           \
-    hipLaunchKernelGGL(ln_bwd_kernel<n>, dim3((unsigned)nblk), dim3(256), 0, s, dy, (long)lddy, (int)dy_f32, x,     \
-                       (long)ldx, mean, rstd, gamma, dres, (long)lddres, dx, (long)lddx, (bf16_t*)dx_bf16,           \
-                       (long)lddxb, partial, (int)rows, (int)D, drop);                                              \
+    if (D == n * 256)                                                                                               \
+      hipLaunchKernelGGL((ln_bwd_kernel<n, true>), dim3((unsigned)nblk), dim3(256), 0, s, dy, (long)lddy, (int)dy_f32, \
+                         x, (long)ldx, mean, rstd, gamma, dres, (long)lddres, dx, (long)lddx, (bf16_t*)dx_bf16,      \
+                         (long)lddxb, partial, (int)rows, (int)D, drop);                                            \
+    else                                                                                                            \
+      hipLaunchKernelGGL((ln_bwd_kernel<n, false>), dim3((unsigned)nblk), dim3(256), 0, s, dy, (long)lddy,           \
+                         (int)dy_f32, x, (long)ldx, mean, rstd, gamma, dres, (long)lddres, dx, (long)lddx,          \
+                         (bf16_t*)dx_bf16, (long)lddxb, partial, (int)rows, (int)D, drop);                          \
     break;
     C(1) C(2) C(3) C(4) C(5) C(6) C(7) C(8)
 #undef C
