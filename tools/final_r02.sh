@@ -1,7 +1,7 @@
 #!/bin/bash
-# end-of-session check: full GPU test suite, then the round-2 evidence set (tools/prof_r02b.sh, V=6)
+# end-of-session check: full GPU test suite, then the default bench line (with the CPU baseline)
 set -o pipefail
 export TMPDIR=/tmp
 timeout -k 10 800 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/gputest.log 2>&1
 rc=$?; tail -2 gpurun_out/gputest.log; [ $rc -eq 0 ] || exit $rc
-V=6 bash tools/prof_r02b.sh > gpurun_out/prof_v6.log 2>&1
+timeout -k 10 300 python3 -u bench.py --steps 20 --warmup 5 > gpurun_out/bench_final.json 2> gpurun_out/bench_final.err
