@@ -105,6 +105,34 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const void* __restrict__ dy
   auto load_row = [&](int row, float4* d4, float4* x4, float4* r4, float& mu, float& rs) {
     mu = mean[row];
     rs = rstd[row];
+    if constexpr (FULL) {
+      // wave-uniform choices outside the chunk loops: each loop is straight-line, so the row's loads
+      // issue together (a per-chunk branch made hipcc wait for each chunk's loads in turn)
+      if (dy_f32) {
+#pragma unroll
+        for (int k = 0; k < NV; ++k)
+          d4[k] = *reinterpret_cast<const float4*>((const float*)dy + (long)row * lddy + (k * 64 + lane) * 4);
+      } else {
+        uint2 u[NV];
+#pragma unroll
+        for (int k = 0; k < NV; ++k)
+          u[k] = *reinterpret_cast<const uint2*>((const bf16_t*)dy + (long)row * lddy + (k * 64 + lane) * 4);
+#pragma unroll
+        for (int k = 0; k < NV; ++k)
+          d4[k] = make_float4(bf2f(u[k].x & 0xffff), bf2f(u[k].x >> 16), bf2f(u[k].y & 0xffff), bf2f(u[k].y >> 16));
+      }
+#pragma unroll
+      for (int k = 0; k < NV; ++k) x4[k] = *reinterpret_cast<const float4*>(x + (long)row * ldx + (k * 64 + lane) * 4);
+      if (dres) {
+#pragma unroll
+        for (int k = 0; k < NV; ++k)
+          r4[k] = *reinterpret_cast<const float4*>(dres + (long)row * lddres + (k * 64 + lane) * 4);
+      } else {
+#pragma unroll
+        for (int k = 0; k < NV; ++k) r4[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+      return;
+    }
 #pragma unroll
     for (int k = 0; k < NV; ++k) {
       const int c = (k * 64 + lane) * 4;
