@@ -135,13 +135,44 @@ def cpu_baseline(arch, image_size, num_classes, seconds_budget=20.0):
                        f"steps in {t[2]:.1f} s; each after 1 warm-up step")
 
 
+def _free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n, argv, module=None, script=None):
+    """Start n ranks of this program (one process per GPU, torch.distributed.run on 127.0.0.1) as a
+    child process and return its exit code. Called before anything touches the GPU: only
+    torch.cuda.device_count(), which does not initialise HIP on this image, is consulted. More ranks
+    than visible GPUs is an error unless VITMI_SHARE_GPU=1 (functional rehearsal on one card)."""
+    import subprocess
+    visible = torch.cuda.device_count()
+    if n > visible and not os.environ.get("VITMI_SHARE_GPU"):
+        print(f"error: {n} ranks requested but {visible} GPU(s) visible "
+              "(VITMI_SHARE_GPU=1 rehearses the multi-rank path on fewer GPUs)", file=sys.stderr)
+        return 2
+    port = os.environ.get("MASTER_PORT") or str(_free_port())
+    target = ["-m", module] if module else [script]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", port, *target, *argv]
+    env = dict(os.environ)
+    pp = [os.path.join(REPO, "vit-of-pytorch_amd"), REPO]
+    env["PYTHONPATH"] = os.pathsep.join(pp + ([env["PYTHONPATH"]] if env.get("PYTHONPATH") else []))
+    return subprocess.call(cmd, env=env)
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="GPUs (ranks) of this node; >1 without a torch.distributed.run environment starts "
+                         "that many ranks itself")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=256, help="images per GPU")
-    ap.add_argument("--arch", default="b16", choices=sorted(ARCHS))
+    ap.add_argument("--batch", type=int, default=None, help="images per GPU (default 256; resvit_b16: 128)")
+    ap.add_argument("--arch", default="b16", choices=sorted(ARCHS) + ["resvit_b16"],
+                    help="resvit_b16: BASELINE config C5, the Res-ViT-B/16 training step (res-vit/train.py)")
     ap.add_argument("--image-size", type=int, default=224)
     ap.add_argument("--num-classes", type=int, default=1000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -149,18 +180,32 @@ def main():
     ap.add_argument("--grad-compress", choices=["none", "bf16"], default="none",
                     help="N>1: all-reduce the gradient buckets in bf16 (vitmi.dist compress='bf16')")
     args = ap.parse_args()
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:], script=os.path.abspath(__file__)))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"error: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        sys.exit(2)
     if os.environ.get("VITMI_SHARE_GPU"):  # functional rehearsal of the N>1 path on fewer GPUs (gloo)
         local %= max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    backend = None
     if world > 1:
         import torch.distributed as dist
         backend = os.environ.get("VITMI_DIST_BACKEND", "nccl")
         dist.init_process_group(backend, **({"device_id": dev} if backend == "nccl" else {}))
+    # torch's "nccl" backend is RCCL on ROCm; any other backend is named as itself
+    comm = {None: None, "nccl": "RCCL"}.get(backend, backend)
+    if args.arch == "resvit_b16":
+        return bench_resvit(args, world, rank, dev, backend, comm)
+    if args.batch is None:
+        args.batch = 256
 
     from vitmi import ops
     from vitmi.dist import GradAllReducer
@@ -237,10 +282,15 @@ def main():
     fc1_tflops = fc1_flop / (fc1_ms * 1e-3) / 1e12
     # the step's dominant kernel by time: the split-K weight-gradient GEMM (gemm_pp_kernel; ~22% of the
     # step), every launch of the timed steps; achieved = its algorithmic FLOPs / its own time
-    wg_ms = [s_.elapsed_time(e_) for s_, e_, _ in probe_w]
-    wg_flop = sum(f_ for _, _, f_ in probe_w)
+    # headline: the launches over all T tokens (K = T rounded up to 64); the pruned last layer's
+    # launches (K = the b cls rows padded to 64) are reported beside it, not averaged in
+    full_w = [p_ for p_ in probe_w if p_[3] >= T]
+    pr_w = [p_ for p_ in probe_w if p_[3] < T]
+    wg_ms = [s_.elapsed_time(e_) for s_, e_, _, _ in full_w]
+    wg_flop = sum(p_[2] * T / p_[3] for p_ in full_w)  # algorithmic: the T real rows, not the padding
     wg_tflops = wg_flop / (sum(wg_ms) * 1e-3) / 1e12 if wg_ms else 0.0
     wg_avg_ms = sum(wg_ms) / max(1, len(wg_ms))
+    pr_ms = sum(s_.elapsed_time(e_) for s_, e_, _, _ in pr_w)
     imgs = args.steps * b * world
     value = imgs / dt
     fpi = train_flops_per_image(arch, args.image_size, args.num_classes)
@@ -270,19 +320,23 @@ def main():
         "dtype": "bf16",
         "data": "synthetic (N(0,1) images, uniform labels, seed-42 reference-order random init)",
         "config": {"workload": f"ViT-{args.arch.upper()} @{args.image_size} train step (fwd+CE+bwd+"
-                               f"{'RCCL all-reduce+' if world > 1 else ''}SGD-momentum/OneCycleLR)",
+                               f"{comm + ' all-reduce+' if world > 1 else ''}SGD-momentum/OneCycleLR)",
                    "model": f"ViT-{args.arch.upper()}", "image_size": args.image_size, "per_gpu_batch": b,
                    "global_batch": b * world, "seq_len": cfg.tokens, "num_classes": args.num_classes,
-                   "parallelism": f"dp{world}",
+                   "parallelism": f"dp{world}", "dist_backend": backend,
                    **({"grad_allreduce_dtype": "bf16"} if compress and world > 1 else {})},
         "roofline": {"bound": "mfma", "kernel": "split-K weight-gradient GEMM gemm_pp_kernel (the step's dominant "
-                                                f"kernel): {len(wg_ms)} launches per step (HIP events, last timed step), "
-                                                f"K = tokens = {T}",
+                                                f"kernel): the {len(wg_ms)} launches over all tokens of the last "
+                                                f"timed step (HIP events), K = {T} tokens padded to 64; fc1 / fc2 / "
+                                                "out-proj weights one GEMM each, q|k|v three GEMMs in one batched launch",
                      "achieved": round(wg_tflops, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                      "frac": round(wg_tflops / PEAK_BF16_TFLOPS, 4), "traffic": (traffic_w or {}).get("bytes"),
                      "traffic_detail": traffic_w,
                      "algorithmic_flop_per_launch": round(wg_flop / max(1, len(wg_ms))),
-                     "avg_launch_ms": round(wg_avg_ms, 4), "launches": len(wg_ms)},
+                     "avg_launch_ms": round(wg_avg_ms, 4), "launches": len(wg_ms),
+                     "pruned_layer_launches": {"launches": len(pr_w), "total_ms": round(pr_ms, 4),
+                                               "note": "last layer's cls-row weight gradients (K = batch padded "
+                                                       "to 64), excluded from achieved"}},
         "roofline_fc1_fwd": {"bound": "mfma", "kernel": "gemm fc1 fwd (bias + GELU + GELU' epilogue), "
                                                 f"M={T} N={cfg.mlp_dim} K={cfg.emb_dim}",
                      "achieved": round(fc1_tflops, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
@@ -297,6 +351,108 @@ def main():
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(arch, args.image_size, args.num_classes, args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+def resvit_flops_per_image(a, image_size, block_heads, active_ratio):
+    """executed matrix FLOPs per image of the Res-ViT training step (res-vit/model.py:590-702 under
+    res-vit/train.py:23-68) with LoRA (frozen bases: no base weight gradients) and residual low-rank
+    routing. Per layer, G = the q/k/v/o + FFN GEMMs, A = the two attention matmuls, of all N tokens:
+    student forward every layer (computed on every token, then selected), teacher forward from
+    dynamic_start_layer on, backward of the student path (data gradients G + attention 2A); router MLPs
+    at block heads and LoRA: forward + data + weight gradients (3x); approximators on the
+    (1 - active_ratio) routed rows (3x)."""
+    D, M, L, P, r, h = a["dim"], a["mlp_dim"], a["n_layers"], a["patch"], a["lora_rank"], a["router_hdim"]
+    s0, lr_dim, bs = a["dynamic_start_layer"], a["low_rank_dim"], a["block_size"]
+    n = (image_size // P) ** 2
+    N = n + 1
+    G = 2 * N * (4 * D * D + 2 * D * M)
+    A = 4 * N * N * D
+    lora = 3 * 2 * N * 3 * (2 * D * r)
+    router = 3 * 2 * N * (D * h + 2 * h * h + h * (h // 2) + (h // 2) * 2 * bs)
+    approx = 3 * 2 * N * (2 * D * lr_dim) * (1.0 - active_ratio)
+    patch = 2 * n * 3 * P * P * D
+    return (patch + L * (G + A + lora) + (L - s0) * (G + A + lora) + L * (G + 2 * A + lora) +
+            block_heads * router + (L - s0) * approx)
+
+
+def bench_resvit(args, world, rank, dev, backend, comm):
+    """BASELINE config C5: Res-ViT-B/16 @224 training step (res-vit/train.py:23-68) with the
+    res-vit/config.py defaults (LoRA rank 8 over frozen bases, residual low-rank routing from layer 2,
+    block size 1, active target 0.6, 100 classes, AdamW lr 1e-4 wd 0.05, clip 1.0, cosine warm-up
+    schedule, lambdas class 1 / active 1e-4 / distill 1e-2), the clip folded into the HIP AdamW update;
+    N > 1: one rank per GPU, flat gradient buckets all-reduced during the backward."""
+    from vitmi import resvit
+    from vitmi.optim import AdamW, get_cosine_schedule_with_warmup
+    from vitmi.resvit_train import train_step
+    b = args.batch or 128
+    a = dict(dim=768, mlp_dim=3072, n_layers=12, n_heads=12, n_kv_heads=12, norm_eps=1e-5, lora_rank=8,
+             dynamic_active_target=0.6, dynamic_start_layer=2, dynamic_router_hdim=512, dynamic_reserve_initials=1,
+             low_rank_dim=256, block_size=1, use_lora=True, use_reslr=True, image_size=(args.image_size,) * 2,
+             patch_size=(16, 16), num_classes=100, device="cuda")
+    torch.manual_seed(42)
+    model = resvit.Transformer(resvit.ModelArgs(**a)).to(dev).train()
+    opt = AdamW(model.parameters(), lr=1e-4, weight_decay=0.05, betas=(0.9, 0.999), eps=1e-8, max_grad_norm=1.0)
+    sched = get_cosine_schedule_with_warmup(opt, 500, 15000)
+    reducer = None
+    if world > 1:
+        from vitmi.dist import FlatGradAllReducer
+        reducer = FlatGradAllReducer(opt.flat).attach()
+    g = torch.Generator(device=dev).manual_seed(1000 + rank)
+    x = torch.randn(b, 3, args.image_size, args.image_size, device=dev, generator=g)
+    y = torch.randint(0, 100, (b,), device=dev, generator=g)
+    ratios = []
+
+    def step():
+        out = train_step(model, x, y, opt, sched, 1e-4, 1e-2, 1.0, True, reducer)
+        ratios.append(out[5]["non_low_rank_ratio"])
+
+    def barrier():
+        if world > 1:
+            import torch.distributed as dist
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        step()
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        import torch.distributed as dist
+        t = torch.tensor([dt], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t)
+    active = float(torch.stack(ratios[-args.steps:]).mean())
+    value = args.steps * b * world / dt
+    heads = sum(1 for l in model.layers if hasattr(l, "router"))
+    fpi = resvit_flops_per_image(dict(a, patch=16, router_hdim=512), args.image_size, heads, active)
+    achieved = value / world * fpi / 1e12
+    out = {
+        "metric": f"images/sec training step, Res-ViT-B/16 {args.image_size}px bf16",
+        "value": round(value, 2), "unit": "images/sec", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "bf16",
+        "data": "synthetic (N(0,1) images, uniform labels, seed-42 reference-order random init, Gumbel routing)",
+        "config": {"workload": f"Res-ViT-B/16 @{args.image_size} train step (teacher+routed student fwd, 1c+1e-4a+"
+                               f"1e-2d loss, bwd, {comm + ' all-reduce, ' if world > 1 else ''}clip 1.0 + AdamW, "
+                               "cosine warm-up)",
+                   "model": "Res-ViT-B/16 (LoRA r8, reslr, block 1, 100 classes)", "image_size": args.image_size,
+                   "per_gpu_batch": b, "global_batch": b * world, "seq_len": (args.image_size // 16) ** 2 + 1,
+                   "parallelism": f"dp{world}", "dist_backend": backend},
+        "roofline": {"bound": "mfma", "kernel": "whole step (executed matrix FLOPs, resvit_flops_per_image)",
+                     "achieved": round(achieved, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+                     "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": None},
+        "executed_gflop_per_image": round(fpi / 1e9, 3),
+        "active_ratio": round(active, 4),
+    }
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -322,6 +322,35 @@ int vit_add_bcast_f32(const float* x, const float* y, float* out, int64_t outer,
 int vit_unpack_bf16_f32(const void* in, int64_t ldi, int64_t rows, int64_t cols, float* out, int64_t ldo,
                         vit_stream_t stream);
 
+/* ------------------------------------------------------------------------------------------
+ * Res-ViT optimizer step (res-vit/train.py:64-66 clip_grad_norm_(params, 1.0, 2) + AdamW.step(),
+ * :272-277) over ONE flat f32 buffer of the trainable parameters, one 64-element-aligned segment per
+ * parameter (replaces torch.nn.utils.clip_grad_norm_ and torch.optim.AdamW's per-tensor loops).
+ * ---------------------------------------------------------------------------------------- */
+/* partial[i] (f64) = sum of g[j]^2 over workgroup i's fixed grid-stride slice (nparts workgroups) */
+int vit_sqnorm_partial(const float* g, int64_t n, double* partial, int32_t nparts, vit_stream_t stream);
+/* one workgroup: norm = sqrt(sum partial) (partial may be NULL: no clipping), clip coefficient
+ * min(1, max_norm / (norm + 1e-6)) (1 when max_norm <= 0); norm_out[0..1] = {norm, coef} if non-NULL.
+ * For each of nseg segments: if used[s] > 0, steps[s] += 1 and table[s] (float4) = {lr / (1 - beta1^step),
+ * sqrt(1 - beta2^step), 1, coef}; otherwise {0, 0, 0, coef} (torch skips parameters without a grad). */
+int vit_adamw_prep(const double* partial, int32_t nparts, const float* used, float* steps, int32_t nseg,
+                   float lr, float beta1, float beta2, float max_norm, float* table, float* norm_out,
+                   vit_stream_t stream);
+/* per chunk c (chunks[3c..3c+2] = {segment, start element, length <= vit_adamw_chunk_elems()}), for the
+ * segment's active parameters, torch's AdamW (decoupled decay) on the clipped gradient g*coef:
+ *   p *= decay; m += (1-beta1)(g - m); v = beta2 v + (1-beta2) g^2;
+ *   p -= step_size * m / (sqrt(v) / sqrt(bc2) + eps);   g <- g*coef if write_grad; p_bf16 = bf16(p)
+ * decay = 1 - lr*weight_decay and the (1 - beta) factors are rounded from the caller's doubles, as torch's
+ * Python scalars are. */
+int vit_adamw_update(float* p, float* g, float* m, float* v, void* p_bf16, const int64_t* chunks, int32_t nchunks,
+                     const float* table, float decay, float beta1, float beta2, float one_minus_beta1,
+                     float one_minus_beta2, float eps, int32_t write_grad, vit_stream_t stream);
+int vit_adamw_chunk_elems(void);
+/* g[i] *= *coef (device scalar; the in-place scaling of clip_grad_norm_) */
+int vit_scale_by_coef(float* g, int64_t n, const float* coef, vit_stream_t stream);
+/* bytes of device memory at ptr set to 0 on the stream (hipMemsetAsync) */
+int vit_zero(void* ptr, int64_t bytes, vit_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,239 @@
+"""The Res-ViT training step (BASELINE config C5; res-vit/train.py:23-68) on the MI355X against three
+steps of the reference itself: tests/golden/resvit_train3.npz, written by
+tests/golden/make_resvit_train_golden.py from the imported res-vit/model.py driven by torch.optim.AdamW,
+torch.nn.utils.clip_grad_norm_(params, 1.0) and transformers.get_cosine_schedule_with_warmup. GPU only.
+
+* optimizer alone: the reference's recorded gradients fed to vitmi's clip_grad_norm_ + AdamW
+  (csrc/optim.hip, flat buffer): the clip norm, the clipped gradients, and after three steps every
+  parameter and its AdamW moments / step count to f32 rounding (1e-5 relative), including the
+  parameters some steps leave without a gradient (skipped, as torch skips `.grad is None`);
+* end to end: the three steps through vitmi.resvit_train.train_step with the reference's Gumbel draws
+  and routing decisions replayed: every step's losses (1e-3 relative; bf16 operands), clip norm
+  (2e-2) and the parameter trajectory (the accumulated update p3 - p0 of every tensor with a
+  meaningful update within 0.15 relative: Adam's first steps are ~lr * sign(g), so bf16-level gradient
+  noise flips the sign of near-zero gradient elements).
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from test_resvit_cpu import TINY
+
+pytestmark = pytest.mark.gpu
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def gold(golden_dir):
+    return np.load(os.path.join(golden_dir, "resvit_train3.npz"))
+
+
+def rel(a, b):
+    a = torch.as_tensor(a).detach().double().cpu()
+    b = torch.as_tensor(b).double().cpu()
+    return float((a - b).norm() / b.norm().clamp_min(1e-30))
+
+
+def hp(gold):
+    lr, wd, b1, b2, eps, warm, total, lc, la, ld = gold["hparams"].tolist()
+    return dict(lr=lr, wd=wd, betas=(b1, b2), eps=eps, warmup=int(warm), total=int(total), lc=lc, la=la, ld=ld)
+
+
+def build(gold):
+    from vitmi import resvit
+    torch.manual_seed(42)
+    m = resvit.Transformer(resvit.ModelArgs(**dict(TINY, device="cuda")))
+    m.load_state_dict({k[3:]: torch.from_numpy(gold[k]) for k in gold.files if k.startswith("p0/")})
+    return m.cuda()
+
+
+@pytest.mark.parametrize("fused", [False, True])
+def test_adamw_and_clip_match_reference_on_recorded_grads(gold, fused):
+    from vitmi.optim import AdamW, clip_grad_norm_, get_cosine_schedule_with_warmup
+    h = hp(gold)
+    m = build(gold)
+    trainable = [str(t) for t in gold["trainable"]]
+    named = dict(m.named_parameters())
+    opt = AdamW(m.parameters(), lr=h["lr"], weight_decay=h["wd"], betas=h["betas"], eps=h["eps"],
+                max_grad_norm=1.0 if fused else None)
+    sched = get_cosine_schedule_with_warmup(opt, h["warmup"], h["total"])
+    f = opt.flat
+    assert sorted(map(id, f.params)) == sorted(id(named[n]) for n in trainable)
+    for s in range(3):
+        assert opt.param_groups[0]["lr"] == pytest.approx(float(gold[f"s{s}/lr"]), rel=1e-12)
+        opt.zero_grad()
+        for n in trainable:  # the reference's gradients, as the backward would leave them
+            if bool(gold[f"s{s}/has_grad/{n}"]):
+                named[n].grad.copy_(torch.from_numpy(gold[f"s{s}/grad/{n}"]))
+                f.used_host[f.index(named[n])] = True
+        if not fused:
+            norm = clip_grad_norm_(None, 1.0, flat=opt)
+            assert float(norm) == pytest.approx(float(gold[f"s{s}/norm"]), rel=1e-6)
+        opt.step()
+        sched.step()
+        if fused:
+            assert float(opt.last_norm[0]) == pytest.approx(float(gold[f"s{s}/norm"]), rel=1e-6)
+        for n in trainable:  # .grad holds the clipped gradient afterwards (clip_grad_norm_ is in place)
+            if bool(gold[f"s{s}/has_grad/{n}"]):
+                assert rel(named[n].grad, gold[f"s{s}/cgrad/{n}"]) < 1e-6, (s, n)
+    bad = []
+    for n in trainable:
+        i = f.index(named[n])
+        if rel(named[n], gold["p3/" + n]) > 1e-5:
+            bad.append((n, "p", rel(named[n], gold["p3/" + n])))
+        d_ref = gold["p3/" + n].astype(np.float64) - gold["p0/" + n].astype(np.float64)
+        d_me = named[n].detach().double().cpu() - torch.from_numpy(gold["p0/" + n]).double()
+        if np.abs(d_ref).max() > 0 and rel(d_me, d_ref) > 1e-4:
+            bad.append((n, "update", rel(d_me, d_ref)))
+        if ("m3/" + n) in gold.files:
+            assert float(opt.steps[i]) == float(gold["t3/" + n]), n
+            rm, rv = rel(f.view(opt.exp_avg, i), gold["m3/" + n]), rel(f.view(opt.exp_avg_sq, i), gold["v3/" + n])
+            if rm > 1e-5 or rv > 1e-5:
+                bad.append((n, "moments", rm, rv))
+        else:
+            assert float(opt.steps[i]) == 0.0, n
+    assert not bad, bad
+    # a parameter with no gradient in some step kept its step count behind the others (torch's skip)
+    assert len({float(v) for v in opt.steps.cpu()}) > 1
+
+
+def _replay(m, gold, s):
+    routers = [l.router for l in m.layers if hasattr(l, "router")]
+    for j, r in enumerate(routers):
+        hard = torch.from_numpy(gold[f"s{s}/router{j}_hard"]).cuda()
+        g = torch.from_numpy(gold[f"s{s}/gumbel{j}"]).cuda()
+        r.hard_override = lambda logits, hh=hard: hh
+        r.gumbel_noise = lambda logits, gg=g: gg
+
+
+@pytest.mark.parametrize("fused", [False, True])
+def test_three_training_steps_match_reference(gold, fused):
+    from vitmi.optim import AdamW, get_cosine_schedule_with_warmup
+    from vitmi.resvit_train import train_step
+    h = hp(gold)
+    m = build(gold).train()
+    opt = AdamW(m.parameters(), lr=h["lr"], weight_decay=h["wd"], betas=h["betas"], eps=h["eps"],
+                max_grad_norm=1.0 if fused else None)
+    sched = get_cosine_schedule_with_warmup(opt, h["warmup"], h["total"])
+    trainable = [str(t) for t in gold["trainable"]]
+    named = dict(m.named_parameters())
+    for s in range(3):
+        _replay(m, gold, s)
+        x = torch.from_numpy(gold[f"s{s}/x"]).cuda()
+        y = torch.from_numpy(gold[f"s{s}/y"]).cuda()
+        total, c, a, d, ent, _ = train_step(m, x, y, opt, sched, h["la"], h["ld"], h["lc"], clip_grad_norm=True)
+        assert abs(float(c) - float(gold[f"s{s}/c_loss"])) <= 1e-3 * float(gold[f"s{s}/c_loss"]), s
+        assert abs(float(total) - float(gold[f"s{s}/total"])) <= 1e-3 * float(gold[f"s{s}/total"]), s
+        assert abs(float(d) - float(gold[f"s{s}/d_loss"])) <= 2e-2 * float(gold[f"s{s}/d_loss"]), s
+        # (after the first update the parameter trajectory itself carries bf16-level differences)
+        assert rel(m.logits, gold[f"s{s}/logits"]) < (1e-2 if s == 0 else 2e-2), s
+        # which parameters got a gradient is the reference's (routing replayed)
+        for n in trainable:
+            assert opt.flat.used_host[opt.flat.index(named[n])] == bool(gold[f"s{s}/has_grad/{n}"]), (s, n)
+        # the clip's input norm (vitmi AdamW keeps {norm, coef} of its last clip, fused or not)
+        assert float(opt.last_norm[0]) == pytest.approx(float(gold[f"s{s}/norm"]), rel=2e-2), s
+    tot_upd = sum(float(np.square(gold["p3/" + n].astype(np.float64) - gold["p0/" + n]).sum()) for n in trainable)
+    bad = []
+    for n in trainable:
+        d_ref = gold["p3/" + n].astype(np.float64) - gold["p0/" + n].astype(np.float64)
+        if float(np.square(d_ref).sum()) < 1e-4 * tot_upd:
+            continue
+        d_me = named[n].detach().double().cpu() - torch.from_numpy(gold["p0/" + n]).double()
+        if rel(d_me, d_ref) > 0.15:
+            bad.append((n, rel(d_me, d_ref)))
+    assert not bad, bad
+
+
+def test_flat_params_keep_grad_views_and_skip_unused():
+    """FlatParams: parameters become views of one buffer, autograd accumulates into the preset .grad
+    views in place, a parameter outside the graph is marked unused, module.zero_grad() (set_to_none)
+    is recovered by adopt_grads()."""
+    from vitmi.flat import FlatParams
+    a = torch.nn.Parameter(torch.randn(5, 7, device="cuda"))
+    b = torch.nn.Parameter(torch.randn(3, device="cuda"))
+    c = torch.nn.Parameter(torch.randn(130, device="cuda"))
+    a0, b0 = a.detach().clone(), b.detach().clone()
+    f = FlatParams([a, b, c])
+    assert torch.equal(a.detach(), a0) and torch.equal(b.detach(), b0)
+    assert all(o % 64 == 0 for o in f.offsets)
+    f.zero_grad()
+    (a.sum() * 2 + (b * b).sum()).backward()
+    assert a.grad.data_ptr() == f.view(f.grad, f.index(a)).data_ptr()
+    assert torch.allclose(a.grad, torch.full_like(a, 2.0)) and torch.allclose(b.grad, 2 * b0)
+    assert f.used_host[f.index(a)] and f.used_host[f.index(b)] and not f.used_host[f.index(c)]
+    f.zero_grad()
+    assert float(f.grad.abs().sum()) == 0.0 and not any(f.used_host)
+    a.grad = None  # e.g. nn.Module.zero_grad()
+    (a * 3).sum().backward()
+    f.adopt_grads()
+    assert a.grad.data_ptr() == f.view(f.grad, f.index(a)).data_ptr()
+    assert torch.allclose(a.grad, torch.full_like(a, 3.0))
+
+
+def test_resvit_data_parallel_two_ranks(tmp_path):
+    """Res-ViT DP (new: the reference is single-device): 2 ranks on one GPU over gloo, 4 images each,
+    FlatGradAllReducer on the LoRA / router / approximator / head gradients, vitmi AdamW with the clip
+    folded in. Both replicas end bit-identical, and (lambda_active = 0: the ratio loss is a non-linear
+    function of the per-rank mean) equal to one 8-image step of a single process within 2e-2 of the
+    update."""
+    script = tmp_path / "dp_resvit.py"
+    script.write_text(r'''
+import os, sys, torch, numpy as np, torch.distributed as dist
+sys.path.insert(0, os.path.join(os.environ["REPO"], "vit-of-pytorch_amd")); sys.path.insert(0, os.environ["REPO"])
+sys.path.insert(0, os.path.join(os.environ["REPO"], "tests"))
+from test_resvit_cpu import TINY
+from vitmi import resvit
+from vitmi.optim import AdamW
+from vitmi.dist import FlatGradAllReducer
+from vitmi.resvit_train import train_step
+rank = int(os.environ["RANK"]); world = int(os.environ["WORLD_SIZE"])
+dist.init_process_group("gloo")
+g = torch.Generator().manual_seed(5)
+X = torch.randn(8, 3, 32, 32, generator=g); Y = torch.randint(0, 10, (8,), generator=g)
+
+def make():
+    torch.manual_seed(42)
+    m = resvit.Transformer(resvit.ModelArgs(**dict(TINY, device="cuda"))).cuda().train()
+    gn = torch.Generator().manual_seed(9)
+    for j, l in enumerate([l for l in m.layers if hasattr(l, "router")]):
+        noise = -torch.empty(8, 17, 2, 2).exponential_(generator=gn).log()  # [B, tokens, block_size, 2]
+        l.router.gumbel_noise = (lambda nz: lambda logits: nz[:logits.shape[0]] if logits.shape[0] == 8 else
+                                 nz[rank * 4:(rank + 1) * 4])(noise.cuda())
+    return m
+
+def run(m, x, y, reducer=None):
+    opt = AdamW(m.parameters(), lr=1e-2, weight_decay=0.05, max_grad_norm=1.0)
+    if reducer:
+        red = FlatGradAllReducer(opt.flat, bucket_elems=2000).attach()
+    for _ in range(2):
+        train_step(m, x, y, opt, None, 0.0, 1e-2, 1.0, True, red if reducer else None)
+    torch.cuda.synchronize()
+    return torch.cat([p.detach().reshape(-1) for p in m.parameters()]).cpu()
+
+m = make()
+flat = run(m, X[rank * 4:(rank + 1) * 4].cuda(), Y[rank * 4:(rank + 1) * 4].cuda(), reducer=True)
+out = [torch.zeros_like(flat) for _ in range(world)]
+dist.all_gather(out, flat)
+if rank == 0:
+    assert torch.equal(out[0], out[1]), "replicas diverged"
+    torch.manual_seed(42)
+    p0 = torch.cat([p.detach().reshape(-1) for p in resvit.Transformer(resvit.ModelArgs(**dict(TINY, device="cuda"))).parameters()])
+    ref = run(make(), X.cuda(), Y.cuda())
+    r = float((flat - ref).norm() / (ref - p0).norm())
+    print("rel", r)
+    assert r < 2e-2, r
+dist.barrier()
+dist.destroy_process_group()
+open(os.path.join(os.environ["OUTDIR"], f"rank{rank}.ok"), "w").write("ok")
+''')
+    import subprocess
+    import sys
+    env = dict(os.environ, REPO=REPO, OUTDIR=str(tmp_path), MASTER_ADDR="127.0.0.1", MASTER_PORT="29541")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2", "--master-addr",
+           "127.0.0.1", "--master-port", "29541", str(script)]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert (tmp_path / "rank0.ok").exists() and (tmp_path / "rank1.ok").exists()

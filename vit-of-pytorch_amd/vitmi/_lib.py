@@ -17,7 +17,7 @@ c_i32 = ctypes.c_int32
 c_f32 = ctypes.c_float
 c_vp = ctypes.c_void_p
 
-ABI_VERSION = 5  # vit_abi_version() of the library these prototypes describe
+ABI_VERSION = 6  # vit_abi_version() of the library these prototypes describe
 
 # enum vit_layout / vit_epilogue (include/vit_hip.h)
 K_CONTIG, MN_CONTIG = 0, 1
@@ -97,6 +97,13 @@ _SIGS = {
     "vit_unpack_bf16_f32": (c_i32, [c_vp, c_i64, c_i64, c_i64, c_vp, c_i64, c_vp]),
     "vit_attention_fwd_varlen": (c_i32, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_i64, c_i64,
                                          c_i64, c_i64, c_f32, c_vp]),
+    "vit_sqnorm_partial": (c_i32, [c_vp, c_i64, c_vp, c_i32, c_vp]),
+    "vit_adamw_prep": (c_i32, [c_vp, c_i32, c_vp, c_vp, c_i32, c_f32, c_f32, c_f32, c_f32, c_vp, c_vp, c_vp]),
+    "vit_adamw_update": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_vp, c_f32, c_f32, c_f32, c_f32, c_f32,
+                                 c_f32, c_i32, c_vp]),
+    "vit_adamw_chunk_elems": (c_i32, []),
+    "vit_scale_by_coef": (c_i32, [c_vp, c_i64, c_vp, c_vp]),
+    "vit_zero": (c_i32, [c_vp, c_i64, c_vp]),
 }
 
 EXPORTED = tuple(_SIGS)

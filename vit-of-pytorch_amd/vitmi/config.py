@@ -19,7 +19,8 @@ from datetime import datetime
 
 
 def _add_common(parser, train: bool):
-    parser.add_argument("--n-gpu", type=int, default=1, help="number of gpus to use")
+    parser.add_argument("--n-gpu", type=int, default=1,
+                        help="number of gpus to use (one rank per GPU; --batch-size is the global batch)")
     parser.add_argument("--model-arch", type=str, default="b16", help="model setting to use",
                         choices=["b16", "b32", "l16", "l32", "h14"])
     parser.add_argument("--batch-size", type=int, default=32, help="batch size")
@@ -137,7 +138,9 @@ def get_h14_config(config):
 
 def process_config(config):
     """Experiment directories + config.json (reference src/utils.py:56-76)."""
-    timestamp = datetime.now().strftime("%y%m%d_%H%M%S")
+    # (ranks started by `--n-gpu k` inherit their launcher's stamp, so all share one experiment dir)
+    timestamp = os.environ.get("VITMI_EXP_STAMP") or datetime.now().strftime("%y%m%d_%H%M%S")
+    config.exp_stamp = timestamp
     exp_name = config.exp_name + "_{}_bs{}_lr{}_wd{}".format(config.dataset, config.batch_size, config.lr, config.wd)
     exp_name += "_" + timestamp
     config.summary_dir = os.path.join("experiments", "tb", exp_name)

@@ -116,3 +116,91 @@ class GradAllReducer:
         for t in self._to_scale:
             t.mul_(1.0 / self.world)
         self._to_scale = []
+
+
+class FlatGradAllReducer:
+    """Data-parallel gradient exchange for parameters held by a vitmi.flat.FlatParams (the Res-ViT
+    trainable set: LoRA, routers, approximators, head), overlapped with the autograd backward.
+
+    The flat gradient buffer is cut into buckets of whole parameters (~bucket_elems each, in the
+    buffer's order, which is the order the backward finishes them). Each parameter's post-accumulate
+    hook counts it into its bucket; a complete bucket is all-reduced on the exchange stream while the
+    backward continues. Buckets are launched strictly in index order — every rank issues the same
+    sequence of collectives even when dynamic routing leaves a parameter without a gradient on one rank
+    (its bucket then waits for finish(), which launches whatever is left, in order). The used flags
+    (which parameters received a gradient anywhere) are summed across ranks in the last collective, so
+    every replica's AdamW skips / updates the same parameters and the replicas stay bit-identical."""
+
+    def __init__(self, flat, group=None, bucket_elems=4 << 20, average=True):
+        self.flat = flat
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.average = average
+        self.native_avg = average and dist.is_initialized() and dist.get_backend(group) == "nccl"
+        self.cuda = flat.device.type == "cuda"
+        self.stream = torch.cuda.Stream(device=flat.device) if self.cuda else None
+        self.buckets, cur, start = [], [], 0
+        self.bucket_of = [0] * flat.nseg
+        for i, (p, o) in enumerate(zip(flat.params, flat.offsets)):
+            cur.append(i)
+            end = flat.offsets[i + 1] if i + 1 < flat.nseg else flat.numel
+            if end - start >= bucket_elems or i + 1 == flat.nseg:
+                self.buckets.append((start, end, len(cur)))
+                for j in cur:
+                    self.bucket_of[j] = len(self.buckets) - 1
+                cur, start = [], end
+        self._reset()
+
+    def _reset(self):
+        self.count = [0] * len(self.buckets)
+        self.launched = 0
+
+    def attach(self):
+        self.flat.on_grad = self._on_grad
+        return self
+
+    def detach(self):
+        self.flat.on_grad = None
+
+    def _launch(self, k):
+        s, e, _ = self.buckets[k]
+        t = self.flat.grad[s:e]
+        op = dist.ReduceOp.AVG if self.native_avg else dist.ReduceOp.SUM
+        if self.cuda:
+            self.stream.wait_stream(torch.cuda.current_stream(self.flat.device))
+            with torch.cuda.stream(self.stream):
+                dist.all_reduce(t, op=op, group=self.group)
+        else:
+            dist.all_reduce(t, op=op, group=self.group)
+
+    def _on_grad(self, i):
+        if self.world == 1:
+            return
+        k = self.bucket_of[i]
+        self.count[k] += 1
+        while self.launched < len(self.buckets) and self.count[self.launched] >= self.buckets[self.launched][2]:
+            self._launch(self.launched)
+            self.launched += 1
+
+    def finish(self):
+        """launch the buckets still pending (in order), OR the used flags over ranks, and make the current
+        stream wait; call after backward, before clip / optimizer step"""
+        if self.world == 1:
+            self._reset()
+            return
+        for k in range(self.launched, len(self.buckets)):
+            self._launch(k)
+        f = self.flat
+        used = f.upload_used()
+        cur = torch.cuda.current_stream(f.device) if self.cuda else None
+        if self.cuda:
+            self.stream.wait_stream(cur)
+            with torch.cuda.stream(self.stream):
+                dist.all_reduce(used, op=dist.ReduceOp.SUM, group=self.group)
+            cur.wait_stream(self.stream)
+        else:
+            dist.all_reduce(used, op=dist.ReduceOp.SUM, group=self.group)
+        f.used_reduced = True  # the device flags now hold the all-rank sums (> 0: received a gradient)
+        if self.average and not self.native_avg:
+            f.grad.mul_(1.0 / self.world)
+        self._reset()

@@ -302,7 +302,7 @@ class ViTEngine:
         # for them, so they fill the tails of the GEMM launches instead of sitting between them
         self._bias_st = None
         self.probe = None  # list: (start, end) HIP events around every fc1 forward GEMM launch
-        self.probe_wgrad = None  # list: (start, end, flop) around every split-K weight-gradient GEMM launch
+        self.probe_wgrad = None  # list: (start, end, flop, K) around every split-K weight-gradient GEMM launch
         # dropout (nn.Dropout of PositionEmbs / EncoderBlock / MlpBlock, reference src/model.py:19-20,
         # 46-49, 124-125): counter-based Philox masks keyed by (seed, per-forward offset, site, row,
         # col), regenerated by the backward instead of stored. Seeded from torch's initial seed.
@@ -396,7 +396,7 @@ class ViTEngine:
         if self.probe_wgrad is not None:
             ev1 = torch.cuda.Event(enable_timing=True)
             ev1.record()
-            self.probe_wgrad.append((ev0, ev1, 2.0 * M * N * K * batch))
+            self.probe_wgrad.append((ev0, ev1, 2.0 * M * N * K * batch, K))
         ops.splitk_reduce(ws, batch, s, M, N, out, ldo, out_bs)
 
     # ---- forward -------------------------------------------------------------------------------

@@ -297,3 +297,38 @@ def attention_fwd_varlen(q, ldq, k, ldk, v, ldv, o, ldo, cu_q, B, max_q, Nkv, H,
     _chk(cu_q, torch.int32, "cu_q")
     check(lib().vit_attention_fwd_varlen(_p(q), ldq, _p(k), ldk, _p(v), ldv, _p(o), ldo, _p(cu_q), B, max_q, Nkv, H,
                                          hd, scale, _stream()), "vit_attention_fwd_varlen")
+
+
+# ---- Res-ViT optimizer step: clip_grad_norm_ + AdamW over a flat buffer (csrc/optim.hip) ----------
+def sqnorm_partial(g, n, partial):
+    _chk(g, F32, "g")
+    _chk(partial, torch.float64, "partial")
+    check(lib().vit_sqnorm_partial(_p(g), n, _p(partial), partial.numel(), _stream()), "vit_sqnorm_partial")
+
+
+def adamw_prep(partial, used, steps, lr, beta1, beta2, max_norm, table, norm_out):
+    nseg = 0 if steps is None else steps.numel()
+    check(lib().vit_adamw_prep(_p(partial), 0 if partial is None else partial.numel(), _p(used), _p(steps), nseg,
+                               lr, beta1, beta2, max_norm, _p(table), _p(norm_out), _stream()), "vit_adamw_prep")
+
+
+def adamw_update(p, g, m, v, p_bf16, chunks, table, lr, beta1, beta2, eps, wd, write_grad):
+    # (1 - lr*wd) and (1 - beta) in double, then rounded: torch's Python-scalar arithmetic
+    check(lib().vit_adamw_update(_p(p), _p(g), _p(m), _p(v), _p(p_bf16), _p(chunks), chunks.numel() // 3, _p(table),
+                                 1.0 - lr * wd, beta1, beta2, 1.0 - beta1, 1.0 - beta2, eps, int(write_grad),
+                                 _stream()), "vit_adamw_update")
+
+
+def adamw_chunk_elems():
+    return lib().vit_adamw_chunk_elems()
+
+
+def scale_by_coef(g, n, coef):
+    check(lib().vit_scale_by_coef(_p(g), n, _p(coef), _stream()), "vit_scale_by_coef")
+
+
+def zero_(t):
+    """t[...] = 0 with hipMemsetAsync on the current stream (contiguous tensors)"""
+    if not t.is_contiguous():
+        raise ValueError("zero_: contiguous tensor expected")
+    check(lib().vit_zero(_p(t), t.numel() * t.element_size(), _stream()), "vit_zero")

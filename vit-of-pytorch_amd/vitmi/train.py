@@ -1,7 +1,8 @@
 """Training driver, mirroring reference src/train.py on the MI355X HIP engine.
 
     python -m vitmi.train --model-arch b16 --batch-size 256 --synthetic --checkpoint-path "" --no-save
-    torchrun --nproc-per-node 8 -m vitmi.train ...   # data parallel, one process per GPU (RCCL)
+    python -m vitmi.train --n-gpu 8 --batch-size 512 ...     # data parallel: starts 8 ranks (RCCL)
+    torchrun --nproc-per-node 8 -m vitmi.train --n-gpu 8 ... # the same ranks under an outside launcher
 
 Entry points keep the reference signatures: train_epoch (src/train.py:12-37), valid_epoch (:40-66),
 save_model (:69-81), main (:84-194); MetricTracker / the step writer follow src/utils.py:79-100,
@@ -11,7 +12,13 @@ save_model (:69-81), main (:84-194); MetricTracker / the step writer follow src/
     by the reference (:159-163);
   * multi-GPU is one process per GPU with gradient all-reduce over RCCL overlapped with the
     backward (vitmi.dist, attached to the model's engine: the backward hands autograd reduced
-    gradients), instead of single-process nn.DataParallel (:128-129);
+    gradients), instead of single-process nn.DataParallel (:128-129). `--n-gpu k` keeps its meaning:
+    main() starts k ranks itself (torch.distributed.run, before anything touches the GPU), after
+    clamping k to the visible GPUs with the reference's warning (src/utils.py:44-54). `--batch-size`
+    stays the GLOBAL batch, as under DataParallel (which scatters it): each rank takes batch/k
+    images, and the per-rank mean loss averaged over ranks is the global-batch mean;
+  * the printed loss and the returned {loss, acc1, acc5} means are averaged over ranks (what the
+    reference computes on the gathered batch);
   * loss / top-1 / top-5 come from the fused cross-entropy kernel's per-row statistics and are
     accumulated on the device, read back when printed, instead of three .item() host syncs per
     step (:29-32); the reported means are the same.
@@ -56,10 +63,16 @@ def accuracy(output, target, topk=(1,)):
 class StepWriter:
     """The metrics writer interface train_epoch / valid_epoch drive (reference SwanLabWriter,
     src/utils.py:177-230, with SwanLab absent): set_step / add_scalar / log_metric, keeping the
-    step, mode and steps_per_sec in memory (device scalars stay on the device)."""
+    step, mode and steps_per_sec in memory. Device scalars are kept as detached device tensors (no
+    host sync per step); `scalars_host()` reads them back in one batch."""
 
     def __init__(self, log_dir=None, enabled=False):
-        self.enabled = False  # no SwanLab / TensorBoard backend in this environment
+        if enabled:
+            import warnings
+            warnings.warn("StepWriter: no SwanLab / TensorBoard backend in this environment; scalars are kept "
+                          "in memory only (log_dir=%r ignored)" % (log_dir,), stacklevel=2)
+        self.enabled = False
+        self.log_dir = log_dir
         self.step = 0
         self.mode = ""
         self.timer = time.perf_counter()
@@ -70,16 +83,26 @@ class StepWriter:
         self.step = step
         now = time.perf_counter()
         if step != 0:
+            # host-side rate between set_step calls: with asynchronous launches this is the rate at which
+            # steps are issued, which tracks GPU throughput only once the launch queue is full
             self.log_metric("steps_per_sec", 1.0 / max(now - self.timer, 1e-9))
         self.timer = now
 
     def add_scalar(self, tag, data, *args, **kwargs):
+        if torch.is_tensor(data):
+            data = data.detach().clone()
         self.scalars.append((self.step, f"{tag}/{self.mode}" if self.mode else tag, data))
         if len(self.scalars) > 4096:
             del self.scalars[:2048]
 
     def log_metric(self, tag, data, *args, **kwargs):
         self.add_scalar(tag, data)
+
+    def scalars_host(self):
+        """[(step, tag, float)] with every device scalar read back in one transfer"""
+        dev = [v for _, _, v in self.scalars if torch.is_tensor(v)]
+        host = iter(torch.stack([v.reshape(()).double() for v in dev]).cpu().tolist()) if dev else iter(())
+        return [(s, t, next(host) if torch.is_tensor(v) else float(v)) for s, t, v in self.scalars]
 
 
 class MetricTracker:
@@ -106,7 +129,20 @@ class MetricTracker:
         return t / max(1, self._count[key])
 
     def result(self):
+        if dist.is_initialized() and dist.get_world_size() > 1:
+            return self._result_all_ranks()
         return {k: self.avg(k) for k in self.keys}
+
+    def _result_all_ranks(self):
+        """means over every rank's batches (equal per-rank batch sizes: the mean of rank means)"""
+        dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl" else torch.device("cpu")
+        tot = [self._total[k] for k in self.keys]
+        t = torch.stack([(v.detach().double().to(dev) if torch.is_tensor(v) else torch.tensor(float(v), dtype=torch.float64,
+                                                                                           device=dev)) for v in tot] +
+                        [torch.tensor(float(self._count[k]), dtype=torch.float64, device=dev) for k in self.keys])
+        dist.all_reduce(t)
+        n = len(self.keys)
+        return {k: float(t[i]) / max(1.0, float(t[n + i])) for i, k in enumerate(self.keys)}
 
 
 def _step_accuracy(criterion, pred, target):
@@ -168,6 +204,16 @@ def _world():
     return dist.get_world_size() if dist.is_initialized() else 1
 
 
+def _rank_mean(*vals):
+    """host floats of device / host scalars, averaged over ranks when data parallel"""
+    if not (dist.is_initialized() and dist.get_world_size() > 1):
+        return [float(v) for v in vals]
+    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl" else torch.device("cpu")
+    t = torch.stack([torch.as_tensor(v, dtype=torch.float64).to(dev).reshape(()) for v in vals])
+    dist.all_reduce(t)
+    return [float(v) / dist.get_world_size() for v in t]
+
+
 def train_epoch(epoch, model, data_loader, criterion, optimizer, lr_scheduler, metrics, device=torch.device("cpu")):
     """reference src/train.py:12-37 (one optimizer step per batch)."""
     metrics.reset()
@@ -185,9 +231,11 @@ def train_epoch(epoch, model, data_loader, criterion, optimizer, lr_scheduler, m
         metrics.update("loss", loss.detach())
         metrics.update("acc1", acc1)
         metrics.update("acc5", acc5)
-        if batch_idx % 100 == 0 and (not dist.is_initialized() or dist.get_rank() == 0):
-            print("Train Epoch: {:03d} Batch: {:05d}/{:05d} Loss: {:.4f} Acc@1: {:.2f}, Acc@5: {:.2f}"
-                  .format(epoch, batch_idx, len(data_loader), float(loss.detach()), float(acc1), float(acc5)), flush=True)
+        if batch_idx % 100 == 0:
+            shown = _rank_mean(loss.detach(), acc1, acc5)
+            if not dist.is_initialized() or dist.get_rank() == 0:
+                print("Train Epoch: {:03d} Batch: {:05d}/{:05d} Loss: {:.4f} Acc@1: {:.2f}, Acc@5: {:.2f}"
+                      .format(epoch, batch_idx, len(data_loader), *shown), flush=True)
     return metrics.result()
 
 
@@ -238,18 +286,65 @@ def build_model(config, device):
                              dropout_rate=config.dropout_rate)
 
 
+def _launched_world(config):
+    """(world, rank, local rank) of this process. Under torch.distributed.run the environment says;
+    --n-gpu must then be 1 (unset) or equal to WORLD_SIZE."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if "WORLD_SIZE" in os.environ and config.n_gpu not in (1, world):
+        raise SystemExit(f"--n-gpu {config.n_gpu} but the launcher started WORLD_SIZE={world} ranks")
+    return world, int(os.environ.get("RANK", "0")), int(os.environ.get("LOCAL_RANK", "0"))
+
+
+def rank_batch(global_batch, world):
+    """images per rank for a global --batch-size (DataParallel scatter semantics, src/train.py:128-129)"""
+    if global_batch % world:
+        raise SystemExit(f"--batch-size {global_batch} is the global batch and must divide evenly over {world} "
+                         "GPUs (every rank's mean loss carries the same weight in the averaged gradient)")
+    return global_batch // world
+
+
 def main(argv=None):
     config = get_train_config(argv)
+    if "WORLD_SIZE" not in os.environ and config.n_gpu > 1:
+        # reference setup_device (src/utils.py:44-54): clamp to the visible GPUs with a warning;
+        # then one rank per GPU, started here before any HIP call (device_count() makes none)
+        n = torch.cuda.device_count()
+        k = config.n_gpu
+        if k > n and not os.environ.get("VITMI_SHARE_GPU"):
+            print("Warning: The number of GPU's configured to use is {}, but only {} are available on this "
+                  "machine.".format(k, n))
+            k = n
+        if k > 1:
+            rank_batch(config.batch_size, k)
+            import subprocess
+            from socket import socket
+            with socket() as s_:
+                s_.bind(("127.0.0.1", 0))
+                port = str(s_.getsockname()[1])
+            args = list(sys.argv[1:] if argv is None else argv)
+            args += ["--n-gpu", str(k)]  # (argparse: the last occurrence wins)
+            pkg = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+            env = dict(os.environ, VITMI_EXP_STAMP=getattr(config, "exp_stamp", ""))
+            env["PYTHONPATH"] = os.pathsep.join([pkg] + ([env["PYTHONPATH"]] if env.get("PYTHONPATH") else []))
+            rc = subprocess.call([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                                  f"--nproc-per-node={k}", "--master-addr", "127.0.0.1", "--master-port", port,
+                                  "-m", "vitmi.train", *args], env=env)
+            if rc:
+                raise SystemExit(rc)
+            return None
+        config.n_gpu = k
     set_seed(config.seed)
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    world, rank, local = _launched_world(config)
     if not torch.cuda.is_available():
         raise SystemExit("vitmi.train needs a ROCm GPU (MI355X)")
+    if os.environ.get("VITMI_SHARE_GPU"):  # functional rehearsal of the N>1 path on fewer GPUs (gloo)
+        local %= max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group(os.environ.get("VITMI_DIST_BACKEND", "nccl"), device_id=device)
+        backend = os.environ.get("VITMI_DIST_BACKEND", "nccl")
+        dist.init_process_group(backend, **({"device_id": device} if backend == "nccl" else {}))
+    batch = rank_batch(config.batch_size, world)
 
     model = build_model(config, device)
     if config.checkpoint_path:
@@ -274,15 +369,15 @@ def main(argv=None):
     if config.synthetic_source_size > 0:
         # uint8 images (CIFAR-shaped when 32) through the device-side reference transform
         g = torch.Generator().manual_seed(config.seed + rank)
-        n = config.batch_size * config.steps_per_epoch
+        n = batch * config.steps_per_epoch
         src = torch.randint(0, 256, (n, config.synthetic_source_size, config.synthetic_source_size, 3),
                             generator=g, dtype=torch.uint8)
         train_loader = DeviceImageLoader(src, torch.randint(0, config.num_classes, (n,), generator=g),
-                                         config.batch_size, config.image_size, device, seed=config.seed + rank)
+                                         batch, config.image_size, device, seed=config.seed + rank)
     else:
-        train_loader = SyntheticDataLoader(config.batch_size, config.image_size, config.num_classes,
+        train_loader = SyntheticDataLoader(batch, config.image_size, config.num_classes,
                                            config.steps_per_epoch, device, seed=config.seed + rank)
-    valid_loader = SyntheticDataLoader(config.batch_size, config.image_size, config.num_classes,
+    valid_loader = SyntheticDataLoader(batch, config.image_size, config.num_classes,
                                        max(1, config.steps_per_epoch // 10), device, seed=10_000 + config.seed + rank)
 
     criterion = CrossEntropyLoss()
