@@ -359,36 +359,41 @@ def test_large_arch_step_matches_oracle(cfg, bs):
     assert rel(exact, ref_logits) < 1e-3, rel(exact, ref_logits)
 
 
-def test_b16_bs256_step_consistent_with_small_batches():
-    """The benchmarked shape (ViT-B/16 @224, bs 256, T = 50 432 rows: wave-split GEMM tiles, split-K
-    weight gradients, 3072-(image, head) attention grid) against 128 bs-2 runs of the same images:
-    logits / per-image loss equal within bf16 tolerance, and the bs-256 gradient equals the mean of
-    the bs-2 gradients; an 8-image slice's loss against the oracle (fp32 CPU)."""
+@pytest.mark.parametrize("cfg,bs,small,nref", [(B16, 256, 2, 8), (L16, 64, 2, 4), (H14, 128, 4, 4)],
+                         ids=["b16_bs256", "l16_bs64", "h14_bs128"])
+def test_benchmarked_step_consistent_with_small_batches(cfg, bs, small, nref):
+    """The benchmarked per-GPU shapes — ViT-B/16 bs 256 (config C2, T = 50 432 rows), ViT-L/16 bs 64 (C3's
+    512 over 8 GPUs, T = 12 608) and ViT-H/14 bs 128 (C4's 1024 over 8, T = 32 896, hd 80, N 257): their
+    wave-split GEMM tiles, split-K weight gradients and attention grids against bs-`small` runs of the
+    same images: logits / per-image loss equal within bf16 tolerance, the big-batch gradient equals the
+    mean of the small-batch gradients; an `nref`-image slice's logits and loss against the oracle (fp32
+    CPU). Reference src/config.py:57-104 (presets)."""
     from vitmi.engine import ArchConfig, ViTEngine
-    cfg = B16
     params = tame_params(init_params(cfg, seed=42))
-    eng = ViTEngine(ArchConfig())
+    eng = ViTEngine(ArchConfig(image_size=cfg.image_size, patch_size=cfg.patch_size, emb_dim=cfg.emb_dim,
+                               mlp_dim=cfg.mlp_dim, num_heads=cfg.num_heads, num_layers=cfg.num_layers,
+                               num_classes=cfg.num_classes))
     eng.load_params(params)
     eng.refresh_mirror()
     g = torch.Generator().manual_seed(23)
-    x = torch.randn(256, 3, 224, 224, generator=g)
-    y = torch.randint(0, 1000, (256,), generator=g)
+    x = torch.randn(bs, 3, cfg.image_size, cfg.image_size, generator=g)
+    y = torch.randint(0, cfg.num_classes, (bs,), generator=g)
     xd, yd = x.cuda(), y.cuda()
     logits = eng.forward(xd).clone()
     _, st = eng.cross_entropy(yd)
     loss_rows = st[:, 0].clone()
-    gbig = eng.backward(eng.cross_entropy(yd, grad_scale=1.0 / 256)[0]).clone()
+    gbig = eng.backward(eng.cross_entropy(yd, grad_scale=1.0 / bs)[0]).clone()
     small_logits, small_loss = [], []
     gsum = torch.zeros_like(gbig)
-    for k in range(0, 256, 2):
-        small_logits.append(eng.forward(xd[k:k + 2]).clone())
-        dl, st2 = eng.cross_entropy(yd[k:k + 2], grad_scale=1.0 / 256)
+    for k in range(0, bs, small):
+        small_logits.append(eng.forward(xd[k:k + small]).clone())
+        dl, st2 = eng.cross_entropy(yd[k:k + small], grad_scale=1.0 / bs)
         small_loss.append(st2[:, 0].clone())
         gsum += eng.backward(dl)
     torch.cuda.synchronize()
     assert rel(logits, torch.cat(small_logits)) < 5e-3
     assert rel(loss_rows, torch.cat(small_loss)) < 1e-3
     assert rel(gbig, gsum) < 1e-2, rel(gbig, gsum)
-    ref_logits, ref_loss, _ = loss_and_grads(params, x[:8], y[:8], cfg)
-    assert rel(logits[:8], ref_logits) < 1e-2
-    assert abs(float(loss_rows[:8].mean()) - float(ref_loss)) <= 1e-3 * float(ref_loss)
+    ref_logits, ref_loss, _ = loss_and_grads(params, x[:nref], y[:nref], cfg)
+    assert rel(logits[:nref], ref_logits) < 1e-2
+    assert abs(float(loss_rows[:nref].mean()) - float(ref_loss)) <= 1e-3 * float(ref_loss)

@@ -240,10 +240,11 @@ def test_train_n_gpu_2_starts_two_ranks():
     env = dict(os.environ, VITMI_SHARE_GPU="1", VITMI_DIST_BACKEND="gloo",
                PYTHONPATH=os.path.join(REPO, "vit-of-pytorch_amd"))
     env.pop("WORLD_SIZE", None)
-    r = subprocess.run([sys.executable, "-m", "vitmi.train", "--n-gpu", "2", "--model-arch", "b32", "--batch-size", "16",
-                        "--synthetic", "--checkpoint-path", "", "--steps-per-epoch", "4", "--train-steps", "8",
-                        "--warmup-steps", "2", "--no-save", "--num-classes", "10"],
-                       env=env, capture_output=True, text=True, timeout=600)
+    # (config C1's shape, as test_train_main_c1_cifar100_shape runs it on one GPU: global batch 32)
+    r = subprocess.run([sys.executable, "-m", "vitmi.train", "--n-gpu", "2", "--model-arch", "b32", "--image-size", "32",
+                        "--any-image-size", "--batch-size", "32", "--num-classes", "100", "--synthetic",
+                        "--checkpoint-path", "", "--steps-per-epoch", "3", "--train-steps", "6", "--warmup-steps", "2",
+                        "--no-save"], env=env, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     assert r.stdout.count("val_acc1") == 2  # 2 epochs, printed by rank 0 only
     losses = [float(l.split("Loss: ")[1].split()[0]) for l in r.stdout.splitlines() if l.startswith("Train Epoch")]

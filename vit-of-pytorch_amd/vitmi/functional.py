@@ -11,7 +11,8 @@ kernels (LDS-resident or K/V-tiled), LayerNorm, GELU, counter-based dropout.
 
 There is no PyTorch compute fallback: every function raises on CPU tensors. Padding copies are
 allocated per call (the standalone path favours generality over the engine's preallocated
-workspaces).
+workspaces); bf16 copies of weights that take no gradient (LoRA's frozen bases) are cached per
+weight version.
 """
 from __future__ import annotations
 
@@ -41,11 +42,48 @@ def _f32(t):
 
 
 def _pad_bf16(x2, rows_p, cols_p):
-    """bf16 copy of f32 [rows][cols] in a zero [rows_p][cols_p] buffer."""
+    """bf16 copy of f32 [rows][cols] in a [rows_p][cols_p] buffer whose padding is zero (vit_cast_pad_rows
+    zeroes the pad columns; only the pad rows are cleared separately)."""
     rows, cols = x2.shape
-    out = torch.zeros(rows_p, cols_p, device=x2.device, dtype=BF16)
+    out = torch.empty(rows_p, cols_p, device=x2.device, dtype=BF16)
     if rows:
         ops.cast_pad_rows(x2, rows, cols, out, cols_p)
+    if rows_p > rows:
+        ops.zero_(out[rows:])
+    return out
+
+
+_ZROW = {}
+
+
+def _zero_row(n, dev):
+    """a zero f32 row of >= n elements: the bias epilogue's residual operand at row stride 0 (bias only)"""
+    z = _ZROW.get(dev)
+    if z is None or z.numel() < n:
+        z = torch.zeros(max(n, 4096), device=dev, dtype=F32)
+        _ZROW[dev] = z
+    return z
+
+
+def _frozen_bf16(w, key, make):
+    """bf16 operand copies of a weight that takes no gradient (LoRA's frozen bases, res-vit/model.py:573-584):
+    made once per (weight, layout) and kept on the weight object itself, valid while its storage and
+    version counter are unchanged, instead of per call"""
+    if w.requires_grad:
+        return make()
+    cache = getattr(w, "_vitmi_bf16", None)
+    if cache is None:
+        cache = {}
+        try:
+            w._vitmi_bf16 = cache
+        except AttributeError:
+            return make()
+    sig = (w.data_ptr(), w._version, tuple(w.shape))
+    hit = cache.get(key)
+    if hit is not None and hit[0] == sig:
+        return hit[1]
+    out = make()
+    cache[key] = (sig, out)
     return out
 
 
@@ -53,7 +91,7 @@ def _pad_bf16(x2, rows_p, cols_p):
 class HipLinear(torch.autograd.Function):
     """y [rows, n_out] = x [rows, k] @ W + b (bf16 MFMA operands, f32 accumulate and output).
     w_in_out: W stored [k][n_out] (LinearGeneral, JAX layout, src/model.py:58) instead of nn.Linear's
-    [n_out][k]."""
+    [n_out][k]. Weight gradients: split-K over the rows (ops.wgrad)."""
 
     @staticmethod
     def forward(ctx, x2, w, b, w_in_out):
@@ -64,18 +102,20 @@ class HipLinear(torch.autograd.Function):
         w2 = _f32(w).reshape(k, n_out) if w_in_out else _f32(w).reshape(n_out, k)
         xb = _pad_bf16(x2, rp, kp)
         if w_in_out:  # B(k, n) = W[k][n]: MN-contiguous rows of n_out (16-B padded), zero rows past k
-            wb, bl, ldb = _pad_bf16(w2, kp, np8), MN_CONTIG, np8
+            wb, bl, ldb = _frozen_bf16(w, "fwd", lambda: _pad_bf16(w2, kp, np8)), MN_CONTIG, np8
         else:         # B(k, n) = W[n][k]: K-contiguous
-            wb, bl, ldb = _pad_bf16(w2, n_out, kp), K_CONTIG, kp
-        y = torch.zeros(rows, n_out, device=x2.device, dtype=F32)
+            wb, bl, ldb = _frozen_bf16(w, "fwd", lambda: _pad_bf16(w2, n_out, kp)), K_CONTIG, kp
+        y = torch.empty(rows, n_out, device=x2.device, dtype=F32)
         if rows:
             if b is not None:
                 ops.gemm(xb, wb, y, rows, n_out, kp, a_layout=K_CONTIG, b_layout=bl, lda=kp, ldb=ldb, ldc=n_out,
-                         epilogue=EPI_BIAS_RESID_F32, bias=_f32(b).reshape(-1), aux=y, ldaux=n_out)
+                         epilogue=EPI_BIAS_RESID_F32, bias=_f32(b).reshape(-1), aux=_zero_row(n_out, x2.device),
+                         ldaux=0)
             else:
                 ops.gemm(xb, wb, y, rows, n_out, kp, a_layout=K_CONTIG, b_layout=bl, lda=kp, ldb=ldb, ldc=n_out,
                          epilogue=EPI_F32)
         ctx.save_for_backward(xb, w2)
+        ctx.w_obj = w  # the weight object (a Parameter): the frozen-weight cache lives on it
         ctx.dims = (rows, k, n_out, w_in_out, b is not None, tuple(w.shape))
         return y
 
@@ -88,24 +128,25 @@ class HipLinear(torch.autograd.Function):
         dyb = _pad_bf16(dy, rp, npd)
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
-            dx = torch.zeros(rows, k, device=dy.device, dtype=F32)
+            dx = torch.empty(rows, k, device=dy.device, dtype=F32)
             if rows:
+                w2r = w2.reshape(k, n_out) if w_in_out else w2.reshape(n_out, k)
                 if w_in_out:  # B(kk = n, n' = k_in) = W[k_in][n]: K-contiguous [k][npd]
-                    wt, bl, ldb = _pad_bf16(w2, k, npd), K_CONTIG, npd
+                    wt = _frozen_bf16(ctx.w_obj, "dgrad", lambda: _pad_bf16(_f32(w2r), k, npd))
+                    bl, ldb = K_CONTIG, npd
                 else:         # B(kk = n, n' = k_in) = W[n][k_in]: MN-contiguous [npd][k8]
                     k8 = _rup(k, 8)
-                    wt, bl, ldb = _pad_bf16(w2, npd, k8), MN_CONTIG, k8
+                    wt = _frozen_bf16(ctx.w_obj, "dgrad", lambda: _pad_bf16(_f32(w2r), npd, k8))
+                    bl, ldb = MN_CONTIG, k8
                 ops.gemm(dyb, wt, dx, rows, k, npd, a_layout=K_CONTIG, b_layout=bl, lda=npd, ldb=ldb, ldc=k,
                          epilogue=EPI_F32)
         if ctx.needs_input_grad[1]:
             if w_in_out:  # dW [k][n_out] = x^T dy
                 dw = torch.empty(k, n_out, device=dy.device, dtype=F32)
-                ops.gemm(xb, dyb, dw, k, n_out, rp, a_layout=MN_CONTIG, b_layout=MN_CONTIG, lda=kp, ldb=npd,
-                         ldc=n_out, epilogue=EPI_F32)
+                ops.wgrad(xb, kp, dyb, npd, k, n_out, rp, dw, n_out)
             else:         # dW [n_out][k] = dy^T x
                 dw = torch.empty(n_out, k, device=dy.device, dtype=F32)
-                ops.gemm(dyb, xb, dw, n_out, k, rp, a_layout=MN_CONTIG, b_layout=MN_CONTIG, lda=npd, ldb=kp, ldc=k,
-                         epilogue=EPI_F32)
+                ops.wgrad(dyb, npd, xb, kp, n_out, k, rp, dw, k)
             dw = dw.reshape(wshape)
         if has_b and ctx.needs_input_grad[2]:
             db = torch.empty(n_out, device=dy.device, dtype=F32)

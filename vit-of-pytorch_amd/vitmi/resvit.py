@@ -416,7 +416,10 @@ class TransformerBlock(nn.Module):
                             torch.tensor(LRA_mask[self.current_block_pos][1], device=x.device).long())
 
         if self.training:
-            teacher_out = self._full(x if teacher_x is None else teacher_x)  # teacher: every token, every layer
+            # teacher: every token, every layer. Its outputs reach the loss only through DistillLoss's
+            # .detach() (res-vit/model.py:40-59), so no gradient flows through it: run without autograd
+            with torch.no_grad():
+                teacher_out = self._full(x if teacher_x is None else teacher_x)
             student_out = _select_rows(active, self._full(x), x)
             return teacher_out, approximators(student_out, router_indices, lra_lora), w, block_info
 
