@@ -248,6 +248,26 @@ def test_attention(B, N, H, hd, path):
     assert rel(mv, gv) < 2e-2
 
 
+@pytest.mark.parametrize("N,path", [(197, 0), (197, 2), (257, 0)])
+def test_attention_backward_keeps_nan(N, path):
+    """a NaN in one query row (a diverging run) must surface as NaN in that row's dQ, not be clamped into a
+    finite gradient by the padded-key exponent clamp"""
+    B, H, hd = 2, 2, 64
+    D = H * hd
+    qkv = torch.randn(B * N, 3 * D, device=DEV).bfloat16()
+    qkv[5, 3] = float("nan")  # image 0, token 5, head 0: q
+    o = torch.empty(B * N, D, device=DEV, dtype=torch.bfloat16)
+    lse = torch.empty(B, H, N, device=DEV)
+    ops.attention_fwd(qkv, o, lse, B, N, H, hd, 1.0 / math.sqrt(hd), path=path)
+    dout = torch.randn(B * N, D, device=DEV).bfloat16()
+    dqkv = torch.zeros(B * N, 3 * D, device=DEV, dtype=torch.bfloat16)
+    ops.attention_bwd(qkv, o, dout, lse, dqkv, B, N, H, hd, 1.0 / math.sqrt(hd), path=path)
+    dq = dqkv.float()[:, :D]
+    assert torch.isnan(dq[5, :hd]).any()
+    # other images and the other head are untouched by the NaN
+    assert torch.isfinite(dq[N:]).all() and torch.isfinite(dq[:, hd:]).all()
+
+
 @pytest.mark.parametrize("B,img,P,D", [(2, 32, 8, 64), (3, 224, 16, 768), (2, 224, 14, 1280), (2, 64, 32, 1024)])
 def test_im2col_and_embed_grad(B, img, P, D):
     """vector paths (P % 8 == 0, D % 4 == 0) and the scalar fallback (P = 14)"""

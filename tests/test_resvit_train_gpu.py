@@ -237,3 +237,41 @@ open(os.path.join(os.environ["OUTDIR"], f"rank{rank}.ok"), "w").write("ok")
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     assert (tmp_path / "rank0.ok").exists() and (tmp_path / "rank1.ok").exists()
+
+
+@pytest.mark.parametrize("dims", [dict(dim=64, mlp_dim=128, n_heads=2, n_kv_heads=2, lora_rank=4),
+                                  dict(dim=768, mlp_dim=3072, n_heads=12, n_kv_heads=12, lora_rank=8)],
+                         ids=["tiny", "b16"])
+def test_fused_layer_matches_per_op_path(dims):
+    """vitmi.resvit_fused (one autograd node per TransformerBlock._full, LoRA folded into the q|k|v GEMM as
+    extra K columns) against the per-op path on the same kernels (vitmi.functional): output, input
+    gradient and the six LoRA factor gradients of one layer; N = 197 tokens, 3 images."""
+    from vitmi import resvit, resvit_fused
+    torch.manual_seed(3)
+    args = resvit.ModelArgs(**dict(TINY, **dims, device="cuda"))
+    m = resvit.Transformer(args).cuda()
+    blk = m.layers[0]
+    with torch.no_grad():  # LoRA factors at a scale where their contribution is visible
+        for p in blk.attention.parameters():
+            if p.requires_grad:
+                p.normal_(0.0, 0.05)
+    assert resvit_fused.supported(blk)
+    g = torch.Generator(device="cuda").manual_seed(5)
+    x = torch.randn(3, 197, args.dim, device="cuda", generator=g)
+    w = torch.randn(3, 197, args.dim, device="cuda", generator=g)
+    lora = [p for p in blk.attention.parameters() if p.requires_grad]
+    assert len(lora) == 6
+    res = {}
+    for fused in (True, False):
+        blk.fused = fused
+        xi = x.clone().requires_grad_(True)
+        for p in lora:
+            p.grad = None
+        out = blk._full(xi)
+        (out * w).sum().backward()
+        res[fused] = (out.detach(), xi.grad.detach(), [p.grad.detach().clone() for p in lora])
+    (o1, dx1, g1), (o0, dx0, g0) = res[True], res[False]
+    assert rel(o1, o0) < 2e-3
+    assert rel(dx1, dx0) < 1e-2
+    for a, b in zip(g1, g0):
+        assert rel(a, b) < 2e-2

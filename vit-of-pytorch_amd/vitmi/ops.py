@@ -334,7 +334,7 @@ def zero_(t):
     check(lib().vit_zero(_p(t), t.numel() * t.element_size(), _stream()), "vit_zero")
 
 
-def wgrad(A, lda, B, ldb, M, N, K, out, ldo, accumulate=False, batch=1, b_bs=0, out_bs=0, target=256):
+def wgrad(A, lda, B, ldb, M, N, K, out, ldo, accumulate=False, batch=1, a_bs=0, b_bs=0, out_bs=0, target=256):
     """Weight gradient out[z] ([M][N] f32, row stride ldo) (+)= sum_t A[t][m] B[t][n] over K token rows
     (both operands token-major, i.e. M/N-contiguous; K a multiple of 64, rows past the data zero):
     split-K over the tokens into f32 slabs sized to about one wave of `target` workgroups, then the
@@ -346,5 +346,5 @@ def wgrad(A, lda, B, ldb, M, N, K, out, ldo, accumulate=False, batch=1, b_bs=0, 
     s = max(1, min(round(target / tiles), max(1, nkt // 8), 32))
     ws = torch.empty(batch * s * M * N, device=out.device, dtype=F32)
     gemm(A, B, ws, M, N, K, a_layout=MN_CONTIG, b_layout=MN_CONTIG, lda=lda, ldb=ldb, ldc=N, epilogue=EPI_SPLITK,
-         batch=batch, b_bs=b_bs, split_k=s)
+         batch=batch, a_bs=a_bs, b_bs=b_bs, split_k=s)
     splitk_reduce(ws, batch, s, M, N, out, ldo, out_bs, accumulate)

@@ -31,6 +31,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import functional as HF
+from . import resvit_fused as _fused
 from .model import GELU, CrossEntropyLoss, LayerNorm as _HipLayerNorm, Linear
 
 __all__ = ["ModelArgs", "DistillLoss", "ActiveLoss", "PositionEmbs", "LoRAModule", "LayerNorm", "RouterModule",
@@ -368,6 +369,7 @@ class TransformerBlock(nn.Module):
         self.current_epoch = 0
         self.use_lora = args.use_lora
         self.use_reslr = args.use_reslr
+        self.fused = True  # False: the per-op path (vitmi.functional) for every configuration
         self.attention = Attention(args)
         self.attention_norm = LayerNorm(args.dim, eps=args.norm_eps, use_lora=args.use_lora)
         self.feed_forward = FeedForward(dim=args.dim, mlp_dim=args.mlp_dim)
@@ -386,6 +388,8 @@ class TransformerBlock(nn.Module):
                 self.block_path_approximators = BlockPathApproximators(args.dim, args.low_rank_dim, self.block_size)
 
     def _full(self, x):
+        if self.fused and x.dim() == 3 and x.is_cuda and _fused.supported(self):
+            return _fused.full_layer(self, x)  # one fused node (LoRA configuration, vitmi.resvit_fused)
         h = HF.add(self.attention(self.attention_norm(x)), x)
         return HF.add(self.feed_forward(self.ffn_norm(h)), h)
 

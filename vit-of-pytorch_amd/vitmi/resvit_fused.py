@@ -1,0 +1,240 @@
+"""One Res-ViT transformer layer (`TransformerBlock._full`, res-vit/model.py:213-317,471-492) as a single
+autograd node on the engine's fused kernels, for the LoRA configuration of BASELINE config C5
+(res-vit/config.py defaults: every base weight and LayerNorm frozen, res-vit/model.py:573-584; only
+the rank-r LoRA factors on q / k / v take gradients here).
+
+    h   = x + wo(attn(q, k, v)),  [q|k|v] = LN1(x) [Wq|Wk|Wv]^T + b + (LN1(x) A_z^T) B_z^T
+    out = h + fc2(GELU(fc1(LN2(h))))
+
+Forward (T = B*N token rows; bf16 GEMM operands, f32 accumulation / residual stream / LN statistics):
+  LN1 writes its bf16 output into columns [0, D) of a [T][D + 64] operand; the LoRA down-projections
+  u_z = LN1(x) A_z^T land in the next 3*r8 columns (one GEMM, N = 3 r8); the q|k|v GEMM then runs over
+  K = D + 64 against [W_qkv | blockdiag(B_q, B_k, B_v)] — the LoRA up-projection folded into the same
+  MFMA pass without rounding B A into the frozen weight (|BA| << |W| would vanish in bf16) — with the
+  bias epilogue writing bf16 q|k|v for the attention kernel; attention (LDS-resident / tiled); out-proj
+  + bias + f32 residual; LN2 (bf16); fc1 with the bias + GELU + GELU' epilogue; fc2 + bias + residual.
+Backward: fc2 data gradient times GELU' (one epilogue), fc1 data gradient, LN2 backward with the
+residual gradient added, out-proj data gradient, attention backward, LoRA: v_z = dq_z B_z (batched
+GEMM), dB_z = dq_z^T u_z and dA_z = v_z^T LN1(x) (split-K over tokens), the q|k|v data gradient
+dqkv W_qkv + v A (two GEMMs into f32), LN1 backward with the residual gradient. Frozen weights take no
+gradient; their bf16 operand copies (forward and transposed for the data gradients) are cached per
+weight version on the block.
+
+The generic per-op path (vitmi.functional) remains for every other configuration (no LoRA: all
+weights trainable; grouped-query attention; shapes the kernels do not cover).
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from . import ops
+from ._lib import (EPI_BF16, EPI_BIAS_BF16, EPI_BIAS_GELU_DGELU, EPI_BIAS_RESID_F32, EPI_F32, EPI_MUL_BF16,
+                   K_CONTIG, MN_CONTIG)
+
+BF16, F32 = torch.bfloat16, torch.float32
+KX = 64  # extra K columns of the q|k|v operand (LoRA down-projections, zero padded)
+
+
+def _rup(x, m):
+    return (x + m - 1) // m * m
+
+
+_ZROW = {}
+
+
+def _zero_row(n, dev):
+    z = _ZROW.get(dev)
+    if z is None or z.numel() < n:
+        z = torch.zeros(max(n, 4096), device=dev, dtype=F32)
+        _ZROW[dev] = z
+    return z
+
+
+def supported(block):
+    """the fused layer covers: LoRA on, every base weight / norm frozen, n_kv_heads == n_heads, head dim a
+    multiple of 16 up to 96, D and mlp_dim multiples of 64, rank <= 21"""
+    a = block.attention
+    if not block.use_lora or a.n_rep != 1:
+        return False
+    D = block.dim
+    hd = a.head_dim
+    M = block.feed_forward.fc1.weight.shape[0]
+    r = a.lora_q.rank
+    frozen = [a.wq, a.wk, a.wv, a.wo, block.feed_forward.fc1, block.feed_forward.fc2]
+    if any(p.requires_grad for m in frozen for p in m.parameters()):
+        return False
+    if any(p.requires_grad for n in (block.attention_norm, block.ffn_norm) for p in n.parameters()):
+        return False
+    return D % 64 == 0 and M % 64 == 0 and hd % 16 == 0 and hd <= 96 and 3 * _rup(r, 8) <= KX
+
+
+class _Frozen:
+    """bf16 operand copies of a block's frozen weights, rebuilt when a weight's storage or version changes"""
+
+    def __init__(self):
+        self.sig = None
+
+    def get(self, block):
+        a, ff = block.attention, block.feed_forward
+        ws = (a.wq.weight, a.wk.weight, a.wv.weight, a.wq.bias, a.wk.bias, a.wv.bias, a.wo.weight, ff.fc1.weight,
+              ff.fc2.weight)
+        sig = tuple((w.data_ptr(), w._version) for w in ws)
+        if sig == self.sig:
+            return self
+        D, M = block.dim, ff.fc1.weight.shape[0]
+        dev = a.wq.weight.device
+        Kq = D + KX
+        # q|k|v forward operand [3D][D + 64] (K-contiguous); the LoRA columns are rewritten per call
+        self.wcat = torch.zeros(3 * D, Kq, device=dev, dtype=BF16)
+        for z, w in enumerate((a.wq.weight, a.wk.weight, a.wv.weight)):
+            ops.pack_cols(w.detach(), 0, D, D, D, 1, self.wcat[z * D:], Kq)
+        self.bqkv = torch.cat([a.wq.bias.detach(), a.wk.bias.detach(), a.wv.bias.detach()]).float().contiguous()
+        # data-gradient operands: W^T, K-contiguous over the output features
+        self.wqkv_t = torch.empty(D, 3 * D, device=dev, dtype=BF16)
+        for z, w in enumerate((a.wq.weight, a.wk.weight, a.wv.weight)):
+            ops.transpose_bf16(w.detach(), D, D, D, self.wqkv_t[:, z * D:], 3 * D)
+        self.wo = torch.empty(D, D, device=dev, dtype=BF16)
+        ops.cast_bf16(a.wo.weight.detach(), self.wo, D * D)
+        self.wo_t = torch.empty(D, D, device=dev, dtype=BF16)
+        ops.transpose_bf16(a.wo.weight.detach(), D, D, D, self.wo_t, D)
+        self.w1 = torch.empty(M, D, device=dev, dtype=BF16)
+        ops.cast_bf16(ff.fc1.weight.detach(), self.w1, M * D)
+        self.w1_t = torch.empty(D, M, device=dev, dtype=BF16)
+        ops.transpose_bf16(ff.fc1.weight.detach(), M, D, D, self.w1_t, M)
+        self.w2 = torch.empty(D, M, device=dev, dtype=BF16)
+        ops.cast_bf16(ff.fc2.weight.detach(), self.w2, D * M)
+        self.w2_t = torch.empty(M, D, device=dev, dtype=BF16)
+        ops.transpose_bf16(ff.fc2.weight.detach(), D, M, M, self.w2_t, D)
+        self.sig = sig
+        return self
+
+
+class _FusedLayer(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, aq, bq, ak, bk, av, bv, block):
+        a, ff = block.attention, block.feed_forward
+        fz = block._vitmi_frozen.get(block)
+        B, N, D = x.shape
+        H, hd = a.n_local_heads, a.head_dim
+        M = ff.fc1.weight.shape[0]
+        r = aq.shape[0]
+        r8 = _rup(r, 8)
+        T = B * N
+        Tp = _rup(T, 64)
+        Kq = D + KX
+        dev = x.device
+        x = x.contiguous().float()
+        xf = x.view(T, D)
+        eps1, eps2 = block.attention_norm.layer_norm.eps, block.ffn_norm.layer_norm.eps
+        n1, n2 = block.attention_norm.layer_norm, block.ffn_norm.layer_norm
+        # LoRA factors as bf16 operands: A_all [64][D] (row z*r8 + i = A_z[i]); B columns of the q|k|v operand
+        a_all = torch.zeros(KX, D, device=dev, dtype=BF16)
+        for z, A in enumerate((aq, ak, av)):
+            ops.cast_pad_rows(A.detach().float().contiguous(), r, D, a_all[z * r8:], D)
+        for z, Bz in enumerate((bq, bk, bv)):
+            ops.pack_cols(Bz.detach().float().contiguous(), 0, r, D, r, 1, fz.wcat[z * D:, D + z * r8:], Kq)
+        a1 = torch.empty(Tp, Kq, device=dev, dtype=BF16)
+        ops.zero_(a1)
+        mu1, rs1 = torch.empty(T, device=dev), torch.empty(T, device=dev)
+        ops.layernorm_fwd(xf, D, n1.weight, n1.bias, a1, Kq, mu1, rs1, T, D, eps1)
+        # u_z = LN1(x) A_z^T -> columns D + z*r8 .. of the same operand
+        ops.gemm(a1, a_all, a1[:, D:], T, 3 * r8, D, a_layout=K_CONTIG, b_layout=K_CONTIG, lda=Kq, ldb=D, ldc=Kq,
+                 epilogue=EPI_BF16)
+        qkv = torch.empty(Tp, 3 * D, device=dev, dtype=BF16)
+        ops.gemm(a1, fz.wcat, qkv, T, 3 * D, Kq, a_layout=K_CONTIG, b_layout=K_CONTIG, lda=Kq, ldb=Kq, ldc=3 * D,
+                 epilogue=EPI_BIAS_BF16, bias=fz.bqkv)
+        o = torch.empty(Tp, D, device=dev, dtype=BF16)
+        lse = torch.empty(B, H, N, device=dev)
+        scale = 1.0 / math.sqrt(hd)
+        ops.attention_fwd(qkv, o, lse, B, N, H, hd, scale)
+        h = torch.empty(T, D, device=dev)
+        ops.gemm(o, fz.wo, h, T, D, D, a_layout=K_CONTIG, b_layout=K_CONTIG, lda=D, ldb=D, ldc=D,
+                 epilogue=EPI_BIAS_RESID_F32, bias=a.wo.bias.detach(), aux=xf, ldaux=D)
+        a2 = torch.empty(Tp, D, device=dev, dtype=BF16)
+        mu2, rs2 = torch.empty(T, device=dev), torch.empty(T, device=dev)
+        ops.layernorm_fwd(h, D, n2.weight, n2.bias, a2, D, mu2, rs2, T, D, eps2)
+        gp = torch.empty(Tp, M, device=dev, dtype=BF16)
+        g = torch.empty(Tp, M, device=dev, dtype=BF16)
+        ops.gemm(a2, fz.w1, gp, T, M, D, a_layout=K_CONTIG, b_layout=K_CONTIG, lda=D, ldb=D, ldc=M,
+                 epilogue=EPI_BIAS_GELU_DGELU, bias=ff.fc1.bias.detach(), C2=g, ldc2=M)
+        out = torch.empty(T, D, device=dev)
+        ops.gemm(g, fz.w2, out, T, D, M, a_layout=K_CONTIG, b_layout=K_CONTIG, lda=M, ldb=M, ldc=D,
+                 epilogue=EPI_BIAS_RESID_F32, bias=ff.fc2.bias.detach(), aux=h, ldaux=D)
+        if torch.is_grad_enabled() or any(ctx.needs_input_grad):
+            ctx.save_for_backward(xf, a1, mu1, rs1, qkv, o, lse, h, mu2, rs2, gp, a_all, bq, bk, bv)
+            ctx.block = block
+            ctx.dims = (B, N, D, H, hd, M, r, r8, T, Tp, scale)
+        return out.view(B, N, D)
+
+    @staticmethod
+    def backward(ctx, dout):
+        xf, a1, mu1, rs1, qkv, o, lse, h, mu2, rs2, gp, a_all, bq, bk, bv = ctx.saved_tensors
+        block = ctx.block
+        fz = block._vitmi_frozen.get(block)
+        B, N, D, H, hd, M, r, r8, T, Tp, scale = ctx.dims
+        Kq = D + KX
+        dev = xf.device
+        n1, n2 = block.attention_norm.layer_norm, block.ffn_norm.layer_norm
+        dout = dout.contiguous().float().view(T, D)
+        dob = torch.empty(T, D, device=dev, dtype=BF16)
+        ops.cast_bf16(dout, dob, T * D)
+        # fc2 data gradient x GELU'(fc1 pre-activation)
+        dg = torch.empty(T, M, device=dev, dtype=BF16)
+        ops.gemm(dob, fz.w2_t, dg, T, M, D, a_layout=K_CONTIG, b_layout=K_CONTIG, lda=D, ldb=D, ldc=M,
+                 epilogue=EPI_MUL_BF16, aux=gp, ldaux=M)
+        dy2 = torch.empty(T, D, device=dev, dtype=BF16)
+        ops.gemm(dg, fz.w1_t, dy2, T, D, M, a_layout=K_CONTIG, b_layout=K_CONTIG, lda=M, ldb=M, ldc=D,
+                 epilogue=EPI_BF16)
+        del dg
+        part = torch.empty(ops.layernorm_bwd_partial_rows(T), 3 * D, device=dev)
+        dh = torch.empty(T, D, device=dev)
+        dhb = torch.empty(T, D, device=dev, dtype=BF16)
+        ops.layernorm_bwd(dy2, D, h, D, mu2, rs2, n2.weight, dh, D, part, T, D, dres=dout, lddres=D, dx_bf16=dhb,
+                          lddxb=D)
+        dO = torch.empty(T, D, device=dev, dtype=BF16)
+        ops.gemm(dhb, fz.wo_t, dO, T, D, D, a_layout=K_CONTIG, b_layout=K_CONTIG, lda=D, ldb=D, ldc=D,
+                 epilogue=EPI_BF16)
+        dqkv = torch.empty(Tp, 3 * D, device=dev, dtype=BF16)
+        if Tp > T:
+            ops.zero_(dqkv[T:])
+        ops.attention_bwd(qkv, o, dO, lse, dqkv, B, N, H, hd, scale)
+        # LoRA: v_z = dq_z B_z (batched), dB_z = dq_z^T u_z, dA_z = v_z^T LN1(x)
+        b_all = torch.zeros(3, D, r8, device=dev, dtype=BF16)
+        for z, Bz in enumerate((bq, bk, bv)):
+            ops.cast_pad_rows(Bz.detach().float().contiguous(), D, r, b_all[z], r8)
+        v_all = torch.empty(Tp, KX, device=dev, dtype=BF16)
+        ops.zero_(v_all)
+        ops.gemm(dqkv, b_all, v_all, T, r, D, a_layout=K_CONTIG, b_layout=MN_CONTIG, lda=3 * D, ldb=r8, ldc=KX,
+                 epilogue=EPI_BF16, batch=3, a_bs=D, b_bs=D * r8, c_bs=r8)
+        need = ctx.needs_input_grad
+        dB = torch.empty(3, D, r, device=dev)
+        ops.wgrad(dqkv, 3 * D, a1[:, D:], Kq, D, r, Tp, dB, r, batch=3, a_bs=D, b_bs=r8, out_bs=D * r)
+        dA = torch.empty(3, r, D, device=dev)
+        ops.wgrad(v_all, KX, a1, Kq, r, D, Tp, dA, D, batch=3, a_bs=r8, out_bs=r * D)
+        # q|k|v data gradient: dqkv W_qkv + v A (f32), then LN1 backward with the residual gradient
+        dy1 = torch.empty(T, D, device=dev)
+        ops.gemm(v_all, a_all, dy1, T, D, KX, a_layout=K_CONTIG, b_layout=MN_CONTIG, lda=KX, ldb=D, ldc=D,
+                 epilogue=EPI_F32)
+        ops.gemm(dqkv, fz.wqkv_t, dy1, T, D, 3 * D, a_layout=K_CONTIG, b_layout=K_CONTIG, lda=3 * D, ldb=3 * D,
+                 ldc=D, epilogue=EPI_BIAS_RESID_F32, bias=_zero_row(D, dev), aux=dy1, ldaux=D)
+        dx = None
+        if need[0]:
+            dx = torch.empty(T, D, device=dev)
+            ops.layernorm_bwd(dy1, D, xf, D, mu1, rs1, n1.weight, dx, D, part, T, D, dres=dh, lddres=D)
+            dx = dx.view(B, N, D)
+        grads = []
+        for z in range(3):
+            grads += [dA[z] if need[1 + 2 * z] else None, dB[z] if need[2 + 2 * z] else None]
+        return (dx, *grads, None)
+
+
+def full_layer(block, x):
+    """TransformerBlock._full(x) (res-vit/model.py:471-492: attention + residual, FFN + residual) as one
+    fused node; x [B, N, D] f32 -> [B, N, D] f32"""
+    if not hasattr(block, "_vitmi_frozen"):
+        block._vitmi_frozen = _Frozen()
+    a = block.attention
+    return _FusedLayer.apply(x, a.lora_q.lora_A.weight, a.lora_q.lora_B.weight, a.lora_k.lora_A.weight,
+                             a.lora_k.lora_B.weight, a.lora_v.lora_A.weight, a.lora_v.lora_B.weight, block)
