@@ -242,15 +242,33 @@ def main():
         _opt.step()
         sched.step()
 
-    def step(k):
+    # the schedule's {lr, momentum, first-step} of every step on the device: the SGD kernel reads them from
+    # `hyper`, refreshed by a 12-byte device copy before each step, so the step can be one HIP graph
+    hyper_all = torch.tensor([[lr_, mom_, 1.0 if k == 0 else 0.0] for k, (lr_, mom_) in enumerate(hp)],
+                             device=dev, dtype=torch.float32)
+    hyper = hyper_all[0].clone()
+
+    def step_body():
         eng.forward(x)
         dl, _ = eng.cross_entropy(y, grad_scale=1.0 / (b * world))
         eng.backward(dl)
         if reducer is not None:
             reducer.finish()
-        lr, mom = hp[k]
-        ops.sgd_step(eng.flat, eng.grad, mom_buf, eng.mirror, eng.layout.numel, lr, mom, 0.0, k == 0)
+        ops.sgd_step_dev(eng.flat, eng.grad, mom_buf, eng.mirror, eng.layout.numel, hyper, 0.0)
         eng.refresh_mirror(full=False)
+
+    # VITMI_BENCH_GRAPH=1 (one process on one GPU): the whole step (~450 launches on two streams) captured
+    # once as a HIP graph and replayed. Off by default: the launch queue already runs ahead of the GPU, and
+    # in a same-box A/B the replay was 0.5% slower than eager launches (7402 / 7417 vs 7452 / 7455 img/s)
+    use_graph = world == 1 and os.environ.get("VITMI_BENCH_GRAPH", "0") != "0"
+    graph = None
+
+    def step(k):
+        ops.copy2d(hyper, 12, hyper_all[k], 12, 12, 1)
+        if graph is not None:
+            graph.replay()
+        else:
+            step_body()
 
     def barrier():
         if world > 1:
@@ -261,14 +279,23 @@ def main():
     for k in range(args.warmup):
         step(k)
     barrier()
-    probes = ([], [])
+    if use_graph:
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            step_body()
+        barrier()
     t0 = time.perf_counter()
     for k in range(args.warmup, total_steps):
-        if k == total_steps - 1:  # HIP events around the roofline kernels' launches of the last timed step
-            eng.probe, eng.probe_wgrad = probes  # (each event record costs the stream ~10 us of idle)
         step(k)
     barrier()
     dt = time.perf_counter() - t0
+    # HIP events around the roofline kernels' launches of one more (eager) step after the timed region,
+    # on the stream the kernels run on (each event record costs the stream ~10 us of idle)
+    probes = ([], [])
+    eng.probe, eng.probe_wgrad = probes
+    ops.copy2d(hyper, 12, hyper_all[total_steps - 1], 12, 12, 1)
+    step_body()
+    barrier()
     probe, probe_w = probes
     eng.probe = eng.probe_wgrad = None
     if world > 1:
@@ -324,10 +351,12 @@ def main():
                    "model": f"ViT-{args.arch.upper()}", "image_size": args.image_size, "per_gpu_batch": b,
                    "global_batch": b * world, "seq_len": cfg.tokens, "num_classes": args.num_classes,
                    "parallelism": f"dp{world}", "dist_backend": backend,
+                   "step_launch": "one HIP graph per step" if use_graph else "eager",
                    **({"grad_allreduce_dtype": "bf16"} if compress and world > 1 else {})},
         "roofline": {"bound": "mfma", "kernel": "split-K weight-gradient GEMM gemm_pp_kernel (the step's dominant "
-                                                f"kernel): the {len(wg_ms)} launches over all tokens of the last "
-                                                f"timed step (HIP events), K = {T} tokens padded to 64; fc1 / fc2 / "
+                                                f"kernel): the {len(wg_ms)} launches over all tokens of one step "
+                                                f"(HIP events, an eager step after the timed region), K = {T} tokens "
+                                                "padded to 64; fc1 / fc2 / "
                                                 "out-proj weights one GEMM each, q|k|v three GEMMs in one batched launch",
                      "achieved": round(wg_tflops, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                      "frac": round(wg_tflops / PEAK_BF16_TFLOPS, 4), "traffic": (traffic_w or {}).get("bytes"),

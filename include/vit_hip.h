@@ -266,6 +266,10 @@ int vit_cross_entropy(const float* logits, const int64_t* labels, int64_t B, int
  * ---------------------------------------------------------------------------------------- */
 int vit_sgd_step(float* p, const float* g, float* buf, void* p_bf16, int64_t n, float lr,
                  float momentum, float weight_decay, int32_t first, vit_stream_t stream);
+/* vit_sgd_step with hyper = {lr, momentum, first} read from device memory (a step inside a captured HIP
+ * graph; the schedule writes the three floats before each replay) */
+int vit_sgd_step_dev(float* p, const float* g, float* buf, void* p_bf16, int64_t n, const float* hyper,
+                     float weight_decay, vit_stream_t stream);
 int vit_cast_f32_bf16(const float* in, void* out, int64_t n, vit_stream_t stream);
 /* out bf16 [rows][ldo] <- in f32 [rows][cols]; columns cols..ldo-1 are zeroed. */
 int vit_cast_pad_rows(const float* in, int64_t rows, int64_t cols, void* out, int64_t ldo,
@@ -350,6 +354,9 @@ int vit_adamw_chunk_elems(void);
 int vit_scale_by_coef(float* g, int64_t n, const float* coef, vit_stream_t stream);
 /* bytes of device memory at ptr set to 0 on the stream (hipMemsetAsync) */
 int vit_zero(void* ptr, int64_t bytes, vit_stream_t stream);
+/* height rows of width bytes: dst + r*dpitch <- src + r*spitch (hipMemcpy2DAsync, device to device) */
+int vit_copy2d(void* dst, int64_t dpitch, const void* src, int64_t spitch, int64_t width, int64_t height,
+               vit_stream_t stream);
 
 #ifdef __cplusplus
 }

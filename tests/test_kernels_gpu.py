@@ -208,7 +208,8 @@ def _attn_ref(qkv, B, N, H, hd):
     return o, lse
 
 
-ATTN_CASES = [(2, 197, 12, 64, 0), (3, 17, 2, 32, 0), (2, 50, 4, 64, 0), (1, 5, 3, 64, 0), (2, 257, 2, 64, 0),
+ATTN_CASES = [(2, 2, 2, 64, 0),  # (config C1: 2 tokens)
+              (2, 197, 12, 64, 0), (3, 17, 2, 32, 0), (2, 50, 4, 64, 0), (1, 5, 3, 64, 0), (2, 257, 2, 64, 0),
               (2, 257, 3, 80, 0), (1, 197, 2, 48, 0), (2, 33, 2, 96, 0),
               # K/V-tiled path (ops.ATTN_TILED): forced at ViT-224 sizes, and the 384-px sequences it exists for
               # (B/16, L/16 @384: 577 tokens; H/14 @384: 730 tokens, hd 80)
@@ -222,6 +223,7 @@ ATTN_CASES = [(2, 197, 12, 64, 0), (3, 17, 2, 32, 0), (2, 50, 4, 64, 0), (1, 5, 
 def test_attention(B, N, H, hd, path):
     D = H * hd
     qkv = (torch.randn(B * N, 3 * D, device=DEV) * 1.5).bfloat16().requires_grad_(True)
+
     o = torch.empty(B * N, D, device=DEV, dtype=torch.bfloat16)
     lse = torch.empty(B, H, N, device=DEV)
     ops.attention_fwd(qkv.detach(), o, lse, B, N, H, hd, 1.0 / math.sqrt(hd), path=path)
@@ -248,14 +250,35 @@ def test_attention(B, N, H, hd, path):
     assert rel(mv, gv) < 2e-2
 
 
-@pytest.mark.parametrize("N,path", [(197, 0), (197, 2), (257, 0)])
+@pytest.mark.parametrize("N", [2, 17, 197])
+def test_attention_backward_saturated_scores_finite(N):
+    """scores of |s| ~ 1e3 (the reference's std-1 init, config C1's 2 tokens): the LSE of a query can be far
+    below 0, and the zero-padded keys of its last computed key tile must still get P = 0, not 2^-LSE = inf
+    (inf * dP 0 = NaN)"""
+    B, H, hd = 2, 2, 64
+    D = H * hd
+    g = torch.Generator(device=DEV).manual_seed(1)
+    qkv = (torch.randn(B * N, 3 * D, device=DEV, generator=g) * 8.0).bfloat16()
+    qkv[:, :D] = -qkv[:, :D].abs()  # q < 0 < k elementwise: every score q.k is very negative
+    qkv[:, D:2 * D] = qkv[:, D:2 * D].abs()
+    o = torch.empty(B * N, D, device=DEV, dtype=torch.bfloat16)
+    lse = torch.empty(B, H, N, device=DEV)
+    ops.attention_fwd(qkv, o, lse, B, N, H, hd, 1.0 / math.sqrt(hd))
+    assert float(lse.min()) < -100.0
+    dout = torch.randn(B * N, D, device=DEV).bfloat16()
+    dqkv = torch.zeros(B * N, 3 * D, device=DEV, dtype=torch.bfloat16)
+    ops.attention_bwd(qkv, o, dout, lse, dqkv, B, N, H, hd, 1.0 / math.sqrt(hd))
+    assert torch.isfinite(o.float()).all() and torch.isfinite(dqkv.float()).all()
+
+
+@pytest.mark.parametrize("N,path", [(197, 0), (197, 2), (257, 0), (2, 0), (17, 0)])
 def test_attention_backward_keeps_nan(N, path):
     """a NaN in one query row (a diverging run) must surface as NaN in that row's dQ, not be clamped into a
     finite gradient by the padded-key exponent clamp"""
     B, H, hd = 2, 2, 64
     D = H * hd
     qkv = torch.randn(B * N, 3 * D, device=DEV).bfloat16()
-    qkv[5, 3] = float("nan")  # image 0, token 5, head 0: q
+    qkv[min(5, N - 1), 3] = float("nan")  # image 0, token 5 (or the last), head 0: q
     o = torch.empty(B * N, D, device=DEV, dtype=torch.bfloat16)
     lse = torch.empty(B, H, N, device=DEV)
     ops.attention_fwd(qkv, o, lse, B, N, H, hd, 1.0 / math.sqrt(hd), path=path)
@@ -263,7 +286,7 @@ def test_attention_backward_keeps_nan(N, path):
     dqkv = torch.zeros(B * N, 3 * D, device=DEV, dtype=torch.bfloat16)
     ops.attention_bwd(qkv, o, dout, lse, dqkv, B, N, H, hd, 1.0 / math.sqrt(hd), path=path)
     dq = dqkv.float()[:, :D]
-    assert torch.isnan(dq[5, :hd]).any()
+    assert torch.isnan(dq[min(5, N - 1), :hd]).any()
     # other images and the other head are untouched by the NaN
     assert torch.isfinite(dq[N:]).all() and torch.isfinite(dq[:, hd:]).all()
 

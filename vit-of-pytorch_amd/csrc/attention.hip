@@ -826,16 +826,18 @@ __global__ void __launch_bounds__(NW * 64, 2) attn_bwd_kernel(const bf16_t* __re
         }
         // Padded keys (rows N.. of the zero-filled K / V images) need no mask here: their dP = dO V^T
         // is 0, so they add nothing to delta, and their dS only meets the zero K rows in dQ = dS K.
-        // On the last tile (the only one holding padded keys, a wave-uniform condition) the exponent
-        // is clamped at 0 so that P stays finite for them whatever the query's LSE (a real key's
-        // exponent is <= 0 up to rounding: LSE >= every score); elsewhere a NaN score stays NaN. The
-        // per-(tile, row) masks this replaces were spilled SGPR lane masks: 2 v_readlane + 2 v_cndmask
-        // per element.
-        const bool pad_tile = kt == NKT - 1 && N < NKT * 16;
+        // On the tile holding keys >= N (the only one with padded keys that is computed: a wholly padded
+        // last tile is skipped above; a wave-uniform condition) their exponent is clamped at 0 so that P
+        // stays finite for them whatever the query's LSE (a real key's exponent is <= 0 up to rounding:
+        // LSE >= every score; unclamped, a padded key's 2^(-LSE) overflows for LSE << 0 and P dP = inf *
+        // 0 = NaN); elsewhere a NaN score stays NaN. The per-(tile, row) masks this replaces were
+        // spilled SGPR lane masks: 2 v_readlane + 2 v_cndmask per element.
+        // (inside that tile only the padded keys themselves are clamped: a NaN score of a real key stays NaN)
+        const bool pad_tile = (kt + 1) * 16 > N;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const float e = st[r] * c - ls;
-          const float pv = ex2(pad_tile ? fminf(e, 0.f) : e);
+          const float pv = ex2(pad_tile && kt * 16 + 4 * g + r >= N ? fminf(e, 0.f) : e);
           P[kt][r] = pv;
           dlr[r] += pv * dpt[r];
         }

@@ -543,6 +543,52 @@ extern "C" int vit_cross_entropy(const float* logits, const int64_t* labels, int
   VIT_LAUNCH_CHECK("vit_cross_entropy");
 }
 
+// hyper = {lr, momentum, first (0 / 1)} in device memory: the step can sit in a captured HIP graph while the
+// schedule moves (the caller refreshes the three floats before each launch)
+__global__ void sgd_dev_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ buf,
+                               bf16_t* __restrict__ pb, long n, const float* __restrict__ hyper, float wd) {
+  const float lr = hyper[0], mom = hyper[1];
+  const bool first = hyper[2] != 0.0f;
+  const long n4 = n / 4;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
+    float4 pv = reinterpret_cast<float4*>(p)[i];
+    const float4 gv = reinterpret_cast<const float4*>(g)[i];
+    float4 d = make_float4(gv.x + wd * pv.x, gv.y + wd * pv.y, gv.z + wd * pv.z, gv.w + wd * pv.w);
+    if (!first) {
+      const float4 bv = reinterpret_cast<float4*>(buf)[i];
+      d = make_float4(mom * bv.x + d.x, mom * bv.y + d.y, mom * bv.z + d.z, mom * bv.w + d.w);
+    }
+    reinterpret_cast<float4*>(buf)[i] = d;
+    pv = make_float4(pv.x - lr * d.x, pv.y - lr * d.y, pv.z - lr * d.z, pv.w - lr * d.w);
+    reinterpret_cast<float4*>(p)[i] = pv;
+    if (pb) {
+      uint2 u;
+      u.x = pack2bf(pv.x, pv.y);
+      u.y = pack2bf(pv.z, pv.w);
+      reinterpret_cast<uint2*>(pb)[i] = u;
+    }
+  }
+  const long t = n4 * 4 + (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (blockIdx.x == 0 && t < n) {
+    float d = g[t] + wd * p[t];
+    if (!first) d = mom * buf[t] + d;
+    buf[t] = d;
+    p[t] -= lr * d;
+    if (pb) pb[t] = f2bf(p[t]);
+  }
+}
+
+extern "C" int vit_sgd_step_dev(float* p, const float* g, float* buf, void* p_bf16, int64_t n, const float* hyper,
+                                float weight_decay, vit_stream_t stream) {
+  VIT_CHECK_ARG(p && g && buf && hyper && n >= 0, "vit_sgd_step_dev: bad args");
+  VIT_CHECK_ARG(((uintptr_t)p | (uintptr_t)g | (uintptr_t)buf) % 16 == 0 && ((uintptr_t)p_bf16 % 8 == 0),
+                "vit_sgd_step_dev: buffers must be 16-B aligned (bf16 mirror 8-B)");
+  if (n == 0) return VIT_OK;
+  hipLaunchKernelGGL(sgd_dev_kernel, dim3(grid_for(n, 4)), dim3(256), 0, (hipStream_t)stream, p, g, buf,
+                     (bf16_t*)p_bf16, (long)n, hyper, weight_decay);
+  VIT_LAUNCH_CHECK("vit_sgd_step_dev");
+}
+
 extern "C" int vit_sgd_step(float* p, const float* g, float* buf, void* p_bf16, int64_t n, float lr, float momentum,
                             float weight_decay, int32_t first, vit_stream_t stream) {
   VIT_CHECK_ARG(p && g && buf && n >= 0, "vit_sgd_step: bad args");

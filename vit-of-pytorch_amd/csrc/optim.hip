@@ -211,3 +211,12 @@ extern "C" int vit_zero(void* ptr, int64_t bytes, vit_stream_t stream) {
   if (bytes == 0) return VIT_OK;
   return vit::check_hip(hipMemsetAsync(ptr, 0, (size_t)bytes, (hipStream_t)stream), "vit_zero");
 }
+
+extern "C" int vit_copy2d(void* dst, int64_t dpitch, const void* src, int64_t spitch, int64_t width, int64_t height,
+                          vit_stream_t stream) {
+  VIT_CHECK_ARG(dst && src && width >= 0 && height >= 0 && dpitch >= width && spitch >= width, "vit_copy2d: bad args");
+  if (width == 0 || height == 0) return VIT_OK;
+  return vit::check_hip(hipMemcpy2DAsync(dst, (size_t)dpitch, src, (size_t)spitch, (size_t)width, (size_t)height,
+                                         hipMemcpyDeviceToDevice, (hipStream_t)stream),
+                        "vit_copy2d");
+}

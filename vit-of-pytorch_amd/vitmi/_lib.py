@@ -104,6 +104,8 @@ _SIGS = {
     "vit_adamw_chunk_elems": (c_i32, []),
     "vit_scale_by_coef": (c_i32, [c_vp, c_i64, c_vp, c_vp]),
     "vit_zero": (c_i32, [c_vp, c_i64, c_vp]),
+    "vit_copy2d": (c_i32, [c_vp, c_i64, c_vp, c_i64, c_i64, c_i64, c_vp]),
+    "vit_sgd_step_dev": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_f32, c_vp]),
 }
 
 EXPORTED = tuple(_SIGS)

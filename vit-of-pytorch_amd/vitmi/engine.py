@@ -33,6 +33,10 @@ def _rup(x, m):
     return (x + m - 1) // m * m
 
 
+# partial-sum buffers per kind of bias-gradient reduction (the compute stream waits for the reduction that
+# last read a buffer before writing it again; deeper rings let the bias stream lag further behind)
+_NBUF = max(2, int(os.environ.get("VITMI_BIAS_BUFS", "8")))
+
 # workgroups a split-K weight gradient aims for (one per CU); VIT_WGRAD_TARGET for tuning sweeps
 _WGRAD_TARGET = int(os.environ.get("VIT_WGRAD_TARGET", "256"))
 
@@ -168,14 +172,16 @@ class _Acts:
         # bias-gradient partial sums: written on the compute stream, reduced on the engine's bias stream
         # (ViTEngine.backward), so each kind is double-buffered
         self.lnpart = z(ops.layernorm_bwd_partial_rows(T), 3 * D, dt=f)
-        self.lnparts = [self.lnpart, z(ops.layernorm_bwd_partial_rows(T), 3 * D, dt=f)]
+        self.lnparts = [self.lnpart] + [z(ops.layernorm_bwd_partial_rows(T), 3 * D, dt=f) for _ in range(_NBUF - 1)]
+        # scratch of the column reductions, which all run on the engine's bias stream (_BiasReducer.reduce):
+        # nothing on the compute stream reads or writes it
         self.colpart = z(ops.colsum_partial_rows(T), max(3 * D, M, cfg.num_classes), dt=f)
-        self.gelu_parts = [z(-(-T // 128), M, dt=f) for _ in range(2)]  # per-M-tile column sums of dU (fc1 bias)
+        self.gelu_parts = [z(-(-T // 128), M, dt=f) for _ in range(_NBUF)]  # per-M-tile column sums of dU (fc1 bias)
         self.gelu_part = self.gelu_parts[0]
         # column sums of dq|dk|dv (q/k/v bias grads): per image (LDS-resident attention, N <= 320) or per
         # image and 64-row block (K/V-tiled attention, longer sequences)
         self.attn_bias_rows = ops.attention_bias_rows(N)
-        self.qkv_bparts = [z(b * self.attn_bias_rows, 3 * D, dt=f) for _ in range(2)]
+        self.qkv_bparts = [z(b * self.attn_bias_rows, 3 * D, dt=f) for _ in range(_NBUF)]
         self.qkv_bpart = self.qkv_bparts[0]
         nws = ops.attention_workspace_elems(b, N, H)
         self.attn_ws = z(nws, dt=f) if nws else None
@@ -201,6 +207,7 @@ class _BiasReducer:
         if eng._bias_st is None:
             eng._bias_st = torch.cuda.Stream(device=eng.dev)
         self.stream = eng._bias_st
+        self.eng = eng
         self.main = main
         self.a = a
         self.D = eng.cfg.emb_dim
@@ -209,20 +216,22 @@ class _BiasReducer:
 
     def buf(self, kind, bufs):
         i = self.nxt.get(kind, 0)
-        self.nxt[kind] = i ^ 1
+        self.nxt[kind] = (i + 1) % len(bufs)
         ev = self.done.pop((kind, i), None)
-        if ev is not None:
-            self.main.wait_event(ev)
+        if ev is not None:  # (the stream about to write the buffer: compute, or the wgrad side stream)
+            torch.cuda.current_stream(self.main.device).wait_event(ev)
         return bufs[i], (kind, i)
 
     def reduce(self, key, fn):
-        ev = torch.cuda.Event()
-        ev.record(self.main)
+        """fn() on the bias stream after everything issued so far on the compute stream; fn may use
+        a.colpart (the bias stream's scratch: only reductions issued here touch it, in stream order)"""
+        ev = self.eng._event()
+        ev.record(torch.cuda.current_stream(self.main.device))  # after the producer, whichever stream it is on
         self.stream.wait_event(ev)
         with torch.cuda.stream(self.stream):
             fn()
         if key is not None:
-            d = torch.cuda.Event()
+            d = self.eng._event()
             d.record(self.stream)
             self.done[key] = d
 
@@ -301,6 +310,12 @@ class ViTEngine:
         # launches of ~5 us per B/16 step) run on their own stream: nothing on the compute stream waits
         # for them, so they fill the tails of the GEMM launches instead of sitting between them
         self._bias_st = None
+        self._ev_pool, self._ev_next = [], 0
+        self._bias_cur = None  # the backward's _BiasReducer while it runs
+        self._ws_pair = [None, None]
+        # (off by default: on one MI355X the reductions then contend with the GEMMs for CUs, 7402 vs 7446
+        # img/s in a same-box A/B)
+        self._reduce_side = os.environ.get("VITMI_REDUCE_SIDE", "0") != "0"
         self.probe = None  # list: (start, end) HIP events around every fc1 forward GEMM launch
         self.probe_wgrad = None  # list: (start, end, flop, K) around every split-K weight-gradient GEMM launch
         # dropout (nn.Dropout of PositionEmbs / EncoderBlock / MlpBlock, reference src/model.py:19-20,
@@ -309,6 +324,15 @@ class ViTEngine:
         self.drop_seed = (torch.initial_seed() * 0x9E3779B97F4A7C15 + 0x632BE59BD9B4E019) & (2**64 - 1)
         self._drop_offset = 0
         self._drop = None  # (p, seed, offset) of the last forward, or None
+
+    def _event(self):
+        """the next event of the backward's pool (created once, re-recorded every step: a wait enqueued
+        on an event binds to its record at that moment, so re-recording later is safe)"""
+        if self._ev_next == len(self._ev_pool):
+            self._ev_pool.append(torch.cuda.Event())
+        ev = self._ev_pool[self._ev_next]
+        self._ev_next += 1
+        return ev
 
     # ---- parameters --------------------------------------------------------------------------
     def pv(self, name, buf=None):
@@ -384,10 +408,29 @@ class ViTEngine:
             self._ws = torch.empty(numel, device=self.dev)
         return self._ws
 
+    def _side_workspace(self, bias, numel):
+        """one of two split-K slab buffers whose reductions run on the bias stream: the compute stream
+        waits for the reduction that last read the buffer before its GEMM overwrites it"""
+        buf, key = bias.buf("ws", self._ws_pair)
+        i = key[1]
+        if buf is None or buf.numel() < numel:
+            if buf is not None:
+                buf.record_stream(bias.stream)  # a pending reduction may still read the old one
+            buf = torch.empty(numel, device=self.dev)
+            self._ws_pair[i] = buf
+        return buf, key
+
     def _wgrad(self, A, lda, B, ldb, M, N, K, out, ldo, batch=1, b_bs=0, out_bs=0):
-        """out[z] (f32, [M][N], ld ldo) = sum_t A[t][m] B[t][n]  (both operands K-major)."""
+        """out[z] (f32, [M][N], ld ldo) = sum_t A[t][m] B[t][n]  (both operands K-major).
+        During the backward the split-K slab reduction runs on the bias stream (nothing on the compute
+        stream reads a weight gradient; the optimizer and the DP buckets wait for that stream), so the
+        compute stream goes straight on to the next GEMM (VITMI_REDUCE_SIDE=0: inline)."""
         s = self._splitk(M, N, K, batch)
-        ws = self._workspace(batch * s * M * N)
+        bias = self._bias_cur if self._reduce_side else None
+        if bias is not None:
+            ws, key = self._side_workspace(bias, batch * s * M * N)
+        else:
+            ws = self._workspace(batch * s * M * N)
         if self.probe_wgrad is not None:  # bench.py's roofline kernel: events on the stream it runs on
             ev0 = torch.cuda.Event(enable_timing=True)
             ev0.record()
@@ -397,7 +440,10 @@ class ViTEngine:
             ev1 = torch.cuda.Event(enable_timing=True)
             ev1.record()
             self.probe_wgrad.append((ev0, ev1, 2.0 * M * N * K * batch, K))
-        ops.splitk_reduce(ws, batch, s, M, N, out, ldo, out_bs)
+        if bias is not None:
+            bias.reduce(key, lambda: ops.splitk_reduce(ws, batch, s, M, N, out, ldo, out_bs))
+        else:
+            ops.splitk_reduce(ws, batch, s, M, N, out, ldo, out_bs)
 
     # ---- forward -------------------------------------------------------------------------------
     def _dd(self, site, row_stride=1):
@@ -488,7 +534,7 @@ class ViTEngine:
         S = N * D
         ops.gemm(a.o[i], self.woutt[i], a.hm[i], b, D, D, a_layout=K_CONTIG, b_layout=K_CONTIG, lda=S, ldb=D,
                  ldc=S, epilogue=EPI_BIAS_RESID_F32, bias=f[ln("attn.out.bias"):], aux=a.h[i], ldaux=S)
-        a.c_o[:b].copy_(a.o[i][:b * N].view(b, N, D)[:, 0])   # out-proj weight-gradient operand
+        ops.copy2d(a.c_o, D * 2, a.o[i], S * 2, D * 2, b)    # cls rows: the out-proj weight-gradient operand
         ops.layernorm_fwd(a.hm[i], S, f[ln("norm2.weight"):], f[ln("norm2.bias"):], a.c_ln2, D, a.c_mu2, a.c_rs2,
                           b, D)
         ops.gemm(a.c_ln2, mv[ln("mlp.fc1.weight"):], a.c_gp, b, M, D, a_layout=K_CONTIG, b_layout=K_CONTIG, lda=D,
@@ -521,7 +567,7 @@ class ViTEngine:
         bias.ln_bwd(a.c_dyln, D, a.hm[i], S, a.c_mu2, a.c_rs2, f[self.off(self.lname(i, "norm2.weight")):], a.dh, S, b,
                     gv("norm2.weight"), gv("attn.out.bias"), dres=a.dh, lddres=S, dx_bf16=a.c_dh2, lddxb=D)
         on_side(lambda: self._wgrad(a.c_o, D, a.c_dh2, D, D, D, bp, gv("attn.out.weight"), D))
-        a.dO.zero_()
+        ops.zero_(a.dO)
         ops.gemm(a.c_dh2, mv[self.off(self.lname(i, "attn.out.weight")):], a.dO, b, D, D, a_layout=K_CONTIG,
                  b_layout=K_CONTIG, lda=D, ldb=D, ldc=S, epilogue=EPI_BF16)
 
@@ -613,7 +659,7 @@ class ViTEngine:
             if not overlap:
                 fn()
                 return
-            ev = torch.cuda.Event()
+            ev = self._event()
             ev.record(main)
             side.wait_event(ev)
             with torch.cuda.stream(side):
@@ -621,7 +667,7 @@ class ViTEngine:
 
         def release(kind, idx):
             if overlap:
-                ev = torch.cuda.Event()
+                ev = self._event()
                 ev.record(side)
                 free_ev[(kind, idx)] = ev
 
@@ -635,12 +681,14 @@ class ViTEngine:
                 return
             evs = []
             for st in ((main, side) if overlap else (main,)) + (bias.stream,):
-                ev = torch.cuda.Event()
+                ev = self._event()
                 ev.record(st)
                 evs.append(ev)
             hook(g, *bucket, evs)
 
+        self._ev_next = 0  # the event pool is reused from the start by every backward
         bias = _BiasReducer(self, a, main)
+        self._bias_cur = bias
         # classifier head (f32): dWc = dl^T lncls, dbc = colsum(dl), dlncls = dl Wc
         ops.gemm_f32(C, D, b, dl, C, True, a.lncls, D, False, gv("classifier.weight"), D)
         bias.reduce(None, lambda: ops.colsum(dl, b, C, C, a.colpart, gv("classifier.bias")))
@@ -649,9 +697,9 @@ class ViTEngine:
         # (its dx column sum is the last layer's fc2 bias gradient: only the cls rows are non-zero)
         wb = 0  # index of the dhb buffer holding the current residual-gradient copy
         pruned = self._pruned
-        a.dh.zero_()
+        ops.zero_(a.dh)
         if not pruned:
-            a.dhb[wb].zero_()
+            ops.zero_(a.dhb[wb])
         bias.ln_bwd(a.dlncls, D, a.h[L], N * D, a.muf, a.rsf, f[self.off("transformer.norm.weight"):], a.dh, N * D, b,
                     gv("transformer.norm.weight"), gv(self.lname(L - 1, "mlp.fc2.bias")),
                     dx_bf16=a.c_dh if pruned else a.dhb[wb], lddxb=D if pruned else N * D,
@@ -724,6 +772,7 @@ class ViTEngine:
                        gv("embedding.bias"), dropout=dd(0))
         fire(self.layout.buckets[-1])
         bias.finish()
+        self._bias_cur = None
         if overlap:
             main.wait_stream(side)
         return g

@@ -348,3 +348,14 @@ def wgrad(A, lda, B, ldb, M, N, K, out, ldo, accumulate=False, batch=1, a_bs=0, 
     gemm(A, B, ws, M, N, K, a_layout=MN_CONTIG, b_layout=MN_CONTIG, lda=lda, ldb=ldb, ldc=N, epilogue=EPI_SPLITK,
          batch=batch, a_bs=a_bs, b_bs=b_bs, split_k=s)
     splitk_reduce(ws, batch, s, M, N, out, ldo, out_bs, accumulate)
+
+
+def copy2d(dst, dpitch, src, spitch, width, height):
+    """height rows of `width` bytes, dst + r*dpitch <- src + r*spitch (byte pitches; hipMemcpy2DAsync)"""
+    check(lib().vit_copy2d(_p(dst), dpitch, _p(src), spitch, width, height, _stream()), "vit_copy2d")
+
+
+def sgd_step_dev(p, g, buf, p_bf16, n, hyper, wd):
+    """vit_sgd_step with {lr, momentum, first} read from the device tensor `hyper` (graph-capturable)"""
+    _chk(hyper, F32, "hyper")
+    check(lib().vit_sgd_step_dev(_p(p), _p(g), _p(buf), _p(p_bf16), n, _p(hyper), wd, _stream()), "vit_sgd_step_dev")
