@@ -42,7 +42,7 @@ def main():
     rows = list(csv.DictReader(open(sys.argv[1])))
     k = int(sys.argv[2]) if len(sys.argv) > 2 else 1
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-    sgd = [i for i, r in enumerate(rows) if "sgd_kernel" in r["Kernel_Name"] or "adamw_update_kernel" in r["Kernel_Name"]]
+    sgd = [i for i, r in enumerate(rows) if ("sgd_kernel" in r["Kernel_Name"] or "sgd_dev_kernel" in r["Kernel_Name"]) or "adamw_update_kernel" in r["Kernel_Name"]]
     lo, hi = sgd[-k - 1] + 1, sgd[-k] + 1
     step = rows[lo:hi]
     t0 = min(int(r["Start_Timestamp"]) for r in step)

@@ -141,7 +141,7 @@ __device__ __forceinline__ void load_images_lds(lds_t* imgA, const bf16_t* srcA,
 template <int HD, int NKT, int NW>
 __global__ void __launch_bounds__(NW * 64, NW == 8 ? 2 : 3) attn_fwd2_kernel(const bf16_t* __restrict__ qkv,
                                                                bf16_t* __restrict__ o, float* __restrict__ lse,
-                                                               int N, int H, int hd, float scale, int nq, int diag) {
+                                                               int N, int H, int hd, float scale, int nq) {
   constexpr int NP = NKT * 16;
   constexpr int IMG = NP * HD * 2;
   constexpr int T = ImgLane<HD>::TILE;
@@ -155,7 +155,7 @@ __global__ void __launch_bounds__(NW * 64, NW == 8 ? 2 : 3) attn_fwd2_kernel(con
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int g = lane >> 4, i = lane & 15;
   const ImgLane<HD> L(lane);
-  if (!(diag & 1)) load_images_lds<HD, NP, NW * 64>(Ki, base + D, rs, Vi, base + 2 * D, rs, N, hd);
+  load_images_lds<HD, NP, NW * 64>(Ki, base + D, rs, Vi, base + 2 * D, rs, N, hd);
   const float c = scale * LOG2E;
   const int nqa = min(N, (nq + 31) / 32 * 32);  // whole 32-row pairs (the backward's stage 2 reads their lse)
   const int nqt = (nqa + 15) / 16;
@@ -227,494 +227,12 @@ __global__ void __launch_bounds__(NW * 64, NW == 8 ? 2 : 3) attn_fwd2_kernel(con
       for (int dt = 0; dt < HD / 16; ++dt) acc[dt] = mfma16(lds_tr(Vi + (NKT - 1) * T + L.tr[dt]), pp, acc[dt]);
     }
     const int q = qt * 16 + i;
-    if (g == 0 && q < N && !(diag & 2)) lse[(long)bh * N + q] = mx * scale + logf(l);
+    if (g == 0 && q < N) lse[(long)bh * N + q] = mx * scale + logf(l);
     const float inv_l = 1.0f / l;
-    if (!(diag & 2)) {  // whole 2*hd-byte rows through the wave's LDS strip (StripOut)
+    {  // whole 2*hd-byte rows through the wave's LDS strip (StripOut)
       lds_t* so = Vi + IMG + wave * StripOut<HD>::BYTES;
       StripOut<HD>::stage(so, acc, inv_l, lane);
       StripOut<HD>::store(so, o + ((long)b * N + qt * 16) * D + (long)h * hd, D, N - qt * 16, hd, lane);
-    }
-  }
-}
-
-// ------------------------------------------------------------------------------------------------
-// Forward, persistent form: one workgroup of 8 waves per CU walks (image, head) items with stride
-// gridDim.x; the next item's K / V rows (register-staged, 4 + 4 x 16 B per thread) and Q fragments are
-// requested before the current item's MFMAs and land in the second LDS image pair after them, so the
-// HBM stream never waits for a workgroup's compute phase (the one-shot kernel above loads, then
-// computes, and ran at 3.5 TB/s). One barrier per item.
-template <int HD, int NKT>
-struct KVStage {
-  static constexpr int NP = NKT * 16, CPR = HD / 8, TOTAL = NP * CPR, NT = 512;
-  static constexpr int PER = (TOTAL + NT - 1) / NT;
-  v4u a[PER], b[PER];
-  __device__ __forceinline__ void issue(const bf16_t* src, long rs, int D, int N, int hd) {
-    const __amdgpu_buffer_rsrc_t rk = make_rsrc(src + D, (uint32_t)(((long)(N - 1) * rs + hd) * 2));
-    const __amdgpu_buffer_rsrc_t rv = make_rsrc(src + 2 * D, (uint32_t)(((long)(N - 1) * rs + hd) * 2));
-#pragma unroll
-    for (int k = 0; k < PER; ++k) {
-      const int c = threadIdx.x + k * NT;
-      const int row = c / CPR, ch = c % CPR;
-      const bool ok = c < TOTAL && row < N && ch * 8 < hd;
-      const int off = ok ? (int)(((long)row * rs + ch * 8) * 2) : 0x7ffffff0;
-      a[k] = __builtin_amdgcn_raw_buffer_load_b128(rk, off, 0, 0);
-      b[k] = __builtin_amdgcn_raw_buffer_load_b128(rv, off, 0, 0);
-    }
-  }
-  __device__ __forceinline__ void write(lds_t* K, lds_t* V) const {
-#pragma unroll
-    for (int k = 0; k < PER; ++k) {
-      const int c = threadIdx.x + k * NT;
-      if (TOTAL % NT == 0 || c < TOTAL) {
-        const int row = c / CPR, ch = c % CPR;
-        lds_st(K + img_off<HD>(row, ch), a[k]);
-        lds_st(V + img_off<HD>(row, ch), b[k]);
-      }
-    }
-  }
-};
-
-template <int HD, int NKT>
-__global__ void __launch_bounds__(512, 1) attn_fwd_p_kernel(const bf16_t* __restrict__ qkv, bf16_t* __restrict__ o,
-                                                            float* __restrict__ lse, int BH, int N, int H, int hd,
-                                                            float scale, int nq, int diag) {
-  constexpr int NW = 8;
-  constexpr int NP = NKT * 16;
-  constexpr int IMG = NP * HD * 2;
-  constexpr int T = ImgLane<HD>::TILE;
-  constexpr int MAXS = (NKT + NW - 1) / NW;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  lds_t* const L0 = (lds_t*)smem;  // [2 buffers][K image, V image]
-  const int D = H * (int)hd;
-  const long rs = 3L * D;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int g = lane >> 4, i = lane & 15;
-  const ImgLane<HD> L(lane);
-  const float c = scale * LOG2E;
-  const int nqa = min(N, (nq + 31) / 32 * 32);
-  const int nqt = (nqa + 15) / 16;
-  auto item_base = [&](int it) { return qkv + (long)(it / H) * N * rs + (long)(it % H) * hd; };
-
-  KVStage<HD, NKT> st;
-  v8bf qa[MAXS][HD / 32], qn[MAXS][HD / 32];
-  int it = blockIdx.x;
-  {
-    const bf16_t* base = item_base(it);
-    st.issue(base, rs, D, N, hd);
-#pragma unroll
-    for (int u = 0; u < MAXS; ++u)
-#pragma unroll
-      for (int kk = 0; kk < HD / 32; ++kk) qa[u][kk] = gl_row<HD>(base, rs, (wave + u * NW) * 16, kk, N, hd, lane);
-    st.write(L0, L0 + IMG);
-  }
-  __syncthreads();
-  int cur = 0;
-  for (; it < BH; it += gridDim.x) {
-    const int nx = it + gridDim.x;
-    if (nx < BH && !(diag & 1)) {  // diag bit 0 (timing only): keep the first item's operands
-      const bf16_t* nb = item_base(nx);
-      st.issue(nb, rs, D, N, hd);
-#pragma unroll
-      for (int u = 0; u < MAXS; ++u)
-#pragma unroll
-        for (int kk = 0; kk < HD / 32; ++kk) qn[u][kk] = gl_row<HD>(nb, rs, (wave + u * NW) * 16, kk, N, hd, lane);
-    }
-    const lds_t* Ki = L0 + cur * 2 * IMG;
-    const lds_t* Vi = Ki + IMG;
-    const int b = it / H, h = it % H;
-#pragma unroll
-    for (int u = 0; u < MAXS; ++u) {
-      const int qt = wave + u * NW;
-      if (qt < nqt) {
-        v4f s[NKT];
-#pragma unroll
-        for (int kt = 0; kt < NKT; ++kt) {
-          s[kt] = v4f{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-          for (int kk = 0; kk < HD / 32; ++kk)
-            s[kt] = mfma(__builtin_bit_cast(v8bf, lds_ld<v8s>(Ki + kt * T + L.row[kk])), qa[u][kk], s[kt]);
-        }
-        if (N < NP) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            if ((NKT - 1) * 16 + 4 * g + r >= N) s[NKT - 1][r] = -INFINITY;
-        }
-        float mx = fmaxf(fmaxf(s[0][0], s[0][1]), fmaxf(s[0][2], s[0][3]));
-#pragma unroll
-        for (int kt = 1; kt < NKT; ++kt) mx = fmaxf(fmaxf(mx, fmaxf(s[kt][0], s[kt][1])), fmaxf(s[kt][2], s[kt][3]));
-        mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-        const float mc = mx * c;
-        float l = 0.f;
-#pragma unroll
-        for (int kt = 0; kt < NKT; ++kt)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const float p = ex2(fmaf(s[kt][r], c, -mc));
-            s[kt][r] = p;
-            l += p;
-          }
-        l += __shfl_xor(l, 16, 64);
-        l += __shfl_xor(l, 32, 64);
-        const int q = qt * 16 + i;
-        if (g == 0 && q < N) lse[(long)it * N + q] = mx * scale + logf(l);
-        const float inv_l = 1.0f / l;
-        v4f acc[HD / 16];
-#pragma unroll
-        for (int dt = 0; dt < HD / 16; ++dt) acc[dt] = v4f{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int ks = 0; ks < NKT / 2; ++ks) {
-          const v8bf pp = pack8(s[2 * ks], s[2 * ks + 1]);
-#pragma unroll
-          for (int dt = 0; dt < HD / 16; ++dt) {
-            v8s vt;
-            vt.lo = lds_tr(Vi + 2 * ks * T + L.tr[dt]);
-            vt.hi = lds_tr(Vi + (2 * ks + 1) * T + L.tr[dt]);
-            acc[dt] = mfma(__builtin_bit_cast(v8bf, vt), pp, acc[dt]);
-          }
-        }
-        if constexpr (NKT % 2 == 1) {
-          const v4s pp = pack4(s[NKT - 1]);
-#pragma unroll
-          for (int dt = 0; dt < HD / 16; ++dt) acc[dt] = mfma16(lds_tr(Vi + (NKT - 1) * T + L.tr[dt]), pp, acc[dt]);
-        }
-        {
-          lds_t* so = L0 + 4 * IMG + wave * StripOut<HD>::BYTES;
-          StripOut<HD>::stage(so, acc, inv_l, lane);
-          StripOut<HD>::store(so, o + ((long)b * N + qt * 16) * D + (long)h * hd, D, N - qt * 16, hd, lane);
-        }
-      }
-    }
-    if (nx < BH && !(diag & 1)) {
-      st.write(L0 + (cur ^ 1) * 2 * IMG, L0 + (cur ^ 1) * 2 * IMG + IMG);
-#pragma unroll
-      for (int u = 0; u < MAXS; ++u)
-#pragma unroll
-        for (int kk = 0; kk < HD / 32; ++kk) qa[u][kk] = qn[u][kk];
-    }
-    __syncthreads();
-    if (!(diag & 1)) cur ^= 1;
-  }
-}
-
-// ------------------------------------------------------------------------------------------------
-// Backward, lean two-kernel form (HD <= 64). Each kernel has ONE load phase: its two LDS images and
-// every register fragment its waves will use are requested together at the start.
-//   bwd_dq    (K, V images): per 16-query strip, S^T / dP^T of all keys stay in registers, delta =
-//             sum_j P dP (exact; see the round-1 kernel below), dS = P (dP - delta), dQ^T = K^T dS^T.
-//             Writes dQ and delta (f32 [B, H, N], the workspace) for the second kernel.
-//   bwd_dkdv  (Q, dO images + lse, delta): per pair of 16-key tiles and 32-query pair, S and dP with
-//             the key on the lane, P / dS packed as the B operands of dV^T = dO^T P, dK^T = Q^T dS.
-// Keys and queries are padded to whole 16-row tiles only; an odd last tile takes the 16x16x16 MFMA.
-template <int HD, int NKT, int NW>
-__global__ void __launch_bounds__(NW * 64, 2) attn_bwd_dq_kernel(const bf16_t* __restrict__ qkv,
-                                                                 const bf16_t* __restrict__ dout,
-                                                                 const float* __restrict__ lse,
-                                                                 bf16_t* __restrict__ dqkv, float* __restrict__ delta,
-                                                                 float* __restrict__ bias_partial, int N, int H,
-                                                                 int hd, float scale, int nq) {
-  constexpr int NP = NKT * 16;
-  constexpr int IMG = NP * HD * 2;
-  constexpr int T = ImgLane<HD>::TILE;
-  constexpr int MAXS = (NKT + NW - 1) / NW;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  lds_t* Ki = (lds_t*)smem;
-  lds_t* Vi = Ki + IMG;
-  float* bsum = reinterpret_cast<float*>(smem + 2 * IMG);  // [NW][HD]
-  const int bh = blockIdx.x, b = bh / H, h = bh % H;
-  const int D = H * hd;
-  const long rs = 3L * D;
-  const bf16_t* base = qkv + (long)b * N * rs + (long)h * hd;
-  const bf16_t* dob = dout + (long)b * N * D + (long)h * hd;
-  bf16_t* dq_base = dqkv + (long)b * N * rs + (long)h * hd;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int g = lane >> 4, i = lane & 15;
-  const ImgLane<HD> L(lane);
-  const float c = scale * LOG2E;
-  const int nqa = min(N, (nq + 31) / 32 * 32);
-  const int nqt = (nqa + 15) / 16;
-  load_images_lds<HD, NP, NW * 64>(Ki, base + D, rs, Vi, base + 2 * D, rs, N, hd);
-  v8bf qa[MAXS][HD / 32], da[MAXS][HD / 32];
-  float lsa[MAXS];
-#pragma unroll
-  for (int u = 0; u < MAXS; ++u) {
-    const int r0 = (wave + u * NW) * 16;
-#pragma unroll
-    for (int kk = 0; kk < HD / 32; ++kk) {
-      qa[u][kk] = gl_row<HD>(base, rs, r0, kk, N, hd, lane);
-      da[u][kk] = gl_row<HD>(dob, D, r0, kk, N, hd, lane);
-    }
-    const int q = r0 + i;
-    lsa[u] = q < N ? lse[(long)bh * N + q] * LOG2E : INFINITY;  // padded queries: P = 2^-inf = 0
-  }
-  __syncthreads();
-  float bq[HD / 16][4];
-#pragma unroll
-  for (int dt = 0; dt < HD / 16; ++dt)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) bq[dt][r] = 0.f;
-#pragma unroll
-  for (int u = 0; u < MAXS; ++u) {
-    const int qt = wave + u * NW;
-    if (qt * 16 >= N) break;
-    const int q = qt * 16 + i;
-    if (qt >= nqt) {  // no gradient reaches these queries (pruned last layer): dQ = 0, delta = 0
-      if (q < N) {
-        if (g == 0) delta[(long)bh * N + q] = 0.f;
-#pragma unroll
-        for (int dt = 0; dt < HD / 16; ++dt) {
-          const int d = dt * 16 + 4 * g;
-          if (d < hd) store4(dq_base + (long)q * rs + d, v4f{0.f, 0.f, 0.f, 0.f}, 1.f);
-        }
-      }
-      continue;
-    }
-    const float ls = lsa[u];
-    v4f P[NKT], DP[NKT];
-    float dl = 0.f;
-#pragma unroll
-    for (int kt = 0; kt < NKT; ++kt) {
-      v4f st = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int kk = 0; kk < HD / 32; ++kk) {
-        st = mfma(__builtin_bit_cast(v8bf, lds_ld<v8s>(Ki + kt * T + L.row[kk])), qa[u][kk], st);
-        dp = mfma(__builtin_bit_cast(v8bf, lds_ld<v8s>(Vi + kt * T + L.row[kk])), da[u][kk], dp);
-      }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) P[kt][r] = ex2(fmaf(st[r], c, -ls));
-      if (kt == NKT - 1 && N < NP) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          if ((NKT - 1) * 16 + 4 * g + r >= N) P[kt][r] = 0.f;
-      }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) dl = fmaf(P[kt][r], dp[r], dl);
-      DP[kt] = dp;
-    }
-    dl += __shfl_xor(dl, 16, 64);
-    dl += __shfl_xor(dl, 32, 64);
-    if (q >= N) dl = 0.f;
-    if (g == 0 && q < N) delta[(long)bh * N + q] = dl;
-#pragma unroll
-    for (int kt = 0; kt < NKT; ++kt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) P[kt][r] *= DP[kt][r] - dl;  // dS
-    v4f dq[HD / 16];
-#pragma unroll
-    for (int dt = 0; dt < HD / 16; ++dt) dq[dt] = v4f{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int ks = 0; ks < NKT / 2; ++ks) {
-      const v8bf dd = pack8(P[2 * ks], P[2 * ks + 1]);
-#pragma unroll
-      for (int dt = 0; dt < HD / 16; ++dt) {
-        v8s kt8;
-        kt8.lo = lds_tr(Ki + 2 * ks * T + L.tr[dt]);
-        kt8.hi = lds_tr(Ki + (2 * ks + 1) * T + L.tr[dt]);
-        dq[dt] = mfma(__builtin_bit_cast(v8bf, kt8), dd, dq[dt]);
-      }
-    }
-    if constexpr (NKT % 2 == 1) {
-      const v4s dd = pack4(P[NKT - 1]);
-#pragma unroll
-      for (int dt = 0; dt < HD / 16; ++dt) dq[dt] = mfma16(lds_tr(Ki + (NKT - 1) * T + L.tr[dt]), dd, dq[dt]);
-    }
-    {
-      lds_t* so = (lds_t*)(smem + 2 * IMG + NW * HD * 4) + wave * StripOut<HD>::BYTES;
-      StripOut<HD>::stage(so, dq, scale, lane);
-      StripOut<HD>::store(so, dq_base + (long)qt * 16 * rs, rs, N - qt * 16, hd, lane);
-    }
-#pragma unroll
-    for (int dt = 0; dt < HD / 16; ++dt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) bq[dt][r] += dq[dt][r];  // padded queries: dS = 0
-  }
-  if (bias_partial) {
-#pragma unroll
-    for (int dt = 0; dt < HD / 16; ++dt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float v = sum16(bq[dt][r]);
-        if (i == 0) bsum[wave * HD + dt * 16 + 4 * g + r] = v * scale;
-      }
-    __syncthreads();
-    for (int d = threadIdx.x; d < hd; d += NW * 64) {
-      float acc = 0.f;
-#pragma unroll
-      for (int w = 0; w < NW; ++w) acc += bsum[w * HD + d];
-      bias_partial[(long)b * 3 * D + h * hd + d] = acc;
-    }
-  }
-}
-
-template <int HD, int NKT, int NW>
-__global__ void __launch_bounds__(NW * 64, 2) attn_bwd_dkdv_kernel(const bf16_t* __restrict__ qkv,
-                                                                   const bf16_t* __restrict__ dout,
-                                                                   const float* __restrict__ lse,
-                                                                   const float* __restrict__ delta,
-                                                                   bf16_t* __restrict__ dqkv,
-                                                                   float* __restrict__ bias_partial, int N, int H,
-                                                                   int hd, float scale, int nq) {
-  constexpr int NP = NKT * 16;
-  constexpr int IMG = NP * HD * 2;
-  constexpr int T = ImgLane<HD>::TILE;
-  constexpr int NKP = (NKT + 1) / 2;               // key-tile pairs
-  constexpr int MAXP = (NKP + NW - 1) / NW;        // pairs per wave
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  lds_t* Qi = (lds_t*)smem;
-  lds_t* Oi = Qi + IMG;
-  float* lse_s = reinterpret_cast<float*>(smem + 2 * IMG);
-  float* dlt_s = lse_s + NP;
-  float* bsum = dlt_s + NP;  // [NW][2][HD]
-  const int bh = blockIdx.x, b = bh / H, h = bh % H;
-  const int D = H * hd;
-  const long rs = 3L * D;
-  const bf16_t* base = qkv + (long)b * N * rs + (long)h * hd;
-  const bf16_t* dob = dout + (long)b * N * D + (long)h * hd;
-  bf16_t* dk_base = dqkv + (long)b * N * rs + (long)h * hd + D;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int g = lane >> 4, i = lane & 15;
-  const ImgLane<HD> L(lane);
-  const float c = scale * LOG2E;
-  const int nqa = min(N, (nq + 31) / 32 * 32);
-  const int nqt = (nqa + 15) / 16;  // query tiles that carry a gradient (their lse / delta are valid)
-  load_images_lds<HD, NP, NW * 64>(Qi, base, rs, Oi, dob, D, N, hd);
-  v8bf ka[MAXP][2][HD / 32], va[MAXP][2][HD / 32];
-#pragma unroll
-  for (int u = 0; u < MAXP; ++u)
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int kk = 0; kk < HD / 32; ++kk) {
-        const int r0 = (2 * (wave + u * NW) + t) * 16;
-        ka[u][t][kk] = gl_row<HD>(base + D, rs, r0, kk, N, hd, lane);
-        va[u][t][kk] = gl_row<HD>(base + 2 * D, rs, r0, kk, N, hd, lane);
-      }
-  for (int r = threadIdx.x; r < NP; r += NW * 64) {
-    const bool ok = r < N && r < nqt * 16;
-    lse_s[r] = ok ? lse[(long)bh * N + r] * LOG2E : INFINITY;  // P = 0 on padded / gradient-free rows
-    dlt_s[r] = ok ? delta[(long)bh * N + r] : 0.f;
-  }
-  __syncthreads();
-  float bk[HD / 16][4], bv[HD / 16][4];
-#pragma unroll
-  for (int dt = 0; dt < HD / 16; ++dt)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) bk[dt][r] = bv[dt][r] = 0.f;
-  const int nqp = nqt / 2;            // whole query-tile pairs carrying a gradient
-  const bool qtail = (nqt & 1) != 0;  // and a single last tile
-#pragma unroll
-  for (int u = 0; u < MAXP; ++u) {
-    const int kp = wave + u * NW;
-    if (kp >= NKP) break;
-    const bool two = 2 * kp + 1 < NKT;  // the last pair of an odd tile count holds one key tile
-    v4f dv[2][HD / 16], dk[2][HD / 16];
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int dt = 0; dt < HD / 16; ++dt) dv[t][dt] = dk[t][dt] = v4f{0.f, 0.f, 0.f, 0.f};
-    bool kval[2];
-#pragma unroll
-    for (int t = 0; t < 2; ++t) kval[t] = (2 * kp + t) * 16 + i < N;
-    for (int qs = 0; qs < nqp + (qtail ? 1 : 0); ++qs) {
-      const bool full = qs < nqp;  // a query pair (else the single last tile)
-      v4f P[2][2], DS[2][2];       // [key tile t][query tile w]
-#pragma unroll
-      for (int w = 0; w < 2; ++w) {
-        if (w == 1 && !full) break;
-        const int qt = 2 * qs + w;
-        const v4f lq = *reinterpret_cast<const v4f*>(lse_s + qt * 16 + 4 * g);
-        const v4f dq4 = *reinterpret_cast<const v4f*>(dlt_s + qt * 16 + 4 * g);
-        v8bf qr[HD / 32], orr[HD / 32];
-#pragma unroll
-        for (int kk = 0; kk < HD / 32; ++kk) {
-          qr[kk] = __builtin_bit_cast(v8bf, lds_ld<v8s>(Qi + qt * T + L.row[kk]));
-          orr[kk] = __builtin_bit_cast(v8bf, lds_ld<v8s>(Oi + qt * T + L.row[kk]));
-        }
-#pragma unroll
-        for (int t = 0; t < 2; ++t) {
-          if (t == 1 && !two) break;
-          v4f sv = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-          for (int kk = 0; kk < HD / 32; ++kk) {
-            sv = mfma(qr[kk], ka[u][t][kk], sv);
-            dp = mfma(orr[kk], va[u][t][kk], dp);
-          }
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const float p = kval[t] ? ex2(fmaf(sv[r], c, -lq[r])) : 0.f;
-            P[t][w][r] = p;
-            DS[t][w][r] = p * (dp[r] - dq4[r]);
-          }
-        }
-      }
-      if (full) {
-#pragma unroll
-        for (int dt = 0; dt < HD / 16; ++dt) {
-          v8s o8, q8;
-          o8.lo = lds_tr(Oi + 2 * qs * T + L.tr[dt]);
-          o8.hi = lds_tr(Oi + (2 * qs + 1) * T + L.tr[dt]);
-          q8.lo = lds_tr(Qi + 2 * qs * T + L.tr[dt]);
-          q8.hi = lds_tr(Qi + (2 * qs + 1) * T + L.tr[dt]);
-#pragma unroll
-          for (int t = 0; t < 2; ++t) {
-            if (t == 1 && !two) break;
-            dv[t][dt] = mfma(__builtin_bit_cast(v8bf, o8), pack8(P[t][0], P[t][1]), dv[t][dt]);
-            dk[t][dt] = mfma(__builtin_bit_cast(v8bf, q8), pack8(DS[t][0], DS[t][1]), dk[t][dt]);
-          }
-        }
-      } else {
-#pragma unroll
-        for (int dt = 0; dt < HD / 16; ++dt) {
-          const v4s o4 = lds_tr(Oi + 2 * qs * T + L.tr[dt]);
-          const v4s q4 = lds_tr(Qi + 2 * qs * T + L.tr[dt]);
-#pragma unroll
-          for (int t = 0; t < 2; ++t) {
-            if (t == 1 && !two) break;
-            dv[t][dt] = mfma16(o4, pack4(P[t][0]), dv[t][dt]);
-            dk[t][dt] = mfma16(q4, pack4(DS[t][0]), dk[t][dt]);
-          }
-        }
-      }
-    }
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      if (t == 1 && !two) break;
-      {
-        const int k0 = (2 * kp + t) * 16;
-        lds_t* so = (lds_t*)(bsum + NW * 2 * HD) + wave * StripOut<HD>::BYTES;
-        StripOut<HD>::stage(so, dk[t], scale, lane);
-        StripOut<HD>::store(so, dk_base + (long)k0 * rs, rs, N - k0, hd, lane);
-        StripOut<HD>::stage(so, dv[t], 1.0f, lane);
-        StripOut<HD>::store(so, dk_base + (long)k0 * rs + D, rs, N - k0, hd, lane);
-      }
-#pragma unroll
-      for (int dt = 0; dt < HD / 16; ++dt)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {  // invalid keys hold exact zeros (P = 0)
-          bk[dt][r] += dk[t][dt][r];
-          bv[dt][r] += dv[t][dt][r];
-        }
-    }
-  }
-  if (bias_partial) {
-#pragma unroll
-    for (int dt = 0; dt < HD / 16; ++dt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float a = sum16(bk[dt][r]), v = sum16(bv[dt][r]);
-        if (i == 0) {
-          bsum[(wave * 2 + 0) * HD + dt * 16 + 4 * g + r] = a * scale;
-          bsum[(wave * 2 + 1) * HD + dt * 16 + 4 * g + r] = v;
-        }
-      }
-    __syncthreads();
-    for (int e = threadIdx.x; e < 2 * HD; e += NW * 64) {
-      const int z = e / HD, d = e % HD;
-      if (d >= hd) continue;
-      float acc = 0.f;
-#pragma unroll
-      for (int w = 0; w < NW; ++w) acc += bsum[(w * 2 + z) * HD + d];
-      bias_partial[(long)b * 3 * D + (1 + z) * D + h * hd + d] = acc;
     }
   }
 }
@@ -738,7 +256,7 @@ __global__ void __launch_bounds__(NW * 64, 2) attn_bwd_kernel(const bf16_t* __re
                                                               const bf16_t* __restrict__ dout,
                                                               const float* __restrict__ lse, bf16_t* __restrict__ dqkv,
                                                               float* __restrict__ bias_partial, int N, int H, int hd,
-                                                              float scale, int stages, int nq) {
+                                                              float scale, int nq) {
   constexpr int NP = NKT * 16;
   constexpr int IMG = NP * HD * 2;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -757,7 +275,8 @@ __global__ void __launch_bounds__(NW * 64, 2) attn_bwd_kernel(const bf16_t* __re
 
   load_images<HD, NP, NW * 64>(ImA, base + D, rs, ImB, base + 2 * D, rs, N, hd);
   for (int r = threadIdx.x; r < NP; r += blockDim.x) {
-    lse_s[r] = r < N ? lse[(long)bh * N + r] * LOG2E : INFINITY;  // padded queries: P = 2^-inf = 0
+    // padded queries: P = 2^-1e30 = 0 (finite, so that nan_of() of their exponent stays 0)
+    lse_s[r] = r < N ? lse[(long)bh * N + r] * LOG2E : 1e30f;
     dlt_s[r] = 0.f;
   }
   __syncthreads();
@@ -777,8 +296,7 @@ __global__ void __launch_bounds__(NW * 64, 2) attn_bwd_kernel(const bf16_t* __re
     for (int r = 0; r < 4; ++r) bq[dt][r] = bk[dt][r] = bv[dt][r] = 0.f;
 
   // ---- stage 1: delta and dQ ----
-  if (!(stages & 1)) {
-  } else if constexpr (HD <= 64) {
+  if constexpr (HD <= 64) {
     // one 16-query strip at a time with P and dP of ALL keys kept in registers (2 x NKT x 4 f32):
     // delta = sum_j P dP comes out of the same pass, so dS and dQ need no recompute of S / dP
     const int nqt = (N + 15) / 16;
@@ -826,18 +344,16 @@ __global__ void __launch_bounds__(NW * 64, 2) attn_bwd_kernel(const bf16_t* __re
         }
         // Padded keys (rows N.. of the zero-filled K / V images) need no mask here: their dP = dO V^T
         // is 0, so they add nothing to delta, and their dS only meets the zero K rows in dQ = dS K.
-        // On the tile holding keys >= N (the only one with padded keys that is computed: a wholly padded
-        // last tile is skipped above; a wave-uniform condition) their exponent is clamped at 0 so that P
-        // stays finite for them whatever the query's LSE (a real key's exponent is <= 0 up to rounding:
-        // LSE >= every score; unclamped, a padded key's 2^(-LSE) overflows for LSE << 0 and P dP = inf *
-        // 0 = NaN); elsewhere a NaN score stays NaN. The per-(tile, row) masks this replaces were
-        // spilled SGPR lane masks: 2 v_readlane + 2 v_cndmask per element.
-        // (inside that tile only the padded keys themselves are clamped: a NaN score of a real key stays NaN)
-        const bool pad_tile = (kt + 1) * 16 > N;
+        // Their exponent -LSE is clamped at 0 so that P stays finite whatever the query's LSE (unclamped,
+        // LSE << 0 gives 2^-LSE = inf and P dP = inf * 0 = NaN); a real key's exponent is <= 0 up to
+        // rounding (LSE >= every score), so the clamp is applied to every key without a mask (the
+        // per-(tile, row) masks it replaces were spilled SGPR lane masks: 2 v_readlane + 2 v_cndmask per
+        // element). nan_of(e) = e - e in hardware (0, or NaN for a NaN score) keeps a diverging run's NaN
+        // visible in dQ: v_min alone returns the non-NaN operand.
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const float e = st[r] * c - ls;
-          const float pv = ex2(pad_tile && kt * 16 + 4 * g + r >= N ? fminf(e, 0.f) : e);
+          const float pv = ex2(fminf(e, 0.f) + nan_of(e));
           P[kt][r] = pv;
           dlr[r] += pv * dpt[r];
         }
@@ -1019,18 +535,12 @@ __global__ void __launch_bounds__(NW * 64, 2) attn_bwd_kernel(const bf16_t* __re
   for (int t = 0; t < 2; ++t)
 #pragma unroll
     for (int kk = 0; kk < HD / 32; ++kk) {
-      if (stages & 4) {  // diagnostic (VIT_ATTN_BWD_STAGES bit 2): the first pair from HBM as well
-        kn[t][kk] = gl_row<HD>(base + D, rs, (2 * wave + t) * 16, kk, N, hd, lane);
-        vn[t][kk] = gl_row<HD>(base + 2 * D, rs, (2 * wave + t) * 16, kk, N, hd, lane);
-      } else {
-        kn[t][kk] = wave < npair ? rd_row<HD>(ImA, (2 * wave + t) * 16, kk, lane) : v8bf{};
-        vn[t][kk] = wave < npair ? rd_row<HD>(ImB, (2 * wave + t) * 16, kk, lane) : v8bf{};
-      }
+      kn[t][kk] = wave < npair ? rd_row<HD>(ImA, (2 * wave + t) * 16, kk, lane) : v8bf{};
+      vn[t][kk] = wave < npair ? rd_row<HD>(ImB, (2 * wave + t) * 16, kk, lane) : v8bf{};
     }
   __syncthreads();  // K / V images no longer read; delta complete
 
   // ---- stage 2: dK and dV, key-tile pairs ----
-  if (!(stages & 2)) return;  // diagnostic timing of stage 1 alone (VIT_ATTN_BWD_STAGES)
   // Q, dO: only the query pairs stage 2 visits (rows past nqa read as zeros without a memory access)
   load_images<HD, NP, NW * 64>(ImA, base, rs, ImB, dob, D, min(N, 32 * npair_q), hd);
   __syncthreads();
@@ -1175,304 +685,6 @@ __global__ void __launch_bounds__(NW * 64, 2) attn_bwd_kernel(const bf16_t* __re
   }
 }
 
-// ------------------------------------------------------------------------------------------------
-// Persistent backward (HD <= 64, N <= 224): one 512-thread workgroup per CU walks the (image, head)
-// items. Seven compute waves run the two stages of attn_bwd_kernel above (stage 1: 16-query strips,
-// exact delta = sum_j P dP and dQ; stage 2: one 32-key pair per wave, dK / dV); the eighth wave is a
-// loader that moves the images the compute waves need NEXT into LDS by LDS-DMA while they work:
-// Q / dO of the current item during stage 1, K / V of the next item during stage 2. No image load
-// sits on the critical path (the one-shot kernel's load -> sync -> compute phases cost ~200 us of
-// its ~300 us in the B/16 step: the q_rows = 1 layer, almost no math, took 200 us), and the compute
-// waves' own vmcnt waits (their Q / dO strip rows) never cover the DMA, which the loader alone
-// waits for. Outputs leave through wave-private LDS strips as whole 128-B rows (StripOut).
-template <int HD, int NKT>
-__global__ void __launch_bounds__(512, 1) attn_bwd_p_kernel(const bf16_t* __restrict__ qkv,
-                                                            const bf16_t* __restrict__ dout,
-                                                            const float* __restrict__ lse, bf16_t* __restrict__ dqkv,
-                                                            float* __restrict__ bias_partial, int B, int N, int H,
-                                                            int hd, float scale, int nq) {
-  constexpr int NP = NKT * 16, IMG = NP * HD * 2, NCW = 7;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* ImK = smem;
-  char* ImV = smem + IMG;
-  char* ImQ = smem + 2 * IMG;
-  char* ImO = smem + 3 * IMG;
-  float* lse_s0 = reinterpret_cast<float*>(smem + 4 * IMG);  // [2][NP], by item parity
-  float* dlt_s = lse_s0 + 2 * NP;                             // [NP]
-  float* bsum0 = dlt_s + NP;                                  // [2][NCW][3][HD], by item parity
-  lds_t* strips = (lds_t*)(bsum0 + 2 * NCW * 3 * HD);         // [NCW] StripOut buffers
-
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const bool loader = wave == NCW;
-  const int g = lane >> 4, i = lane & 15;
-  const int D = H * hd;
-  const long rs = 3L * D;
-  const float c = scale * LOG2E;
-  const int items = B * H;
-  const int nqt = (N + 15) / 16, npair = (N + 31) / 32;
-  const int nqa = min(N, (nq + 31) / 32 * 32);
-  const int npair_q = (nqa + 31) / 32;
-  const bool last_half = (2 * npair - 1) * 16 >= N;
-  lds_t* so = strips + (wave < NCW ? wave : 0) * StripOut<HD>::BYTES;
-
-  // loader: rows [0, rows_img) of a [N][hd] slice (row stride ld) into a swizzled image; rows >= N and
-  // columns >= hd land as zeros (out of the descriptor's range). One 1-KiB LDS-DMA per RPI rows:
-  // lane L fills image row r0 + L / CPR at chunk position L % CPR, i.e. source chunk (L % CPR) ^ swizzle.
-  auto dma = [&](char* img, const bf16_t* src, long ld, int rows_img) {
-    constexpr int CPR = HD / 8, RPI = 64 / CPR;
-    const __amdgpu_buffer_rsrc_t rsc = make_rsrc(src, (uint32_t)(((long)(N - 1) * ld + hd) * 2));
-    const int rl = lane / CPR, pc = lane % CPR;
-    for (int r0 = 0; r0 < rows_img; r0 += RPI) {
-      const int r = r0 + rl;
-      const int ch = pc ^ aswz<HD>(r);
-      const int off = (r < N && ch * 8 < hd) ? (int)(((long)r * ld + ch * 8) * 2) : 0x7ffffff0;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsc, LDS_PTR(void, img + r0 * HD * 2), 16, off, 0, 0, 0);
-    }
-  };
-  auto load_lse = [&](int it, float* dst) {
-    for (int r = lane; r < NP; r += 64) dst[r] = r < N ? lse[(long)it * N + r] * LOG2E : INFINITY;
-  };
-  auto kv_base = [&](int it) { return qkv + (long)(it / H) * N * rs + (long)(it % H) * hd; };
-
-  const int it0 = blockIdx.x;
-  if (loader && it0 < items) {
-    const bf16_t* base = kv_base(it0);
-    dma(ImK, base + D, rs, NP);
-    dma(ImV, base + 2 * D, rs, NP);
-    load_lse(it0, lse_s0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __syncthreads();
-
-  int par = 0;
-  for (int it = it0; it < items; it += gridDim.x, par ^= 1) {
-    const int b = it / H, h = it % H;
-    const bf16_t* base = kv_base(it);
-    const bf16_t* dob = dout + (long)b * N * D + (long)h * hd;
-    bf16_t* dq_base = dqkv + (long)b * N * rs + (long)h * hd;
-    const float* lse_s = lse_s0 + par * NP;
-    float* bsum = bsum0 + par * NCW * 3 * HD;
-
-    // ---- phase 1: stage 1 on K / V images; the loader brings Q / dO ----
-    if (loader) {
-      dma(ImQ, base, rs, 32 * npair_q);
-      dma(ImO, dob, D, 32 * npair_q);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    } else {
-      if (i == 0) {
-#pragma unroll
-        for (int dt = 0; dt < HD / 16; ++dt)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) bsum[(wave * 3 + 0) * HD + dt * 16 + 4 * g + r] = 0.f;
-      }
-      v8bf qn[HD / 32], dn[HD / 32];  // next strip's Q / dO rows, requested one strip ahead
-#pragma unroll
-      for (int kk = 0; kk < HD / 32; ++kk) {
-        qn[kk] = gl_row<HD>(base, rs, wave * 16, kk, N, hd, lane);
-        dn[kk] = gl_row<HD>(dob, D, wave * 16, kk, N, hd, lane);
-      }
-      for (int qt = wave; qt < nqt; qt += NCW) {
-        if (qt * 16 >= nqa) {  // no gradient reaches these queries: dQ = 0, delta = 0
-          if (g == 0) dlt_s[qt * 16 + i] = 0.f;
-          v4f z[HD / 16];
-#pragma unroll
-          for (int dt = 0; dt < HD / 16; ++dt) z[dt] = v4f{0.f, 0.f, 0.f, 0.f};
-          StripOut<HD>::stage(so, z, 1.0f, lane);
-          StripOut<HD>::store(so, dq_base + (long)qt * 16 * rs, rs, N - qt * 16, hd, lane);
-          continue;
-        }
-        v8bf qf[HD / 32], df[HD / 32];
-#pragma unroll
-        for (int kk = 0; kk < HD / 32; ++kk) {
-          qf[kk] = qn[kk];
-          df[kk] = dn[kk];
-          qn[kk] = gl_row<HD>(base, rs, (qt + NCW) * 16, kk, N, hd, lane);
-          dn[kk] = gl_row<HD>(dob, D, (qt + NCW) * 16, kk, N, hd, lane);
-        }
-        const float ls = lse_s[qt * 16 + i];
-        v4f P[NKT], DP[NKT];
-        float dl = 0.f;
-#pragma unroll
-        for (int kt = 0; kt < NKT; ++kt) {
-          if (kt == NKT - 1 && kt * 16 >= N) {  // a wholly padded last key tile
-            P[kt] = DP[kt] = v4f{0.f, 0.f, 0.f, 0.f};
-            continue;
-          }
-          v4f st = {0.f, 0.f, 0.f, 0.f}, dpt = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-          for (int kk = 0; kk < HD / 32; ++kk) {
-            st = mfma(rd_row<HD>(ImK, kt * 16, kk, lane), qf[kk], st);
-            dpt = mfma(rd_row<HD>(ImV, kt * 16, kk, lane), df[kk], dpt);
-          }
-          const bool full = (kt + 1) * 16 <= N;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            float pv = ex2(st[r] * c - ls);
-            if (!full && kt * 16 + 4 * g + r >= N) pv = 0.f;
-            P[kt][r] = pv;
-            dl += pv * dpt[r];
-          }
-          DP[kt] = dpt;
-        }
-        dl += __shfl_xor(dl, 16, 64);
-        dl += __shfl_xor(dl, 32, 64);
-        const int q = qt * 16 + i;
-        if (q >= N) dl = 0.f;
-        if (g == 0) dlt_s[q] = dl;
-        v4f dq[HD / 16];
-#pragma unroll
-        for (int dt = 0; dt < HD / 16; ++dt) dq[dt] = v4f{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int ks = 0; ks < NKT / 2; ++ks) {
-          v4f d0, d1;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            d0[r] = P[2 * ks][r] * (DP[2 * ks][r] - dl);
-            d1[r] = P[2 * ks + 1][r] * (DP[2 * ks + 1][r] - dl);
-          }
-          const v8bf bD = pack8(d0, d1);
-#pragma unroll
-          for (int dt = 0; dt < HD / 16; ++dt)
-            dq[dt] = mfma(rd_tr<HD>(ImK, 2 * ks, 2 * ks + 1, dt * 16, lane), bD, dq[dt]);
-        }
-        StripOut<HD>::stage(so, dq, scale, lane);
-        StripOut<HD>::store(so, dq_base + (long)qt * 16 * rs, rs, N - qt * 16, hd, lane);
-        if (bias_partial) {  // the strip's dQ column sums (padded queries: dS = 0) into the wave's slot
-#pragma unroll
-          for (int dt = 0; dt < HD / 16; ++dt)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const float v = sum16(dq[dt][r]);
-              if (i == 0) bsum[(wave * 3 + 0) * HD + dt * 16 + 4 * g + r] += v * scale;
-            }
-        }
-      }
-    }
-    __syncthreads();  // Q / dO images landed; delta complete; K / V images read by stage 1
-
-    // ---- phase 2: each compute wave takes its key pair's K / V rows into registers ----
-    const int kp = wave;
-    const bool has_kp = !loader && kp < npair;
-    v8bf kf[2][HD / 32], vf[2][HD / 32];
-    if (has_kp) {
-#pragma unroll
-      for (int t = 0; t < 2; ++t)
-#pragma unroll
-        for (int kk = 0; kk < HD / 32; ++kk) {
-          kf[t][kk] = rd_row<HD>(ImK, (2 * kp + t) * 16, kk, lane);
-          vf[t][kk] = rd_row<HD>(ImV, (2 * kp + t) * 16, kk, lane);
-        }
-    }
-    __syncthreads();  // K / V images free for the next item
-
-    // ---- phase 3: stage 2 on Q / dO images; the loader brings the next item's K / V ----
-    if (loader) {
-      const int nxt = it + gridDim.x;
-      if (nxt < items) {
-        const bf16_t* nb = kv_base(nxt);
-        dma(ImK, nb + D, rs, NP);
-        dma(ImV, nb + 2 * D, rs, NP);
-        load_lse(nxt, lse_s0 + (par ^ 1) * NP);
-      }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    } else {
-      if (i == 0) {
-#pragma unroll
-        for (int dt = 0; dt < HD / 16; ++dt)
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            bsum[(wave * 3 + 1) * HD + dt * 16 + 4 * g + r] = bsum[(wave * 3 + 2) * HD + dt * 16 + 4 * g + r] = 0.f;
-      }
-      if (has_kp) {
-        v4f dv[2][HD / 16], dk[2][HD / 16];
-#pragma unroll
-        for (int t = 0; t < 2; ++t)
-#pragma unroll
-          for (int dt = 0; dt < HD / 16; ++dt) dv[t][dt] = dk[t][dt] = v4f{0.f, 0.f, 0.f, 0.f};
-        for (int qs = 0; qs < npair_q; ++qs) {
-          v4f P[2][2], DS[2][2];  // [key tile][query tile]
-#pragma unroll
-          for (int u = 0; u < 2; ++u) {
-            const int qt = 2 * qs + u;
-            if (u == 1 && last_half && qs == npair - 1) {
-              P[0][1] = P[1][1] = DS[0][1] = DS[1][1] = v4f{0.f, 0.f, 0.f, 0.f};
-              continue;
-            }
-            v8bf qr[HD / 32], orow[HD / 32];
-#pragma unroll
-            for (int kk = 0; kk < HD / 32; ++kk) {
-              qr[kk] = rd_row<HD>(ImQ, qt * 16, kk, lane);
-              orow[kk] = rd_row<HD>(ImO, qt * 16, kk, lane);
-            }
-            const v4f lq = *reinterpret_cast<const v4f*>(lse_s + qt * 16 + 4 * g);
-            const v4f dq4 = *reinterpret_cast<const v4f*>(dlt_s + qt * 16 + 4 * g);
-#pragma unroll
-            for (int t = 0; t < 2; ++t) {
-              v4f sv = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-              for (int kk = 0; kk < HD / 32; ++kk) {
-                sv = mfma(qr[kk], kf[t][kk], sv);
-                dp = mfma(orow[kk], vf[t][kk], dp);
-              }
-              const bool kvalid = (2 * kp + t) * 16 + i < N;
-#pragma unroll
-              for (int r = 0; r < 4; ++r) {
-                const float pp = kvalid ? ex2(sv[r] * c - lq[r]) : 0.f;
-                P[t][u][r] = pp;
-                DS[t][u][r] = pp * (dp[r] - dq4[r]);
-              }
-            }
-          }
-          const v8bf bP0 = pack8(P[0][0], P[0][1]), bP1 = pack8(P[1][0], P[1][1]);
-          const v8bf bD0 = pack8(DS[0][0], DS[0][1]), bD1 = pack8(DS[1][0], DS[1][1]);
-#pragma unroll
-          for (int dt = 0; dt < HD / 16; ++dt) {
-            const v8bf ot = rd_tr<HD>(ImO, 2 * qs, 2 * qs + 1, dt * 16, lane);
-            const v8bf qtr = rd_tr<HD>(ImQ, 2 * qs, 2 * qs + 1, dt * 16, lane);
-            dv[0][dt] = mfma(ot, bP0, dv[0][dt]);
-            dv[1][dt] = mfma(ot, bP1, dv[1][dt]);
-            dk[0][dt] = mfma(qtr, bD0, dk[0][dt]);
-            dk[1][dt] = mfma(qtr, bD1, dk[1][dt]);
-          }
-        }
-#pragma unroll
-        for (int t = 0; t < 2; ++t) {
-          const int k0 = (2 * kp + t) * 16;
-          if (k0 < N) {
-            StripOut<HD>::stage(so, dk[t], scale, lane);
-            StripOut<HD>::store(so, dq_base + (long)k0 * rs + D, rs, N - k0, hd, lane);
-            StripOut<HD>::stage(so, dv[t], 1.0f, lane);
-            StripOut<HD>::store(so, dq_base + (long)k0 * rs + 2 * D, rs, N - k0, hd, lane);
-          }
-        }
-        if (bias_partial) {  // invalid keys hold exact zeros (P = 0)
-#pragma unroll
-          for (int dt = 0; dt < HD / 16; ++dt)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const float a = sum16(dk[0][dt][r] + dk[1][dt][r]), v = sum16(dv[0][dt][r] + dv[1][dt][r]);
-              if (i == 0) {
-                bsum[(wave * 3 + 1) * HD + dt * 16 + 4 * g + r] = a * scale;
-                bsum[(wave * 3 + 2) * HD + dt * 16 + 4 * g + r] = v;
-              }
-            }
-        }
-      }
-    }
-    __syncthreads();  // item done: Q / dO images and delta free; next K / V and lse landed
-    if (loader && bias_partial) {
-      for (int e = lane; e < 3 * HD; e += 64) {
-        const int z = e / HD, d = e % HD;
-        if (d >= hd) continue;
-        float acc = 0.f;
-#pragma unroll
-        for (int w = 0; w < NCW; ++w) acc += bsum[(w * 3 + z) * HD + d];
-        bias_partial[(long)b * 3 * D + z * D + h * hd + d] = acc;
-      }
-    }
-  }
-}
-
 template <int HD, int NKT, int NW>
 hipError_t launch_fwd_nw(const bf16_t* qkv, bf16_t* o, float* lse, int B, int N, int H, int hd, float scale,
                          int nq, hipStream_t s) {
@@ -1483,156 +695,38 @@ hipError_t launch_fwd_nw(const bf16_t* qkv, bf16_t* o, float* lse, int B, int N,
   return hipGetLastError();
 }
 
-template <int HD, int NKT16, int NW = 4>
+template <int HD, int NKT16, int NW = 8>
 hipError_t launch_fwd2(const bf16_t* qkv, bf16_t* o, float* lse, int B, int N, int H, int hd, float scale, int nq,
                        hipStream_t s) {
   const size_t lds = (size_t)2 * NKT16 * 16 * HD * 2 + (size_t)NW * StripOut<HD>::BYTES;
   auto kern = attn_fwd2_kernel<HD, NKT16, NW>;
   if (lds > 64 * 1024) (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  static const int diag = [] {
-    const char* e = getenv("VIT_ATTN_DIAG");
-    return e ? atoi(e) : 0;
-  }();
-  hipLaunchKernelGGL(kern, dim3(B * H), dim3(NW * 64), lds, s, qkv, o, lse, N, H, hd, scale, nq, diag);
+  hipLaunchKernelGGL(kern, dim3(B * H), dim3(NW * 64), lds, s, qkv, o, lse, N, H, hd, scale, nq);
   return hipGetLastError();
 }
 
-template <int HD, int NKT16>
-hipError_t launch_fwd_p(const bf16_t* qkv, bf16_t* o, float* lse, int B, int N, int H, int hd, float scale, int nq,
-                        hipStream_t s) {
-  const size_t lds = (size_t)4 * NKT16 * 16 * HD * 2 + (size_t)8 * StripOut<HD>::BYTES;
-  auto kern = attn_fwd_p_kernel<HD, NKT16>;
-  if (lds > 64 * 1024) (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  static const int ncu = [] {
-    int dev = 0, n = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
-    return n > 0 ? n : 256;
-  }();
-  const int bh = B * H;
-  static const int diag = [] {
-    const char* e = getenv("VIT_ATTN_DIAG");
-    return e ? atoi(e) : 0;
-  }();
-  static const int grid_mul = [] {
-    const char* e = getenv("VIT_ATTN_FWD_GRID");  // workgroups per CU (diagnostics)
-    return e ? atoi(e) : 1;
-  }();
-  const int grid = ncu * grid_mul;
-  hipLaunchKernelGGL(kern, dim3(bh < grid ? bh : grid), dim3(512), lds, s, qkv, o, lse, bh, N, H, hd, scale, nq, diag);
-  return hipGetLastError();
-}
-
+// Forward: the lean 8-wave kernel (attn_fwd2_kernel) for head widths up to 64; hd 80 / 96 (ViT-H/14) on
+// the 4-wave kernel, whose registers hold one 16-query strip at a time
 template <int HD, int NKT>
 hipError_t launch_fwd(const bf16_t* qkv, bf16_t* o, float* lse, int B, int N, int H, int hd, float scale,
                       int nq, hipStream_t s) {
-  // VIT_ATTN_FWD_VARIANT (diagnostics): 3 one-shot lean 8-wave (default), 1 one-shot lean 4-wave,
-  // 0 persistent double-buffered, 2 the round-1 kernel
-  static const int var = [] {
-    const char* e = getenv("VIT_ATTN_FWD_VARIANT");
-    return e ? atoi(e) : 3;
-  }();
-  const bool old = var == 2;
-  // persistent double-buffered form while two K/V image pairs fit the 160 KiB LDS
-  if (var == 0 && HD <= 64 && 4 * ((N + 15) / 16) * 16 * HD * 2 + 8 * StripOut<HD>::BYTES <= 160 * 1024) {
-    if ((N + 15) / 16 == NKT) return launch_fwd_p<HD, NKT>(qkv, o, lse, B, N, H, hd, scale, nq, s);
-    return launch_fwd_p<HD, NKT - 1>(qkv, o, lse, B, N, H, hd, scale, nq, s);
-  }
-  if (var == 3 && HD <= 64) {
-    if ((N + 15) / 16 == NKT) return launch_fwd2<HD, NKT, 8>(qkv, o, lse, B, N, H, hd, scale, nq, s);
-    return launch_fwd2<HD, NKT - 1, 8>(qkv, o, lse, B, N, H, hd, scale, nq, s);
-  }
-  if (!old && HD <= 64) {  // NKT = 2 * ceil(N / 32); the lean kernel takes ceil(N / 16) tiles
+  if (HD <= 64) {  // NKT = 2 * ceil(N / 32); the lean kernel takes ceil(N / 16) tiles
     if ((N + 15) / 16 == NKT) return launch_fwd2<HD, NKT>(qkv, o, lse, B, N, H, hd, scale, nq, s);
     return launch_fwd2<HD, NKT - 1>(qkv, o, lse, B, N, H, hd, scale, nq, s);
   }
-  static const int nw = [] {
-    const char* e = getenv("VIT_ATTN_FWD_NW");
-    return e ? atoi(e) : 4;
-  }();
-  if (nw == 8) return launch_fwd_nw<HD, NKT, 8>(qkv, o, lse, B, N, H, hd, scale, nq, s);
   return launch_fwd_nw<HD, NKT, 4>(qkv, o, lse, B, N, H, hd, scale, nq, s);
 }
 
-template <int HD, int NKT, int NW>
-hipError_t launch_bwd_nw(const bf16_t* qkv, const bf16_t* dout, const float* lse, bf16_t* dqkv, float* bias_partial,
-                         int B, int N, int H, int hd, float scale, int nq, hipStream_t s) {
+// Backward: the two-stage kernel, 4 waves (two workgroups per CU)
+template <int HD, int NKT>
+hipError_t launch_bwd(const bf16_t* qkv, const bf16_t* dout, const float* lse, bf16_t* dqkv, float* bias_partial,
+                      int B, int N, int H, int hd, float scale, int nq, hipStream_t s) {
+  constexpr int NW = 4;
   const size_t lds = (size_t)2 * NKT * 16 * HD * 2 + 2 * NKT * 16 * 4 + (size_t)NW * 3 * HD * 4;
   auto kern = attn_bwd_kernel<HD, NKT, NW>;
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  static const int stages = [] {
-    const char* e = getenv("VIT_ATTN_BWD_STAGES");
-    return e ? atoi(e) : 3;
-  }();
-  hipLaunchKernelGGL(kern, dim3(B * H), dim3(NW * 64), lds, s, qkv, dout, lse, dqkv, bias_partial, N, H, hd, scale,
-                     stages, nq);
+  hipLaunchKernelGGL(kern, dim3(B * H), dim3(NW * 64), lds, s, qkv, dout, lse, dqkv, bias_partial, N, H, hd, scale, nq);
   return hipGetLastError();
-}
-
-template <int HD, int NKT>
-hipError_t launch_bwd_p(const bf16_t* qkv, const bf16_t* dout, const float* lse, bf16_t* dqkv, float* bias_partial,
-                        int B, int N, int H, int hd, float scale, int nq, hipStream_t s) {
-  constexpr int NP = NKT * 16;
-  const size_t lds = (size_t)4 * NP * HD * 2 + (size_t)3 * NP * 4 + (size_t)2 * 7 * 3 * HD * 4 +
-                     (size_t)7 * StripOut<HD>::BYTES;
-  auto kern = attn_bwd_p_kernel<HD, NKT>;
-  (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  static const int ncu = [] {
-    int dev = 0, n = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-      return 256;
-    return n;
-  }();
-  const int items = B * H;
-  hipLaunchKernelGGL(kern, dim3(items < ncu ? items : ncu), dim3(512), lds, s, qkv, dout, lse, dqkv, bias_partial, B, N,
-                     H, hd, scale, nq);
-  return hipGetLastError();
-}
-
-template <int HD, int NKT16>
-hipError_t launch_bwd2(const bf16_t* qkv, const bf16_t* dout, const float* lse, float* delta, bf16_t* dqkv,
-                       float* bias_partial, int B, int N, int H, int hd, float scale, int nq, hipStream_t s) {
-  constexpr int NP = NKT16 * 16;
-  const size_t lds1 = (size_t)2 * NP * HD * 2 + (size_t)4 * HD * 4 + (size_t)4 * StripOut<HD>::BYTES;
-  auto k1 = attn_bwd_dq_kernel<HD, NKT16, 4>;
-  if (lds1 > 64 * 1024) (void)hipFuncSetAttribute((const void*)k1, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds1);
-  hipLaunchKernelGGL(k1, dim3(B * H), dim3(256), lds1, s, qkv, dout, lse, dqkv, delta, bias_partial, N, H, hd, scale,
-                     nq);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return e;
-  const size_t lds2 = (size_t)2 * NP * HD * 2 + (size_t)2 * NP * 4 + (size_t)4 * 2 * HD * 4 + (size_t)4 * StripOut<HD>::BYTES;
-  auto k2 = attn_bwd_dkdv_kernel<HD, NKT16, 4>;
-  if (lds2 > 64 * 1024) (void)hipFuncSetAttribute((const void*)k2, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds2);
-  hipLaunchKernelGGL(k2, dim3(B * H), dim3(256), lds2, s, qkv, dout, lse, delta, dqkv, bias_partial, N, H, hd, scale,
-                     nq);
-  return hipGetLastError();
-}
-
-template <int HD, int NKT>
-hipError_t launch_bwd(const bf16_t* qkv, const bf16_t* o, const bf16_t* dout, const float* lse, bf16_t* dqkv,
-                      float* bias_partial, int B, int N, int H, int hd, float scale, int nq, float* delta,
-                      hipStream_t s) {
-  (void)o;
-  // VIT_ATTN_BWD_VARIANT: 2 = the single-kernel two-stage form (default: 272 us in the B/16 bs256 step
-  // against 294 us for the two-kernel form), 0 = the lean two-kernel form, 3 = the persistent
-  // loader-wave form (HD <= 64, N <= 224; measured slower: 424 vs 341 us standalone at B/16 bs256,
-  // 274 vs 209 us at q_rows = 1, profiles/r02/attn_bwd_variants.txt)
-  static const int var = [] {
-    const char* e = getenv("VIT_ATTN_BWD_VARIANT");
-    return e ? atoi(e) : 2;
-  }();
-  if (var == 3 && HD <= 64 && NKT <= 14) return launch_bwd_p<HD, NKT>(qkv, dout, lse, dqkv, bias_partial, B, N, H, hd, scale, nq, s);
-  if (var == 0 && HD <= 64 && delta) {
-    if ((N + 15) / 16 == NKT) return launch_bwd2<HD, NKT>(qkv, dout, lse, delta, dqkv, bias_partial, B, N, H, hd,
-                                                         scale, nq, s);
-    return launch_bwd2<HD, NKT - 1>(qkv, dout, lse, delta, dqkv, bias_partial, B, N, H, hd, scale, nq, s);
-  }
-  static const int nw = [] {
-    const char* e = getenv("VIT_ATTN_BWD_NW");
-    return e ? atoi(e) : 4;
-  }();
-  if (nw == 8) return launch_bwd_nw<HD, NKT, 8>(qkv, dout, lse, dqkv, bias_partial, B, N, H, hd, scale, nq, s);
-  return launch_bwd_nw<HD, NKT, 4>(qkv, dout, lse, dqkv, bias_partial, B, N, H, hd, scale, nq, s);
 }
 
 #define VIT_NKT_CASES(X) X(2) X(4) X(6) X(8) X(10) X(12) X(14) X(16) X(18) X(20)
@@ -1649,12 +743,11 @@ hipError_t dispatch_fwd(int nkt, const bf16_t* qkv, bf16_t* o, float* lse, int B
   return hipErrorInvalidValue;
 }
 template <int HD>
-hipError_t dispatch_bwd(int nkt, const bf16_t* qkv, const bf16_t* o, const bf16_t* dout, const float* lse,
-                        bf16_t* dqkv, float* bias_partial, int B, int N, int H, int hd, float scale, int nq,
-                        float* delta, hipStream_t s) {
+hipError_t dispatch_bwd(int nkt, const bf16_t* qkv, const bf16_t* dout, const float* lse, bf16_t* dqkv,
+                        float* bias_partial, int B, int N, int H, int hd, float scale, int nq, hipStream_t s) {
   switch (nkt) {
 #define C(n) \
-  case n: return launch_bwd<HD, n>(qkv, o, dout, lse, dqkv, bias_partial, B, N, H, hd, scale, nq, delta, s);
+  case n: return launch_bwd<HD, n>(qkv, dout, lse, dqkv, bias_partial, B, N, H, hd, scale, nq, s);
     VIT_NKT_CASES(C)
 #undef C
   }
@@ -1757,19 +850,16 @@ extern "C" int vit_attention_bwd_ex(const void* qkv, const void* o, const void* 
     return vit::check_hip(e, "vit_attention_bwd (tiled) launch");
   }
   const int nkt = (int)((N + 31) / 32) * 2;
-  const bf16_t *q = (const bf16_t*)qkv, *ob = (const bf16_t*)o, *d = (const bf16_t*)dout;
+  const bf16_t *q = (const bf16_t*)qkv, *d = (const bf16_t*)dout;
   switch (image_width(hd)) {
     case 32:
-      e = dispatch_bwd<32>(nkt, q, ob, d, lse, (bf16_t*)dqkv, bias_partial, (int)B, (int)N, (int)H, (int)hd, scale, nq,
-                           workspace, s);
+      e = dispatch_bwd<32>(nkt, q, d, lse, (bf16_t*)dqkv, bias_partial, (int)B, (int)N, (int)H, (int)hd, scale, nq, s);
       break;
     case 64:
-      e = dispatch_bwd<64>(nkt, q, ob, d, lse, (bf16_t*)dqkv, bias_partial, (int)B, (int)N, (int)H, (int)hd, scale, nq,
-                           workspace, s);
+      e = dispatch_bwd<64>(nkt, q, d, lse, (bf16_t*)dqkv, bias_partial, (int)B, (int)N, (int)H, (int)hd, scale, nq, s);
       break;
     default:
-      e = dispatch_bwd<96>(nkt, q, ob, d, lse, (bf16_t*)dqkv, bias_partial, (int)B, (int)N, (int)H, (int)hd, scale, nq,
-                           workspace, s);
+      e = dispatch_bwd<96>(nkt, q, d, lse, (bf16_t*)dqkv, bias_partial, (int)B, (int)N, (int)H, (int)hd, scale, nq, s);
       break;
   }
   return vit::check_hip(e, "vit_attention_bwd launch");

@@ -149,6 +149,13 @@ __device__ __forceinline__ v4s lds_tr(const lds_t* p) {
 __device__ __forceinline__ v4f mfma16(const v4s& a, const v4s& b, const v4f& c) {
   return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, b, c, 0, 0, 0);
 }
+// x - x computed by the hardware: 0 for finite x, NaN for NaN / inf (the attention objects are built with
+// -fno-honor-nans, under which the compiler would fold x - x to 0)
+__device__ __forceinline__ float nan_of(float x) {
+  float r;
+  asm("v_sub_f32 %0, %1, %1" : "=v"(r) : "v"(x));
+  return r;
+}
 // max(a, b, c) in one v_max3_f32 (hipcc splits fmaxf chains into v_max_f32 pairs)
 __device__ __forceinline__ float max3f(float a, float b, float c) {
   float r;

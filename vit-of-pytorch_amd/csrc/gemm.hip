@@ -157,6 +157,11 @@ extern "C" int vit_gemm_bf16(const vit_gemm_args* a, vit_stream_t stream) {
       return e ? atoi(e) : 1;
     }();
     d.split_xcd = env_sx;
+    static const int env_prio = [] {
+      const char* e = getenv("VIT_GEMM_PRIO");
+      return e ? atoi(e) : 0;
+    }();
+    d.prio = env_prio;
   }
   if (a->col_partial) {
     VIT_CHECK_ARG(a->batch == 1 && a->split_k == 1 && d.vec && a->N % 8 == 0 &&

@@ -50,6 +50,7 @@ struct GemmDev {
   DropDev drop;        // dropout on the PATCH / BIAS_RESID_F32 / BIAS_GELU_DGELU output (thr 0 = off)
   int diag;            // diagnostics (VIT_GEMM_DIAG): 1 = skip the half-tile kernel's global stores, 2 = its epilogue
   int split_xcd;       // split-K grids: place each XCD's workgroups on one or two K-chunks (VIT_GEMM_SPLIT_XCD)
+  int prio;            // s_setprio(1) around the ping-pong kernels' MFMA clusters (VIT_GEMM_PRIO)
 };
 
 // Internal epilogue flag: the dropout variant of PATCH / BIAS_RESID_F32 / BIAS_GELU_DGELU (its own

@@ -920,6 +920,7 @@ __global__ void __launch_bounds__(512) gemm_pp_kernel(const GemmDev p) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   };
   auto compute = [&]() {
+    if (p.prio) __builtin_amdgcn_s_setprio(1);  // the MFMA cluster ahead of the partner group's issue
 #pragma unroll
     for (int kk = 0; kk < KK; ++kk)
 #pragma unroll
@@ -928,6 +929,7 @@ __global__ void __launch_bounds__(512) gemm_pp_kernel(const GemmDev p) {
         for (int jn = 0; jn < FN; ++jn)
           acc[i][jn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(v8bf, af[kk][i]),
                                                                __builtin_bit_cast(v8bf, bfr[kk][jn]), acc[i][jn], 0, 0, 0);
+    if (p.prio) __builtin_amdgcn_s_setprio(0);
   };
 
   // prologue: k-tiles 0 .. L-1 in flight, k-tile 0 landed
