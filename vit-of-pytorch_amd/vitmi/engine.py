@@ -240,6 +240,8 @@ class _BiasReducer:
         bias gradient of the layer feeding the residual stream) reduced on the bias stream."""
         part, key = self.buf("ln", self.a.lnparts)
         D = self.D
+        if self.eng._diag_skip_lnb and rows > 4096:  # DIAGNOSTIC timing ceiling (the per-layer calls)
+            return
         ops.layernorm_bwd(dy, lddy, x, ldx, mean, rstd, gamma, dx, lddx, part, rows, D, **kw)
         nblk = ops.layernorm_bwd_blocks(rows)
         self.reduce(key, lambda: ops.colsum3(part, nblk, D, 3 * D, self.a.colpart, dgamma_dbeta, dgamma_dbeta[D:],
@@ -316,6 +318,10 @@ class ViTEngine:
         # (off by default: on one MI355X the reductions then contend with the GEMMs for CUs, 7402 vs 7446
         # img/s in a same-box A/B)
         self._reduce_side = os.environ.get("VITMI_REDUCE_SIDE", "0") != "0"
+        # DIAGNOSTIC (timing ceilings only, wrong results): VITMI_DIAG_SKIP_LN=fwd skips the per-layer
+        # LayerNorm forward launches, =bwd the per-layer LayerNorm backward launches (profiles/r03)
+        _skip = os.environ.get("VITMI_DIAG_SKIP_LN", "")
+        self._diag_skip_lnf, self._diag_skip_lnb = "fwd" in _skip, "bwd" in _skip
         self.probe = None  # list: (start, end) HIP events around every fc1 forward GEMM launch
         self.probe_wgrad = None  # list: (start, end, flop, K) around every split-K weight-gradient GEMM launch
         # dropout (nn.Dropout of PositionEmbs / EncoderBlock / MlpBlock, reference src/model.py:19-20,
@@ -487,8 +493,9 @@ class ViTEngine:
         self._pruned = self.prune_last and self._drop is None
         for i in range(L):
             ln = lambda s: self.off(self.lname(i, s))
-            ops.layernorm_fwd(a.h[i], D, f[ln("norm1.weight"):], f[ln("norm1.bias"):], a.ln1[i], D, a.mu1[i],
-                              a.rs1[i], T, D)
+            if not self._diag_skip_lnf:
+                ops.layernorm_fwd(a.h[i], D, f[ln("norm1.weight"):], f[ln("norm1.bias"):], a.ln1[i], D, a.mu1[i],
+                                  a.rs1[i], T, D)
             ops.gemm(a.ln1[i], self.wqkvt[i], a.qkv[i], T, 3 * D, D, a_layout=K_CONTIG, b_layout=K_CONTIG, lda=D,
                      ldb=D, ldc=3 * D, epilogue=EPI_BIAS_BF16, bias=self.bqkv[i])
             last = self._pruned and i == L - 1
@@ -499,8 +506,9 @@ class ViTEngine:
             ops.gemm(a.o[i], self.woutt[i], a.hm[i], T, D, D, a_layout=K_CONTIG, b_layout=K_CONTIG,
                      lda=D, ldb=D, ldc=D, epilogue=EPI_BIAS_RESID_F32, bias=f[ln("attn.out.bias"):], aux=a.h[i],
                      ldaux=D, dropout=dd(1 + 3 * i))
-            ops.layernorm_fwd(a.hm[i], D, f[ln("norm2.weight"):], f[ln("norm2.bias"):], a.ln2[i], D, a.mu2[i],
-                              a.rs2[i], T, D)
+            if not self._diag_skip_lnf:
+                ops.layernorm_fwd(a.hm[i], D, f[ln("norm2.weight"):], f[ln("norm2.bias"):], a.ln2[i], D, a.mu2[i],
+                                  a.rs2[i], T, D)
             if self.probe is not None:
                 ev0 = torch.cuda.Event(enable_timing=True)
                 ev0.record()
