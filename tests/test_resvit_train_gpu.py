@@ -130,9 +130,11 @@ def test_three_training_steps_match_reference(gold, fused):
         assert abs(float(d) - float(gold[f"s{s}/d_loss"])) <= 2e-2 * float(gold[f"s{s}/d_loss"]), s
         # (after the first update the parameter trajectory itself carries bf16-level differences)
         assert rel(m.logits, gold[f"s{s}/logits"]) < (1e-2 if s == 0 else 2e-2), s
-        # which parameters got a gradient is the reference's (routing replayed)
+        # which parameters the update treated as having a gradient is the reference's (routing replayed;
+        # an approximator no token was routed to runs on every row but is gated off on the device)
+        used = opt.flat.used.cpu()
         for n in trainable:
-            assert opt.flat.used_host[opt.flat.index(named[n])] == bool(gold[f"s{s}/has_grad/{n}"]), (s, n)
+            assert bool(used[opt.flat.index(named[n])] > 0) == bool(gold[f"s{s}/has_grad/{n}"]), (s, n)
         # the clip's input norm (vitmi AdamW keeps {norm, coef} of its last clip, fused or not)
         assert float(opt.last_norm[0]) == pytest.approx(float(gold[f"s{s}/norm"]), rel=2e-2), s
     tot_upd = sum(float(np.square(gold["p3/" + n].astype(np.float64) - gold["p0/" + n]).sum()) for n in trainable)

@@ -17,12 +17,33 @@ None, then a fresh tensor from autograd) is folded back into the flat buffer by 
 from __future__ import annotations
 
 import math
+import weakref
 
 import torch
 
 from . import ops
 
 ALIGN = 64
+
+# parameter -> device bool scalar: this step's "did the parameter take part" for parameters whose
+# forward runs on every row and selects (Res-ViT's approximators): the flat optimizer ANDs it into the
+# used flags without a host synchronisation
+_GATES = {}  # id(parameter) -> (weakref to it, flag)
+
+
+def gate(params, flag):
+    if len(_GATES) > 4096:  # (gated parameters no flat optimizer collects)
+        _GATES.clear()
+    for p in params:
+        _GATES[id(p)] = (weakref.ref(p), flag)
+
+
+def _take_gate(p):
+    e = _GATES.get(id(p))
+    if e is None or e[0]() is not p:
+        return None
+    del _GATES[id(p)]
+    return e[1]
 
 
 def _rup(x, m):
@@ -68,6 +89,7 @@ class FlatParams:
         # two pinned staging copies of the host flags, each reused only after its last upload completed
         self._used_pin = [torch.zeros(self.nseg, pin_memory=True) for _ in range(2)]
         self._used_ev = [None, None]
+        self._gate_idx = {}
         self._used_k = 0
         self.on_grad = None  # callable(segment index) after each parameter's gradient accumulation
         self._hooks = [p.register_post_accumulate_grad_hook(self._mark) for p in ps]
@@ -120,6 +142,7 @@ class FlatParams:
         if self.used_reduced:
             self.used_reduced = False
             return self.used
+        gated = [(i, g) for i, g in ((i, _take_gate(p)) for i, p in enumerate(self.params)) if g is not None]
         k = self._used_k = self._used_k ^ 1
         if self._used_ev[k] is not None:
             self._used_ev[k].synchronize()
@@ -129,6 +152,13 @@ class FlatParams:
         ev = torch.cuda.Event()
         ev.record()
         self._used_ev[k] = ev
+        if gated:
+            key = tuple(i for i, _ in gated)
+            idx = self._gate_idx.get(key)
+            if idx is None:
+                idx = self._gate_idx[key] = torch.tensor(key, dtype=torch.int64).to(self.device)
+            flags = torch.stack([f.reshape(()) for _, f in gated]).to(self.used.dtype)
+            self.used[idx] = self.used[idx] * flags
         return self.used
 
     def sq_norm_parts(self):

@@ -30,6 +30,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from . import flat as _flat
 from . import functional as HF
 from . import resvit_fused as _fused
 from .model import GELU, CrossEntropyLoss, LayerNorm as _HipLayerNorm, Linear
@@ -63,6 +64,20 @@ class ModelArgs:
     dropout: float = 0.15
     num_patches: int = (224 // 16) * (224 // 16)
     device: str = "cuda"
+
+
+_CONST = {}
+
+
+def _const(values, device, dtype):
+    """small constant tensors (routing tables, bit weights) made on the device once: torch.tensor(list,
+    device=...) would copy from pageable host memory — a host-device synchronisation — every layer"""
+    key = (values, str(device), dtype)
+    t = _CONST.get(key)
+    if t is None:
+        t = torch.tensor(values, dtype=dtype).reshape(-1).to(device)
+        _CONST[key] = t
+    return t
 
 
 # ---- model_utils (reference res-vit/model_utils.py) ---------------------------------------------
@@ -136,7 +151,7 @@ class ActiveLoss(nn.Module):
 
     def forward(self, activation: torch.Tensor):
         ratio = activation[:, self.reserve_initials:, :].mean()
-        return F.mse_loss(ratio, torch.tensor(self.target, device=activation.device, dtype=ratio.dtype))
+        return F.mse_loss(ratio, ratio.new_full((), self.target))  # (a device fill: no host copy)
 
 
 # ---- modules --------------------------------------------------------------------------------------------
@@ -209,7 +224,7 @@ class RouterModule(nn.Module):
     def _router2indices(keep):
         """binary keep pattern over the block's layers -> index (first layer = most significant bit)."""
         n = keep.shape[-1]
-        w = torch.tensor([2.0 ** (n - 1 - i) for i in range(n)], device=keep.device).unsqueeze(-1)
+        w = _const((tuple(2.0 ** (n - 1 - i) for i in range(n)),), keep.device, torch.float32).view(n, 1)
         return torch.matmul(keep.float(), w)
 
     def forward(self, x):
@@ -340,15 +355,28 @@ class BlockPathApproximators(nn.Module):
 
     def forward(self, x, router_indices, LRA_mask):
         idx = router_indices.squeeze(-1)
-        for key in LRA_mask:
-            key_str = str(int(key))
-            if key_str not in self.approximators:
+        keys = [int(k) for k in (LRA_mask.tolist() if torch.is_tensor(LRA_mask) else LRA_mask)]
+        if torch.is_grad_enabled():
+            # training: every row through the approximator, the routed rows selected (the same values and
+            # gradients as the reference's boolean gather / scatter, which needs the row count on the host:
+            # a device sync per layer). Whether any row was routed to it — torch's AdamW skips an
+            # approximator without a gradient — is handed to the flat optimizer as a device flag.
+            for key in keys:
+                if str(key) not in self.approximators:
+                    continue
+                sel = (idx == key).unsqueeze(-1)
+                m = self.approximators[str(key)]
+                x = torch.where(sel, HF.add(m(x), x), x)
+                _flat.gate(m.parameters(), sel.any())
+            return x
+        for key in keys:
+            if str(key) not in self.approximators:
                 continue
-            sub = idx == int(key)
+            sub = idx == key
             if sub.any():
                 rows = x[sub]
                 x = x.clone()
-                x[sub] = HF.add(self.approximators[key_str](rows), rows)
+                x[sub] = HF.add(self.approximators[str(key)](rows), rows)
         return x
 
 
@@ -415,9 +443,9 @@ class TransformerBlock(nn.Module):
         router_indices = block_info[f"block_{bid}_router_indices"]
         w = block_routing[:, :, self.current_block_pos:self.current_block_pos + 1]
         assert LRA_mask is not None, "LRA_mask must be provided"
-        lra_lora = torch.tensor(LRA_mask[self.current_block_pos][0], device=x.device)
-        active = torch.isin(router_indices.long(),
-                            torch.tensor(LRA_mask[self.current_block_pos][1], device=x.device).long())
+        lra_lora = list(LRA_mask[self.current_block_pos][0])
+        active = torch.isin(router_indices.long(), _const(tuple(LRA_mask[self.current_block_pos][1]), x.device,
+                                                          torch.int64))
 
         if self.training:
             # teacher: every token, every layer. Its outputs reach the loss only through DistillLoss's
@@ -490,8 +518,8 @@ class Transformer(nn.Module):
         self.acts = []
         self.soft_routing_probs = []
         self.routing_maps = {}
-        d_loss = torch.tensor(0.0, device=device)
-        r_entropy = torch.tensor(0.0, device=device)
+        d_loss = torch.zeros((), device=device)
+        r_entropy = torch.zeros((), device=device)
         block_info = {}
         teacher_x, student_x = x, x
         for layer in self.layers:
@@ -524,9 +552,9 @@ class Transformer(nn.Module):
         c_loss = self.criterion(output, labels)
         if self.use_reslr:
             a_loss = (self.criterion_active(torch.cat(self.soft_routing_probs, dim=-1)) if self.soft_routing_probs
-                      else torch.tensor(0.0, device=device))
+                      else torch.zeros((), device=device))
             active_metric = self.criterion_active.metric(activation)
         else:
             a_loss, active_metric = None, None
-            r_entropy = torch.tensor(0.0, device=device)
+            r_entropy = torch.zeros((), device=device)
         return c_loss, a_loss, d_loss, r_entropy, active_metric
