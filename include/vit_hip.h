@@ -245,6 +245,25 @@ int vit_colsum(const void* in, int32_t in_bf16, int64_t rows, int64_t cols, int6
 int vit_colsum3(const void* in, int32_t in_bf16, int64_t rows, int64_t seg, int64_t ld, float* partial,
                 float* out0, float* out1, float* out2, int32_t accumulate, vit_stream_t stream);
 
+/* Up to VIT_COLSUM_BATCH_MAX f32 column reductions in ONE launch, no workspace: for each job,
+ * column c in [0, cols) of in[r*ld + c] summed over r in [0, rows) (a fixed order: deterministic) goes to
+ * out_k[c - k*seg], k = c / seg (seg = 0: out0[c]); NULL outputs are dropped; accumulate adds to them.
+ * Rows of 16-B multiples (cols % 4 == 0, ld % 4 == 0, `in` 16-B aligned) take vector loads. The engine's backward issues every bias-gradient
+ * reduction of one encoder layer (LayerNorm dgamma | dbeta | dx column sums, fc1 bias from the fc2-dgrad
+ * epilogue's tile partials, q|k|v biases from the attention backward's per-image partials) as one batch
+ * on the compute stream. (bias grads of src/model.py:61-63,108,114 under src/train.py:23 autograd) */
+#define VIT_COLSUM_BATCH_MAX 8
+typedef struct vit_colsum_job {
+  const float* in;
+  int64_t rows, cols, ld, seg;
+  float* out0;
+  float* out1;
+  float* out2;
+  int32_t accumulate;
+  int32_t reserved;
+} vit_colsum_job;
+int vit_colsum_batch(const vit_colsum_job* jobs, int32_t njobs, vit_stream_t stream);
+
 /* ------------------------------------------------------------------------------------------
  * Classifier head helpers (tiny, f32): C = op(A) op(B) (+ bias) (+ C if accumulate).
  * a_trans: A(m,k) = A[k*lda+m]; b_trans: B(k,n) = B[n*ldb+k].  nn.Linear src/model.py:194,210

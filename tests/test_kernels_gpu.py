@@ -504,3 +504,34 @@ def test_attention_varlen_ragged_queries(counts, Nkv, H, hd):
         vb = v[b * Nkv:(b + 1) * Nkv].float().view(Nkv, H, hd).transpose(0, 1)
         ref = (torch.softmax(qb @ kb.transpose(-1, -2) / math.sqrt(hd), -1) @ vb).transpose(0, 1).reshape(e - s, D)
         assert rel(o[s:e].float(), ref) < 1e-2, b
+
+
+def test_colsum_batch_exact_integers():
+    """vit_colsum_batch: several jobs in one launch (segments, dropped outputs, accumulate, unaligned
+    widths / strides) against torch sums; integer data, so every order of summation is exact"""
+    g = torch.Generator(device=DEV).manual_seed(5)
+    mk = lambda r, ld: torch.randint(-64, 65, (r, ld), device=DEV, generator=g).float()
+    a, b_, c, d = mk(512, 2304), mk(197, 3072), mk(3, 10), mk(130, 13)
+    o = [torch.full((768,), 7.0, device=DEV) for _ in range(3)]
+    ob = torch.zeros(3072, device=DEV)
+    oc = torch.zeros(10, device=DEV)
+    od = torch.full((12,), 1.0, device=DEV)
+    jobs = [(a, 512, 2304, 2304, 768, (o[0], None, o[2]), False),
+            (b_, 197, 3072, 3072, 0, (ob,), False),
+            (c, 3, 10, 10, 0, (oc,), False),
+            (d, 130, 12, 13, 0, (od,), True)]   # 12 of 13 columns, accumulated
+    ops.colsum_batch(jobs)
+    torch.cuda.synchronize()
+    s = a.sum(0)
+    assert torch.equal(o[0], s[:768]) and torch.equal(o[2], s[1536:])
+    assert torch.equal(o[1], torch.full((768,), 7.0, device=DEV))  # NULL segment: untouched
+    assert torch.equal(ob, b_.sum(0)) and torch.equal(oc, c.sum(0))
+    assert torch.equal(od, 1.0 + d[:, :12].sum(0))
+
+
+def test_colsum_batch_random_matches_torch():
+    x = torch.randn(394, 3072, device=DEV)
+    out = torch.empty(3072, device=DEV)
+    ops.colsum_batch([(x, 394, 3072, 3072, 0, (out,), False)])
+    torch.cuda.synchronize()
+    assert rel(out, x.double().sum(0).float()) < 1e-6

@@ -524,6 +524,116 @@ extern "C" int vit_colsum(const void* in, int32_t in_bf16, int64_t rows, int64_t
   VIT_LAUNCH_CHECK("vit_colsum");
 }
 
+// ---- batched column sums: every bias-gradient reduction of one encoder layer in one launch ----------
+// A workgroup owns 64 columns of one job: 16 column groups of 4 (one 16-B load per row) x 16 row lanes,
+// eight rows in flight per lane, then a fixed-order sum of the 16 lanes through LDS (deterministic).
+// The jobs ride in the kernel argument (no descriptor upload); workgroups [blk0_j, blk0_{j+1}) are job j's.
+namespace {
+struct ColsumJobDev {
+  const float* in;
+  float* out[3];
+  long ld;
+  int rows, cols, seg, acc, blk0;
+  int pad;  // 1: cols % 4 == 0, ld % 4 == 0 and 16-B aligned rows (vector loads)
+};
+struct ColsumBatchDev {
+  ColsumJobDev j[VIT_COLSUM_BATCH_MAX];
+  int n;
+};
+
+__global__ void __launch_bounds__(256) colsum_batch_kernel(const ColsumBatchDev bt) {
+  __shared__ float4 red[16][17];
+  const int bid = blockIdx.x;
+  int jx = 0;
+#pragma unroll
+  for (int k = 1; k < VIT_COLSUM_BATCH_MAX; ++k)
+    if (k < bt.n && bid >= bt.j[k].blk0) jx = k;
+  const ColsumJobDev& J = bt.j[jx];
+  const int c0 = (bid - J.blk0) * 64;
+  const int cg = threadIdx.x & 15, rl = threadIdx.x >> 4;
+  const int c = c0 + cg * 4;
+  float4 acc = {0.f, 0.f, 0.f, 0.f};
+  if (J.pad && c < J.cols) {  // 16-B rows: one float4 per row, eight rows in flight
+    const float* p = J.in + c;
+    const long ld = J.ld;
+    int r = rl;
+    for (; r + 112 < J.rows; r += 128) {
+      float4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const float4*>(p + (long)(r + 16 * u) * ld);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        acc.x += v[u].x; acc.y += v[u].y; acc.z += v[u].z; acc.w += v[u].w;
+      }
+    }
+    for (; r < J.rows; r += 16) {
+      const float4 v = *reinterpret_cast<const float4*>(p + (long)r * ld);
+      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
+  } else if (c < J.cols) {  // any width / stride (e.g. a 10-class head): scalar loads, same order
+    const float* p = J.in + c;
+    const int nc = J.cols - c < 4 ? J.cols - c : 4;
+    for (int r = rl; r < J.rows; r += 16) {
+      const float* q = p + (long)r * J.ld;
+      acc.x += q[0];
+      if (nc > 1) acc.y += q[1];
+      if (nc > 2) acc.z += q[2];
+      if (nc > 3) acc.w += q[3];
+    }
+  }
+  red[rl][cg] = acc;
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    const int g = threadIdx.x >> 2, k = threadIdx.x & 3;
+    const int col = c0 + threadIdx.x;
+    if (col < J.cols) {
+      float s = 0.f;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) s += reinterpret_cast<const float*>(&red[q][g])[k];
+      const int sg = J.seg > 0 ? col / J.seg : 0;
+      float* base = J.out[sg];
+      if (base) {
+        float* dst = base + (col - sg * J.seg);
+        *dst = J.acc ? *dst + s : s;
+      }
+    }
+  }
+}
+}  // namespace
+
+extern "C" int vit_colsum_batch(const vit_colsum_job* jobs, int32_t njobs, vit_stream_t stream) {
+  VIT_CHECK_ARG(jobs && njobs >= 1 && njobs <= VIT_COLSUM_BATCH_MAX, "vit_colsum_batch: njobs=%d outside [1, %d]",
+                (int)njobs, VIT_COLSUM_BATCH_MAX);
+  ColsumBatchDev bt{};
+  int blk = 0;
+  for (int k = 0; k < njobs; ++k) {
+    const vit_colsum_job& s = jobs[k];
+    VIT_CHECK_ARG(s.in && s.rows >= 1 && s.cols >= 1 && s.ld >= s.cols && s.rows <= 0x7fffffff &&
+                      s.cols <= 0x7fffffff,
+                  "vit_colsum_batch: job %d: bad shape (rows %lld, cols %lld, ld %lld)", k, (long long)s.rows,
+                  (long long)s.cols, (long long)s.ld);
+    VIT_CHECK_ARG(s.seg >= 0 && (s.seg == 0 || s.cols <= 3 * s.seg), "vit_colsum_batch: job %d: seg %lld", k,
+                  (long long)s.seg);
+    VIT_CHECK_ARG(s.out0 || s.out1 || s.out2, "vit_colsum_batch: job %d has no output", k);
+    ColsumJobDev& d = bt.j[k];
+    d.in = s.in;
+    d.out[0] = s.out0;
+    d.out[1] = s.out1;
+    d.out[2] = s.out2;
+    d.ld = (long)s.ld;
+    d.rows = (int)s.rows;
+    d.cols = (int)s.cols;
+    d.seg = (int)s.seg;
+    d.acc = s.accumulate ? 1 : 0;
+    d.blk0 = blk;
+    d.pad = (s.cols % 4 == 0 && s.ld % 4 == 0 && ((uintptr_t)s.in % 16) == 0) ? 1 : 0;
+    blk += (int)((s.cols + 63) / 64);
+  }
+  bt.n = njobs;
+  hipLaunchKernelGGL(colsum_batch_kernel, dim3(blk), dim3(256), 0, (hipStream_t)stream, bt);
+  return vit::check_hip(hipGetLastError(), "vit_colsum_batch");
+}
+
 extern "C" int vit_gemm_f32(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda, int32_t a_trans,
                             const float* B, int64_t ldb, int32_t b_trans, float* C, int64_t ldc, const float* bias,
                             int32_t accumulate, vit_stream_t stream) {

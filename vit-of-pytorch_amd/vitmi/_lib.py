@@ -17,7 +17,7 @@ c_i32 = ctypes.c_int32
 c_f32 = ctypes.c_float
 c_vp = ctypes.c_void_p
 
-ABI_VERSION = 6  # vit_abi_version() of the library these prototypes describe
+ABI_VERSION = 7  # vit_abi_version() of the library these prototypes describe
 
 # enum vit_layout / vit_epilogue (include/vit_hip.h)
 K_CONTIG, MN_CONTIG = 0, 1
@@ -45,6 +45,14 @@ class GemmArgs(ctypes.Structure):
         ("epilogue", c_i32), ("tile", c_i32), ("dropout", ctypes.POINTER(Dropout)),
     ]
 
+
+class ColsumJob(ctypes.Structure):
+    """struct vit_colsum_job (include/vit_hip.h)"""
+    _fields_ = [("inp", c_vp), ("rows", c_i64), ("cols", c_i64), ("ld", c_i64), ("seg", c_i64),
+                ("out0", c_vp), ("out1", c_vp), ("out2", c_vp), ("accumulate", c_i32), ("reserved", c_i32)]
+
+
+COLSUM_BATCH_MAX = 8  # VIT_COLSUM_BATCH_MAX
 
 # name -> (restype, argtypes)
 _SIGS = {
@@ -86,6 +94,7 @@ _SIGS = {
     "vit_pack_cols_batched": (c_i32, [c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp, c_i64, c_i64, c_i32, c_i64,
                                       c_vp]),
     "vit_transpose_f32_bf16": (c_i32, [c_vp, c_i64, c_i64, c_i64, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp]),
+    "vit_colsum_batch": (c_i32, [ctypes.POINTER(ColsumJob), c_i32, c_vp]),
     "vit_colsum3": (c_i32, [c_vp, c_i32, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_i32, c_vp]),
     "vit_im2col_f32": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp]),
     "vit_embed_fwd_f32": (c_i32, [c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp]),

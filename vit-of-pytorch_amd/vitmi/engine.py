@@ -33,9 +33,9 @@ def _rup(x, m):
     return (x + m - 1) // m * m
 
 
-# partial-sum buffers per kind of bias-gradient reduction (the compute stream waits for the reduction that
-# last read a buffer before writing it again; deeper rings let the bias stream lag further behind)
-_NBUF = max(2, int(os.environ.get("VITMI_BIAS_BUFS", "8")))
+# partial-sum buffers per kind of bias-gradient reduction: one encoder layer queues at most two of a kind
+# (LayerNorm 1 and 2) before its batch of reductions is issued (_BiasReducer)
+_NBUF = 2
 
 # workgroups a split-K weight gradient aims for (one per CU); VIT_WGRAD_TARGET for tuning sweeps
 _WGRAD_TARGET = int(os.environ.get("VIT_WGRAD_TARGET", "256"))
@@ -169,20 +169,13 @@ class _Acts:
         self.dlncls = z(b, D, dt=f)
         self.dlogits = z(b, cfg.num_classes, dt=f)
         self.row_stats = z(b, 3, dt=f)
-        # bias-gradient partial sums: written on the compute stream, reduced on the engine's bias stream
-        # (ViTEngine.backward), so each kind is double-buffered
-        self.lnpart = z(ops.layernorm_bwd_partial_rows(T), 3 * D, dt=f)
-        self.lnparts = [self.lnpart] + [z(ops.layernorm_bwd_partial_rows(T), 3 * D, dt=f) for _ in range(_NBUF - 1)]
-        # scratch of the column reductions, which all run on the engine's bias stream (_BiasReducer.reduce):
-        # nothing on the compute stream reads or writes it
-        self.colpart = z(ops.colsum_partial_rows(T), max(3 * D, M, cfg.num_classes), dt=f)
+        # bias-gradient partial sums, reduced a layer at a time (_BiasReducer: one vit_colsum_batch launch)
+        self.lnparts = [z(ops.layernorm_bwd_blocks(T), 3 * D, dt=f) for _ in range(_NBUF)]
         self.gelu_parts = [z(-(-T // 128), M, dt=f) for _ in range(_NBUF)]  # per-M-tile column sums of dU (fc1 bias)
-        self.gelu_part = self.gelu_parts[0]
         # column sums of dq|dk|dv (q/k/v bias grads): per image (LDS-resident attention, N <= 320) or per
         # image and 64-row block (K/V-tiled attention, longer sequences)
         self.attn_bias_rows = ops.attention_bias_rows(N)
         self.qkv_bparts = [z(b * self.attn_bias_rows, 3 * D, dt=f) for _ in range(_NBUF)]
-        self.qkv_bpart = self.qkv_bparts[0]
         nws = ops.attention_workspace_elems(b, N, H)
         self.attn_ws = z(nws, dt=f) if nws else None
         # last encoder layer on the cls rows only (ViTEngine.prune_last): compact operands, rows
@@ -195,60 +188,58 @@ class _Acts:
 
 
 class _BiasReducer:
-    """The bias-gradient column reductions of one backward, on the engine's bias stream.
+    """The bias-gradient column reductions of one backward, batched per encoder layer.
 
-    The compute stream writes per-block partial sums (LayerNorm backward: [nblk][dgamma | dbeta | dx];
-    the fc2-dgrad GEMM epilogue: per-tile dU column sums; the attention backward: per-image dq|dk|dv
-    sums); reduce() runs their vit_colsum / vit_colsum3 on the bias stream after everything issued so
-    far on the compute stream, and buf() hands out the two buffers of each kind alternately, making the
-    compute stream wait for the reduction that last read a buffer before it is written again."""
+    Producers on the compute stream write per-block partial sums (LayerNorm backward: [nblk][dgamma |
+    dbeta | dx]; the fc2-dgrad GEMM epilogue: per-tile dU column sums; the attention backward: per-image
+    dq|dk|dv sums); reduce() queues a column reduction of one of them and flush() issues every queued
+    reduction as ONE vit_colsum_batch launch on the compute stream, once per encoder layer (before its
+    gradient bucket is released). No event and no second stream sit between the step's kernels: every
+    event recorded on the compute stream idled it ~13 us, ~50 of them per B/16 step
+    (profiles/r03/step_timeline_v1.txt), and the reductions on a second stream held CU slots the GEMMs
+    wanted. The partial buffers rotate through rings of _NBUF (> the reductions queued between flushes),
+    all in compute-stream order."""
 
-    def __init__(self, eng, a, main):
-        if eng._bias_st is None:
-            eng._bias_st = torch.cuda.Stream(device=eng.dev)
-        self.stream = eng._bias_st
+    def __init__(self, eng, a):
         self.eng = eng
-        self.main = main
         self.a = a
         self.D = eng.cfg.emb_dim
-        self.done = {}   # (kind, index) -> event after the last reduction that read that buffer
         self.nxt = {}
+        self.queued = {}  # kind -> partial buffers of that kind written since the last flush
+        self.jobs = []
 
     def buf(self, kind, bufs):
+        n = self.queued.get(kind, 0)
+        if n == len(bufs):  # every buffer of the ring awaits its reduction
+            self.flush()
+            n = 0
+        self.queued[kind] = n + 1
         i = self.nxt.get(kind, 0)
         self.nxt[kind] = (i + 1) % len(bufs)
-        ev = self.done.pop((kind, i), None)
-        if ev is not None:  # (the stream about to write the buffer: compute, or the wgrad side stream)
-            torch.cuda.current_stream(self.main.device).wait_event(ev)
-        return bufs[i], (kind, i)
+        return bufs[i]
 
-    def reduce(self, key, fn):
-        """fn() on the bias stream after everything issued so far on the compute stream; fn may use
-        a.colpart (the bias stream's scratch: only reductions issued here touch it, in stream order)"""
-        ev = self.eng._event()
-        ev.record(torch.cuda.current_stream(self.main.device))  # after the producer, whichever stream it is on
-        self.stream.wait_event(ev)
-        with torch.cuda.stream(self.stream):
-            fn()
-        if key is not None:
-            d = self.eng._event()
-            d.record(self.stream)
-            self.done[key] = d
+    def reduce(self, part, rows, cols, ld, outs, seg=0):
+        """queue out_k[c - k*seg] = sum_r part[r*ld + c] (seg = 0: one output)"""
+        self.jobs.append((part, rows, cols, ld, seg, outs, False))
+        if len(self.jobs) == ops.COLSUM_BATCH_MAX:
+            self.flush()
+
+    def flush(self):
+        if self.jobs:
+            ops.colsum_batch(self.jobs)
+            self.jobs = []
+        self.queued.clear()
 
     def ln_bwd(self, dy, lddy, x, ldx, mean, rstd, gamma, dx, lddx, rows, dgamma_dbeta, dx_colsum, **kw):
         """LayerNorm backward on the compute stream; dgamma | dbeta (and the column sums of dx, the
-        bias gradient of the layer feeding the residual stream) reduced on the bias stream."""
-        part, key = self.buf("ln", self.a.lnparts)
+        bias gradient of the layer feeding the residual stream) queued as one reduction."""
+        part = self.buf("ln", self.a.lnparts)
         D = self.D
         if self.eng._diag_skip_lnb and rows > 4096:  # DIAGNOSTIC timing ceiling (the per-layer calls)
             return
         ops.layernorm_bwd(dy, lddy, x, ldx, mean, rstd, gamma, dx, lddx, part, rows, D, **kw)
-        nblk = ops.layernorm_bwd_blocks(rows)
-        self.reduce(key, lambda: ops.colsum3(part, nblk, D, 3 * D, self.a.colpart, dgamma_dbeta, dgamma_dbeta[D:],
-                                             dx_colsum))
-
-    def finish(self):
-        self.main.wait_stream(self.stream)
+        self.reduce(part, ops.layernorm_bwd_blocks(rows), 3 * D, 3 * D, (dgamma_dbeta, dgamma_dbeta[D:], dx_colsum),
+                    seg=D)
 
 
 class ViTEngine:
@@ -308,16 +299,7 @@ class ViTEngine:
         self.prune_last = os.environ.get("VITMI_PRUNE_LAST", "1") != "0"
         self._pruned = False
         self._side = None
-        # bias-gradient column reductions (vit_colsum / vit_colsum3 over per-block partial sums: ~100
-        # launches of ~5 us per B/16 step) run on their own stream: nothing on the compute stream waits
-        # for them, so they fill the tails of the GEMM launches instead of sitting between them
-        self._bias_st = None
         self._ev_pool, self._ev_next = [], 0
-        self._bias_cur = None  # the backward's _BiasReducer while it runs
-        self._ws_pair = [None, None]
-        # (off by default: on one MI355X the reductions then contend with the GEMMs for CUs, 7402 vs 7446
-        # img/s in a same-box A/B)
-        self._reduce_side = os.environ.get("VITMI_REDUCE_SIDE", "0") != "0"
         # DIAGNOSTIC (timing ceilings only, wrong results): VITMI_DIAG_SKIP_LN=fwd skips the per-layer
         # LayerNorm forward launches, =bwd the per-layer LayerNorm backward launches (profiles/r03)
         _skip = os.environ.get("VITMI_DIAG_SKIP_LN", "")
@@ -414,29 +396,11 @@ class ViTEngine:
             self._ws = torch.empty(numel, device=self.dev)
         return self._ws
 
-    def _side_workspace(self, bias, numel):
-        """one of two split-K slab buffers whose reductions run on the bias stream: the compute stream
-        waits for the reduction that last read the buffer before its GEMM overwrites it"""
-        buf, key = bias.buf("ws", self._ws_pair)
-        i = key[1]
-        if buf is None or buf.numel() < numel:
-            if buf is not None:
-                buf.record_stream(bias.stream)  # a pending reduction may still read the old one
-            buf = torch.empty(numel, device=self.dev)
-            self._ws_pair[i] = buf
-        return buf, key
-
     def _wgrad(self, A, lda, B, ldb, M, N, K, out, ldo, batch=1, b_bs=0, out_bs=0):
-        """out[z] (f32, [M][N], ld ldo) = sum_t A[t][m] B[t][n]  (both operands K-major).
-        During the backward the split-K slab reduction runs on the bias stream (nothing on the compute
-        stream reads a weight gradient; the optimizer and the DP buckets wait for that stream), so the
-        compute stream goes straight on to the next GEMM (VITMI_REDUCE_SIDE=0: inline)."""
+        """out[z] (f32, [M][N], ld ldo) = sum_t A[t][m] B[t][n]  (both operands K-major): split-K f32
+        slabs, then their fixed-order reduction (vit_splitk_reduce), both on the calling stream."""
         s = self._splitk(M, N, K, batch)
-        bias = self._bias_cur if self._reduce_side else None
-        if bias is not None:
-            ws, key = self._side_workspace(bias, batch * s * M * N)
-        else:
-            ws = self._workspace(batch * s * M * N)
+        ws = self._workspace(batch * s * M * N)
         if self.probe_wgrad is not None:  # bench.py's roofline kernel: events on the stream it runs on
             ev0 = torch.cuda.Event(enable_timing=True)
             ev0.record()
@@ -446,10 +410,7 @@ class ViTEngine:
             ev1 = torch.cuda.Event(enable_timing=True)
             ev1.record()
             self.probe_wgrad.append((ev0, ev1, 2.0 * M * N * K * batch, K))
-        if bias is not None:
-            bias.reduce(key, lambda: ops.splitk_reduce(ws, batch, s, M, N, out, ldo, out_bs))
-        else:
-            ops.splitk_reduce(ws, batch, s, M, N, out, ldo, out_bs)
+        ops.splitk_reduce(ws, batch, s, M, N, out, ldo, out_bs)
 
     # ---- forward -------------------------------------------------------------------------------
     def _dd(self, site, row_stride=1):
@@ -563,12 +524,12 @@ class ViTEngine:
         gv = lambda name: g[self.off(self.lname(i, name)):]
         bp = a.bp
         on_side(lambda: self._wgrad(a.c_dh, D, a.c_g, M, D, M, bp, gv("mlp.fc2.weight"), M))
-        gpart, gkey = bias.buf("gelu", a.gelu_parts)
+        gpart = bias.buf("gelu", a.gelu_parts)
         kw = dict(a_layout=K_CONTIG, b_layout=K_CONTIG, lda=D, ldb=D, ldc=M, epilogue=EPI_MUL_BF16, aux=a.c_gp,
                   ldaux=M, col_partial=gpart)
         ops.gemm(a.c_dh, self.w2t[i], a.c_dg, b, M, D, **kw)
         tiles_m = -(-b // ops.gemm_tile_rows(a.c_dh, self.w2t[i], a.c_dg, b, M, D, **kw))
-        bias.reduce(gkey, lambda: ops.colsum(gpart, tiles_m, M, M, a.colpart, gv("mlp.fc1.bias")))
+        bias.reduce(gpart, tiles_m, M, M, (gv("mlp.fc1.bias"),))
         on_side(lambda: self._wgrad(a.c_dg, M, a.c_ln2, D, M, D, bp, gv("mlp.fc1.weight"), D))
         ops.gemm(a.c_dg, self.w1t[i], a.c_dyln, b, D, M, a_layout=K_CONTIG, b_layout=K_CONTIG, lda=M, ldb=M, ldc=D,
                  epilogue=EPI_BF16)
@@ -685,21 +646,21 @@ class ViTEngine:
                 main.wait_event(ev)
 
         def fire(bucket):
+            bias.flush()  # the layer's bias gradients (and, with DP, the bucket's)
             if not hook:
                 return
             evs = []
-            for st in ((main, side) if overlap else (main,)) + (bias.stream,):
+            for st in ((main, side) if overlap else (main,)):
                 ev = self._event()
                 ev.record(st)
                 evs.append(ev)
             hook(g, *bucket, evs)
 
         self._ev_next = 0  # the event pool is reused from the start by every backward
-        bias = _BiasReducer(self, a, main)
-        self._bias_cur = bias
+        bias = _BiasReducer(self, a)
         # classifier head (f32): dWc = dl^T lncls, dbc = colsum(dl), dlncls = dl Wc
         ops.gemm_f32(C, D, b, dl, C, True, a.lncls, D, False, gv("classifier.weight"), D)
-        bias.reduce(None, lambda: ops.colsum(dl, b, C, C, a.colpart, gv("classifier.bias")))
+        bias.reduce(dl, b, C, C, (gv("classifier.bias"),))
         ops.gemm_f32(b, D, C, dl, C, False, f[self.off("classifier.weight"):], D, False, a.dlncls, D)
         # final LN backward on cls rows -> residual grad (zero elsewhere)
         # (its dx column sum is the last layer's fc2 bias gradient: only the cls rows are non-zero)
@@ -729,12 +690,12 @@ class ViTEngine:
                 release("dhb", wb)
                 dg = a.dg[li]
                 acquire("dg", li)
-                gpart, gkey = bias.buf("gelu", a.gelu_parts)
+                gpart = bias.buf("gelu", a.gelu_parts)
                 kw = dict(a_layout=K_CONTIG, b_layout=K_CONTIG, lda=D, ldb=D, ldc=M, epilogue=EPI_MUL_BF16, aux=a.gp[i],
                           ldaux=M, col_partial=gpart)
                 ops.gemm(dhb, self.w2t[i], dg, T, M, D, **kw)
                 tiles_m = -(-T // ops.gemm_tile_rows(dhb, self.w2t[i], dg, T, M, D, **kw))
-                bias.reduce(gkey, lambda: ops.colsum(gpart, tiles_m, M, M, a.colpart, gv(self.lname(i, "mlp.fc1.bias"))))
+                bias.reduce(gpart, tiles_m, M, M, (gv(self.lname(i, "mlp.fc1.bias")),))
                 on_side(lambda: self._wgrad(dg, M, a.ln2[i], D, M, D, a.Tp, gv(self.lname(i, "mlp.fc1.weight")), D))
                 release("dg", li)
                 ops.gemm(dg, self.w1t[i], a.dyln, T, D, M, a_layout=K_CONTIG, b_layout=K_CONTIG, lda=M,
@@ -752,14 +713,13 @@ class ViTEngine:
                          ldb=D, ldc=D, epilogue=EPI_BF16)
             dqkv = a.dqkv[li]
             acquire("dqkv", li)
-            qpart, qkey = bias.buf("qkv", a.qkv_bparts)
+            qpart = bias.buf("qkv", a.qkv_bparts)
             ops.attention_bwd(a.qkv[i], a.o[i], a.dO, a.lse[i], dqkv, b, N, H, hd, scale, bias_partial=qpart,
                               q_rows=1 if pruned and i == L - 1 else None, workspace=a.attn_ws)
             qo = ln("attn.query.weight")
             zs = ln("attn.key.weight") - qo
             qb = ln("attn.query.bias")
-            bias.reduce(qkey, lambda: ops.colsum3(qpart, b * a.attn_bias_rows, D, 3 * D, a.colpart, g[qb:], g[qb + zs:],
-                                                  g[qb + 2 * zs:]))
+            bias.reduce(qpart, b * a.attn_bias_rows, 3 * D, 3 * D, (g[qb:], g[qb + zs:], g[qb + 2 * zs:]), seg=D)
             on_side(lambda: self._wgrad(a.ln1[i], D, dqkv, 3 * D, D, D, a.Tp, g[qo:], D, batch=3, b_bs=D,
                                         out_bs=zs))
             release("dqkv", li)
@@ -779,8 +739,7 @@ class ViTEngine:
         ops.embed_grad(a.dh, b, N, D, gv("transformer.pos_embedding.pos_embedding"), gv("cls_token"),
                        gv("embedding.bias"), dropout=dd(0))
         fire(self.layout.buckets[-1])
-        bias.finish()
-        self._bias_cur = None
+        bias.flush()
         if overlap:
             main.wait_stream(side)
         return g

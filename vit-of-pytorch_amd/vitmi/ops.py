@@ -11,7 +11,7 @@ import ctypes
 import torch
 
 from . import _lib
-from ._lib import Dropout, GemmArgs, check
+from ._lib import COLSUM_BATCH_MAX, Dropout, GemmArgs, check
 
 BF16 = torch.bfloat16
 F32 = torch.float32
@@ -192,6 +192,18 @@ def colsum_partial_rows(rows):
 def colsum(inp, rows, cols, ld, partial, out, accumulate=False):
     check(lib().vit_colsum(_p(inp), int(inp.dtype == BF16), rows, cols, ld, _p(partial), _p(out), int(accumulate),
                            _stream()), "vit_colsum")
+
+
+def colsum_batch(jobs):
+    """jobs: [(inp f32, rows, cols, ld, seg, (out0, out1, out2), accumulate)], at most COLSUM_BATCH_MAX:
+    every column reduction in one launch (vit_colsum_batch)"""
+    arr = (_lib.ColsumJob * len(jobs))()
+    for k, (inp, rows, cols, ld, seg, outs, acc) in enumerate(jobs):
+        if inp.dtype != F32:
+            raise ValueError("colsum_batch: f32 inputs only")
+        o = list(outs) + [None] * (3 - len(outs))
+        arr[k] = _lib.ColsumJob(_p(inp), rows, cols, ld, seg, _p(o[0]), _p(o[1]), _p(o[2]), int(acc), 0)
+    check(lib().vit_colsum_batch(arr, len(jobs), _stream()), "vit_colsum_batch")
 
 
 def gemm_f32(M, N, K, A, lda, a_trans, B, ldb, b_trans, C, ldc, bias=None, accumulate=False):
