@@ -216,7 +216,8 @@ ATTN_CASES = [(2, 2, 2, 64, 0),  # (config C1: 2 tokens)
               (2, 197, 3, 64, 2), (2, 257, 2, 80, 2), (3, 17, 2, 32, 2), (1, 65, 2, 48, 2), (2, 33, 2, 96, 2),
               (2, 577, 3, 64, 0), (1, 730, 2, 80, 0), (1, 321, 2, 64, 0),
               # more (image, head) items than CUs: the persistent backward's workgroups walk several items
-              (24, 197, 12, 64, 0), (23, 50, 12, 64, 0)]
+              # (its Q / dO slots double as bias scratch: tiny N exercises the padded slot size)
+              (24, 197, 12, 64, 0), (23, 50, 12, 64, 0), (32, 2, 12, 64, 0), (30, 17, 12, 32, 0)]
 
 
 @pytest.mark.parametrize("B,N,H,hd,path", ATTN_CASES)
@@ -250,12 +251,12 @@ def test_attention(B, N, H, hd, path):
     assert rel(mv, gv) < 2e-2
 
 
-@pytest.mark.parametrize("N", [2, 17, 197])
-def test_attention_backward_saturated_scores_finite(N):
+@pytest.mark.parametrize("N,B", [(2, 2), (17, 2), (197, 2), (2, 32)])
+def test_attention_backward_saturated_scores_finite(N, B):
     """scores of |s| ~ 1e3 (the reference's std-1 init, config C1's 2 tokens): the LSE of a query can be far
     below 0, and the zero-padded keys of its last computed key tile must still get P = 0, not 2^-LSE = inf
-    (inf * dP 0 = NaN)"""
-    B, H, hd = 2, 2, 64
+    (inf * dP 0 = NaN); B = 32 x H = 12 puts several items on each workgroup of the persistent backward"""
+    H, hd = (2, 64) if B == 2 else (12, 64)
     D = H * hd
     g = torch.Generator(device=DEV).manual_seed(1)
     qkv = (torch.randn(B * N, 3 * D, device=DEV, generator=g) * 8.0).bfloat16()
@@ -267,8 +268,9 @@ def test_attention_backward_saturated_scores_finite(N):
     assert float(lse.min()) < -100.0
     dout = torch.randn(B * N, D, device=DEV).bfloat16()
     dqkv = torch.zeros(B * N, 3 * D, device=DEV, dtype=torch.bfloat16)
-    ops.attention_bwd(qkv, o, dout, lse, dqkv, B, N, H, hd, 1.0 / math.sqrt(hd))
-    assert torch.isfinite(o.float()).all() and torch.isfinite(dqkv.float()).all()
+    bp = torch.zeros(B, 3 * D, device=DEV)
+    ops.attention_bwd(qkv, o, dout, lse, dqkv, B, N, H, hd, 1.0 / math.sqrt(hd), bias_partial=bp)
+    assert torch.isfinite(o.float()).all() and torch.isfinite(dqkv.float()).all() and torch.isfinite(bp).all()
 
 
 @pytest.mark.parametrize("N,path", [(197, 0), (197, 2), (257, 0), (2, 0), (17, 0)])

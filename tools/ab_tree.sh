@@ -5,6 +5,6 @@ set -e
 REV=${1:-HEAD}
 cd "$(dirname "$0")/.."
 rm -rf abase && mkdir abase
-git archive "$REV" bench.py __graft_entry__.py include oracle vit-of-pytorch_amd | tar -x -C abase
+git archive "$REV" bench.py __graft_entry__.py include oracle tools vit-of-pytorch_amd | tar -x -C abase
 make -C abase/vit-of-pytorch_amd -j8 > /tmp/abase_build.log 2>&1
 echo "abase: $(git rev-parse --short $REV)"

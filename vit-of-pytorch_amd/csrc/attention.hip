@@ -781,6 +781,9 @@ hipError_t vit_attn_tiled_fwd(const void* qkv, void* o, float* lse, int B, int N
                               hipStream_t s);
 hipError_t vit_attn_tiled_bwd(const void* qkv, const void* dout, const float* lse, float* delta, void* dqkv,
                               float* bias_partial, int B, int N, int H, int hd, float scale, int nq, hipStream_t s);
+size_t vit_attn_bwd_pers_lds(int N, int hd);
+hipError_t vit_attn_bwd_pers(const void* qkv, const void* dout, const float* lse, void* dqkv, float* bias_partial,
+                             int B, int N, int H, int hd, float scale, int nq, hipStream_t s);
 
 extern "C" int64_t vit_attention_bias_rows(int64_t N, int32_t path) {
   return resolve_path(path, N) == 1 ? 1 : (N + 63) / 64;
@@ -848,6 +851,10 @@ extern "C" int vit_attention_bwd_ex(const void* qkv, const void* o, const void* 
     e = vit_attn_tiled_bwd(qkv, dout, lse, workspace, dqkv, bias_partial, (int)B, (int)N, (int)H, (int)hd, scale, nq,
                            s);
     return vit::check_hip(e, "vit_attention_bwd (tiled) launch");
+  }
+  if (vit_attn_bwd_pers_lds((int)N, (int)hd) > 0) {  // persistent single-load kernel (attention_bwd.hip)
+    e = vit_attn_bwd_pers(qkv, dout, lse, dqkv, bias_partial, (int)B, (int)N, (int)H, (int)hd, scale, nq, s);
+    return vit::check_hip(e, "vit_attention_bwd (persistent) launch");
   }
   const int nkt = (int)((N + 31) / 32) * 2;
   const bf16_t *q = (const bf16_t*)qkv, *d = (const bf16_t*)dout;

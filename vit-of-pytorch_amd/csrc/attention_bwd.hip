@@ -1,0 +1,596 @@
+// Attention backward, persistent single-load form (head widths up to 64, N up to 208 at hd 64).
+//
+// Replaces the autograd backward of SelfAttention's core (reference src/model.py:90-97).
+//
+// One 8-wave workgroup per CU walks (image, head) items. Every byte of Q, K, V, dO and lse leaves HBM
+// once per item, always by LDS-DMA (buffer_load ... lds) issued one phase ahead, and dQ | dK | dV are
+// written once:
+//   Q, dO, lse  into the idle one of two Q / dO slots at the start of the previous item;
+//   K, V        into the single K / V slot once the previous item's stage 2 has its K / V rows in registers.
+// Nothing is prefetched into registers, so no load is pending across the register-heavy stages (an
+// in-flight register load under full register pressure made hipcc split its live range and wait vmcnt(0)
+// inside stage 2's loop).
+// Per item:
+//   stage 1  each wave owns 16-query strips: S^T = K Q^T and dP^T = V dO^T for ALL keys stay in
+//            registers, so delta_q = sum_j P_qj dP_qj is exact (not rowsum(dO * O) of the bf16 O: see
+//            attention.hip), dS = P (dP - delta) and dQ = dS K come out of the same pass (K^T by
+//            ds_read_b64_tr_b16);
+//   stage 2  each wave owns one pair of 16-key tiles, K / V rows taken from the images into registers;
+//            S, dP recomputed against the Q / dO images, dV = P^T dO, dK = dS^T Q accumulated in
+//            registers (no atomics: deterministic);
+//   bias     per-wave column sums of dQ, dK, dV -> a fixed-order sum over the waves through the item's
+//            (now dead) Q / dO slot -> bias_partial[b][3 D] (q|k|v bias-gradient partials, one row per image).
+// LDS: K / V images, Q / dO slot 0, Q / dO slot 1 ([NP][HD] bf16, NP = 16 * ceil(N / 16), 16-B-chunk XOR
+// swizzle of attn_common.h), lse slot 0 / 1 and delta rows: 6 * NP * HD * 2 + 12 * NP bytes (162 KB at
+// N = 197, hd 64). Separate LDS objects per slot and a slot-templated item body: hipcc then proves that an
+// in-flight LDS-DMA into one slot cannot alias the accesses to another and inserts no vmcnt wait for it.
+#include "attn_common.h"
+#include <type_traits>
+
+namespace {
+using namespace vit_attn;
+
+constexpr int PB_NW = 8;
+
+#ifdef VIT_ATTN_STAMPS
+// DIAGNOSTIC build only (make ... EXTRA=-DVIT_ATTN_STAMPS): s_memtime stamps of workgroup 0's waves 0 and 7,
+// first 4 items, 8 points per item; read back with vit_attn_stamps()
+__device__ unsigned long long g_attn_stamps[2][4][8];
+#define STAMP(k)                                                                                            \
+  do {                                                                                                      \
+    if (blockIdx.x == 0 && (wave == 0 || wave == 7) && it < 4) {                                            \
+      unsigned long long t_;                                                                                \
+      __builtin_amdgcn_sched_barrier(0);                                                                    \
+      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");                            \
+      __builtin_amdgcn_sched_barrier(0);                                                                    \
+      if (lane == 0) g_attn_stamps[wave == 7][it][k] = t_;                                                  \
+    }                                                                                                       \
+  } while (0)
+#else
+#define STAMP(k) \
+  do {           \
+  } while (0)
+#endif
+
+// a pointer every lane holds the same value of, moved to SGPRs (the buffer descriptor of an LDS-DMA must be
+// wave-uniform: from VGPRs hipcc wraps each DMA in a waterfall loop)
+template <class T>
+__device__ __forceinline__ T* uniform_ptr(T* p) {
+  const unsigned long long u = (unsigned long long)p;
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)u), hi = __builtin_amdgcn_readfirstlane((unsigned)(u >> 32));
+  return (T*)(((unsigned long long)hi << 32) | lo);
+}
+
+// sum over the 16 lanes of a DPP row (lanes sharing lane >> 4), fixed order (inclusive prefix by row_shr
+// 1, 2, 4, 8): the total lands in lane 15 of the row
+__device__ __forceinline__ float row_sum16_to15(float v) {
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x111, 0xf, 0xf, true));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x112, 0xf, 0xf, true));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x114, 0xf, 0xf, true));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x118, 0xf, 0xf, true));
+  return v;
+}
+
+// Workgroup barrier for LDS hand-offs only. __syncthreads() also waits vmcnt(0) (global-store visibility),
+// which would stall every wave on the LDS-DMA prefetches in flight; LDS-DMA completion is handled explicitly
+// (each wave drains its own vmcnt before the item-start barrier).
+__device__ __forceinline__ void lds_barrier() {
+  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_barrier" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+// Gather the row totals left in lane 15 of each DPP row by row_sum16_to15 for 16 values v[0..15] into one
+// register: lane 16 g + k receives v[k]'s total of row g. row_ror:n gives lane j the row's lane (j - n) mod 16,
+// so n = k + 1 brings lane 15 to lane k.
+template <int K>
+__device__ __forceinline__ void gather_step(const float (&v)[16], int i, float& out) {
+  if constexpr (K < 16) {
+    float m = v[K];
+    if constexpr (K < 15)
+      m = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v[K]), 0x121 + K, 0xf, 0xf, false));
+    out = i == K ? m : out;
+    gather_step<K + 1>(v, i, out);
+  }
+}
+__device__ __forceinline__ float gather_row_totals(const float (&v)[16], int i) {
+  float out = 0.f;
+  gather_step<0>(v, i, out);
+  return out;
+}
+
+// the lane index, recomputed where it is used (opaque to CSE): lane-derived offsets of a later phase are
+// rebuilt from it instead of being kept live (and spilled) across the register-heavy stage before it
+__device__ __forceinline__ int lane_now() {
+  int l;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+  return l;
+}
+
+// Buffer descriptor over rows [r0, N) of a [rows][stride] bf16 block based at `base` (row 0), up to column hd of
+// row N - 1: loads past it read zero, stores past it are dropped, so padded rows need no per-lane branch.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rows_rsrc(const bf16_t* base, long stride, int r0, int N, int hd) {
+  const long rec = ((long)(N - 1 - r0) * stride + hd) * 2;
+  return make_rsrc(uniform_ptr(base + (long)r0 * stride), r0 < N && rec > 0 ? (uint32_t)rec : 0u);
+}
+__device__ __forceinline__ void st_b64(__amdgpu_buffer_rsrc_t r, int off, const uint2& v) {
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, v), r, off, 0, 0);
+}
+
+// LDS-DMA of image rows [0, rows) (rows >= N land as zeros) of two [N][stride] bf16 blocks (A, B: 1-KiB pieces, 64 lanes x 16 B, contiguous
+// in LDS) into their swizzled [NP][HD] LDS images; pieces are dealt round-robin to the waves from `first`.
+// Each piece gets its own (scalar) descriptor based at its first row, so every piece uses the same one
+// lane-offset VGPR (per-piece offsets get spilled, and hipcc then waits vmcnt(0) on each reload, i.e. on
+// every earlier piece); the record count clips rows past N and columns past hd of row N - 1 to zero.
+template <int HD>
+__device__ __forceinline__ void dma_pair(lds_t* imga, const bf16_t* basea, long stridea, lds_t* imgb,
+                                         const bf16_t* baseb, long strideb, int rows, int N, int hd, int first,
+                                         int wave, int lane) {
+  constexpr int RPP = 1024 / (HD * 2);  // image rows per piece
+  constexpr int CPR = HD / 8;           // 16-B chunks per row
+  static_assert(RPP % 8 == 0, "the swizzle period divides a piece");
+  const int npc = (rows + RPP - 1) / RPP;  // pieces per image
+  const bf16_t* ba = uniform_ptr(basea);
+  const bf16_t* bb = uniform_ptr(baseb);
+  const int lr = lane / CPR, pc = lane % CPR;
+  const int ch = pc ^ aswz<HD>(lr);  // row bits 1..2 of q * RPP + lr are those of lr
+  const bool colok = ch * 8 < hd;
+  const int offa = colok ? (int)(lr * stridea * 2 + ch * 16) : 0x40000000;
+  const int offb = colok ? (int)(lr * strideb * 2 + ch * 16) : 0x40000000;
+  int p = wave - first;
+  if (p < 0) p += PB_NW;
+  for (; p < 2 * npc; p += PB_NW) {
+    const bool isb = p >= npc;
+    const int q = isb ? p - npc : p;
+    const long stride = isb ? strideb : stridea;
+    const long shift = (long)q * RPP * stride;  // elements
+    const long rec = (((long)(N - 1) * stride + hd) - shift) * 2;
+    const __amdgpu_buffer_rsrc_t r = make_rsrc((isb ? bb : ba) + shift, rec > 0 ? (uint32_t)rec : 0u);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (isb ? imgb : imga) + q * 1024, 16, isb ? offb : offa, 0, 0, 0);
+  }
+}
+
+// LDS-DMA of n (<= NP) consecutive floats (an item's lse row) into dst; past n reads zero
+template <int NP>
+__device__ __forceinline__ void dma_floats(lds_t* dst, const float* src, int n, int wave, int lane) {
+  constexpr int PCS = (NP * 4 + 1023) / 1024;
+  const __amdgpu_buffer_rsrc_t r = make_rsrc(uniform_ptr(src), (uint32_t)n * 4);
+  if (wave < PCS) __builtin_amdgcn_raw_ptr_buffer_load_lds(r, dst + wave * 1024, 16, wave * 1024 + lane * 16, 0, 0, 0);
+}
+
+template <int HD, int NKT>
+__global__ void __launch_bounds__(PB_NW * 64, 1) attn_bwd_pers_kernel(const bf16_t* __restrict__ qkv,
+                                                                     const bf16_t* __restrict__ dout,
+                                                                     const float* __restrict__ lse,
+                                                                     bf16_t* __restrict__ dqkv,
+                                                                     float* __restrict__ bias_partial, int nitems, int N,
+                                                                     int H, int hd, float scale, int nq) {
+  constexpr int NW = PB_NW;
+  constexpr int NP = NKT * 16;
+  constexpr int IMG = NP * HD * 2;
+  constexpr int KK = HD / 32;
+  constexpr int T = ImgLane<HD>::TILE;
+  constexpr int LSEB = (NP * 4 + 1023) / 1024 * 1024;  // lse slot bytes (whole DMA pieces)
+  // a Q / dO slot is also the item's bias-sum scratch ([NW][3][HD] floats) once stage 2 is done
+  constexpr int QOB = 2 * IMG > NW * 3 * HD * 4 ? 2 * IMG : NW * 3 * HD * 4;
+  __shared__ __attribute__((aligned(16))) char kv_s[2 * IMG];  // K | V images
+  __shared__ __attribute__((aligned(16))) char qo0_s[QOB];     // Q | dO images, slot 0
+  __shared__ __attribute__((aligned(16))) char qo1_s[QOB];     // Q | dO images, slot 1
+  __shared__ __attribute__((aligned(16))) char ls0_s[LSEB];      // lse rows (natural log), slot 0
+  __shared__ __attribute__((aligned(16))) char ls1_s[LSEB];      // lse rows, slot 1
+  __shared__ __attribute__((aligned(16))) float dlt_s[NP];       // delta rows of the item
+  lds_t* const Ki = (lds_t*)kv_s;
+  lds_t* const Vi = Ki + IMG;
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int g = lane >> 4, i = lane & 15;
+  const ImgLane<HD> L(lane);
+  const int D = H * hd;
+  const long rs = 3L * D;
+  const float c = scale * LOG2E;
+  const int npair = (N + 31) / 32;                   // pairs of 16-row tiles holding valid rows
+  const bool last_half = (2 * npair - 1) * 16 >= N;  // the last pair's second tile is wholly padding
+  // queries [0, nq) carry a gradient (nq < N: the last layer's cls rows); their 32-row pairs are processed
+  // and only their Q / dO rows are loaded
+  const int nqa = min(N, (nq + 31) / 32 * 32);
+  const int npair_q = (nqa + 31) / 32;
+  const int nqt = (N + 15) / 16;  // == NKT
+  const int qrows = min(NP, 32 * npair_q);
+  const int offs = (int)(i * rs * 2) + g * 8;  // 8-B output chunk: row i, columns 16 dt + 4 g ..
+
+  int item = blockIdx.x;
+  if (item >= nitems) return;
+  auto qkv_of = [&](int it_) { return qkv + (long)(it_ / H) * N * rs + (long)(it_ % H) * hd; };
+  auto dout_of = [&](int it_) { return dout + (long)(it_ / H) * N * D + (long)(it_ % H) * hd; };
+  // Q / dO / lse of item it_ into a Q / dO slot (waves 0.. take the pieces; the lse piece goes to the last)
+  auto dma_qo = [&](lds_t* qo, lds_t* ls, int it_) {
+    dma_floats<NP>(ls, lse + (long)it_ * N, N, wave, lane);
+    dma_pair<HD>(qo, qkv_of(it_), rs, qo + IMG, dout_of(it_), D, qrows, N, hd, 0, wave, lane);
+  };
+  auto dma_kv = [&](int it_) {
+    const bf16_t* bq = qkv_of(it_);
+    // all NP rows: the padding rows N.. of the images must be zeros (the last key tile reads them)
+    dma_pair<HD>(Ki, bq + D, rs, Vi, bq + 2 * D, rs, NP, N, hd, 3, wave, lane);
+  };
+  // ---- prologue: everything of the first item
+  dma_kv(item);
+  dma_qo((lds_t*)qo0_s, (lds_t*)ls0_s, item);
+
+  int it = 0;
+  auto body = [&](auto slot) {
+    constexpr int SLOT = decltype(slot)::value;
+    lds_t* const Qi = (lds_t*)(SLOT ? qo1_s : qo0_s);
+    lds_t* const Oi = Qi + IMG;
+    const float* const lse_s = reinterpret_cast<const float*>(SLOT ? ls1_s : ls0_s);
+    lds_t* const Qn = (lds_t*)(SLOT ? qo0_s : qo1_s);
+    lds_t* const Ln = (lds_t*)(SLOT ? ls0_s : ls1_s);
+    const int b = item / H, h = item % H;
+    bf16_t* const dqb = dqkv + (long)b * N * rs + (long)h * hd;
+    const int next = item + gridDim.x;
+
+    // (a) this item's K / V, Q / dO, lse landed (every wave drains its own DMAs, then the barrier), and
+    // every wave is past the previous item's stage 2 / bias sums (the last readers of the other slot)
+    STAMP(0);
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0) (a builtin: hipcc's own wait tracking sees it)
+    STAMP(1);
+    lds_barrier();
+    STAMP(2);
+    // (b) the next item's Q / dO / lse into the other slot
+    if (next < nitems) dma_qo(Qn, Ln, next);
+
+    // ---- stage 1: delta, dS, dQ per 16-query strip ----
+    // the wave's dQ column sums, packed in one register: lane 16 g + 4 dt + r holds column 16 dt + 4 g + r
+    float bq1 = 0.f;
+    for (int qt = wave; qt < nqt; qt += NW) {
+      const int q = qt * 16 + i;
+      const __amdgpu_buffer_rsrc_t rdq = rows_rsrc(dqb, rs, qt * 16, N, hd);
+      if (qt * 16 >= nqa) {  // no gradient reaches these queries: dQ = 0 (delta unused: stage 2 skips them)
+#pragma unroll
+        for (int dt = 0; dt < HD / 16; ++dt)
+          if (dt * 16 < hd) st_b64(rdq, offs + dt * 32, uint2{0u, 0u});
+        continue;
+      }
+      v8bf qf[KK], df[KK];
+#pragma unroll
+      for (int kk = 0; kk < KK; ++kk) {
+        qf[kk] = __builtin_bit_cast(v8bf, lds_ld<v8s>(Qi + qt * T + L.row[kk]));
+        df[kk] = __builtin_bit_cast(v8bf, lds_ld<v8s>(Oi + qt * T + L.row[kk]));
+      }
+      const float ls = q < N ? lse_s[q] * LOG2E : 1e30f;  // padded queries: P = 2^-1e30 = 0
+      v4f P[NKT], DP[NKT];
+      float dlr[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kt = 0; kt < NKT; ++kt) {
+        v4f st = {0.f, 0.f, 0.f, 0.f}, dpt = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kk = 0; kk < KK; ++kk) {
+          st = mfma(__builtin_bit_cast(v8bf, lds_ld<v8s>(Ki + kt * T + L.row[kk])), qf[kk], st);
+          dpt = mfma(__builtin_bit_cast(v8bf, lds_ld<v8s>(Vi + kt * T + L.row[kk])), df[kk], dpt);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float e = st[r] * c - ls;
+          float pv;
+          if (kt == NKT - 1) {
+            // the last tile may hold padded keys (zero K / V rows: dP = 0, nothing added to delta, and
+            // their dS meets zero K rows in dQ): only the exponent is clamped so that P stays finite
+            // whatever the query's LSE; nan_of keeps a NaN score visible (v_min returns the non-NaN operand)
+            pv = ex2(fminf(e, 0.f) + nan_of(e));
+          } else {
+            pv = ex2(e);
+          }
+          P[kt][r] = pv;
+          dlr[r] += pv * dpt[r];
+        }
+        DP[kt] = dpt;
+      }
+      float dl = (dlr[0] + dlr[1]) + (dlr[2] + dlr[3]);
+      dl += __shfl_xor(dl, 16, 64);
+      dl += __shfl_xor(dl, 32, 64);
+      if (q >= N) dl = 0.f;
+      if (g == 0) dlt_s[q] = dl;
+      v4f dq[HD / 16];
+#pragma unroll
+      for (int dt = 0; dt < HD / 16; ++dt) dq[dt] = v4f{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < NKT / 2; ++ks) {
+        v4f d0, d1;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          d0[r] = P[2 * ks][r] * (DP[2 * ks][r] - dl);
+          d1[r] = P[2 * ks + 1][r] * (DP[2 * ks + 1][r] - dl);
+        }
+        const v8bf bD = pack8(d0, d1);
+#pragma unroll
+        for (int dt = 0; dt < HD / 16; ++dt) {
+          v8s kt8;
+          kt8.lo = lds_tr(Ki + 2 * ks * T + L.tr[dt]);
+          kt8.hi = lds_tr(Ki + (2 * ks + 1) * T + L.tr[dt]);
+          dq[dt] = mfma(__builtin_bit_cast(v8bf, kt8), bD, dq[dt]);
+        }
+      }
+      if constexpr (NKT % 2 == 1) {
+        v4f d0;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) d0[r] = P[NKT - 1][r] * (DP[NKT - 1][r] - dl);
+        const v4s bD = pack4(d0);
+#pragma unroll
+        for (int dt = 0; dt < HD / 16; ++dt) dq[dt] = mfma16(lds_tr(Ki + (NKT - 1) * T + L.tr[dt]), bD, dq[dt]);
+      }
+      {
+        uint2 pk[HD / 16];
+#pragma unroll
+        for (int dt = 0; dt < HD / 16; ++dt) pk[dt] = pack4bf(dq[dt], scale);
+#pragma unroll
+        for (int dt = 0; dt < HD / 16; ++dt)
+          if (dt * 16 < hd) st_b64(rdq, offs + dt * 32, pk[dt]);
+#pragma unroll
+        for (int dt = 0; dt < HD / 16; ++dt) keep_live2(pk[dt]);
+      }
+      if (bias_partial) {  // the strip's column sums (padded queries: dS = 0)
+        float t16[16];
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) t16[dt * 4 + r] = dt < HD / 16 ? row_sum16_to15(dq[dt][r]) : 0.f;
+        bq1 += gather_row_totals(t16, i);
+      }
+    }
+    STAMP(3);
+    lds_barrier();  // delta complete
+    STAMP(4);
+
+    // ---- stage 2: dK, dV per pair of 16-key tiles ----
+    const ImgLane<HD> L2(lane_now());  // (rebuilt: see lane_now)
+    const int kp = wave;
+    v8bf kf[2][KK], vf[2][KK];
+    const bool have_pair = kp < npair;
+    const bool t1_valid = (2 * kp + 1) * 16 < N;  // the pair's second tile holds a valid key
+    if (have_pair) {
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int kk = 0; kk < KK; ++kk) {
+          const bool ok = t == 0 || t1_valid;
+          kf[t][kk] = ok ? __builtin_bit_cast(v8bf, lds_ld<v8s>(Ki + (2 * kp + t) * T + L2.row[kk])) : v8bf{};
+          vf[t][kk] = ok ? __builtin_bit_cast(v8bf, lds_ld<v8s>(Vi + (2 * kp + t) * T + L2.row[kk])) : v8bf{};
+        }
+    }
+    // every wave has its K / V rows: the next item's K / V into the images, landing during stage 2
+    lds_barrier();  // (its lgkmcnt(0): this wave's K / V reads are back)
+    if (next < nitems) dma_kv(next);
+    STAMP(7);
+    float bk4[HD / 16][4], bv4[HD / 16][4];
+#pragma unroll
+    for (int dt = 0; dt < HD / 16; ++dt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) bk4[dt][r] = bv4[dt][r] = 0.f;
+    if (have_pair) {
+      v4f dv[2][HD / 16], dk[2][HD / 16];
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int dt = 0; dt < HD / 16; ++dt) dv[t][dt] = dk[t][dt] = v4f{0.f, 0.f, 0.f, 0.f};
+      const bool kv0 = (2 * kp) * 16 + i < N, kv1 = (2 * kp + 1) * 16 + i < N;
+      for (int qs = 0; qs < npair_q; ++qs) {
+        const bool half = last_half && qs == npair - 1;  // tile 2qs+1 is wholly padding (not in the images)
+        v4f Pm[2][2], DS[2][2];  // [key tile][query tile]
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const int qt = 2 * qs + u;
+          if (u == 1 && half) {
+            Pm[0][1] = Pm[1][1] = DS[0][1] = DS[1][1] = v4f{0.f, 0.f, 0.f, 0.f};
+            continue;
+          }
+          v8bf qr[KK], orow[KK];
+#pragma unroll
+          for (int kk = 0; kk < KK; ++kk) {
+            qr[kk] = __builtin_bit_cast(v8bf, lds_ld<v8s>(Qi + qt * T + L2.row[kk]));
+            orow[kk] = __builtin_bit_cast(v8bf, lds_ld<v8s>(Oi + qt * T + L2.row[kk]));
+          }
+          // padded queries (rows >= N) have zero Q and dO rows: their P is finite and dP = delta = 0, so they
+          // add nothing to dV = P^T dO or dK = dS^T Q whatever their (zero) lse
+          const v4f lq = *reinterpret_cast<const v4f*>(lse_s + qt * 16 + 4 * g) * LOG2E;
+          const v4f dq4 = *reinterpret_cast<const v4f*>(dlt_s + qt * 16 + 4 * g);
+#pragma unroll
+          for (int t = 0; t < 2; ++t) {
+            if (t == 1 && !t1_valid) {
+              Pm[1][u] = DS[1][u] = v4f{0.f, 0.f, 0.f, 0.f};
+              continue;
+            }
+            v4f sv = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int kk = 0; kk < KK; ++kk) {
+              sv = mfma(qr[kk], kf[t][kk], sv);
+              dp = mfma(orow[kk], vf[t][kk], dp);
+            }
+            const bool kvalid = t == 0 ? kv0 : kv1;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const float p = kvalid ? ex2(sv[r] * c - lq[r]) : 0.f;
+              Pm[t][u][r] = p;
+              DS[t][u][r] = p * (dp[r] - dq4[r]);
+            }
+          }
+        }
+        if (!half) {
+          const v8bf bP0 = pack8(Pm[0][0], Pm[0][1]), bP1 = pack8(Pm[1][0], Pm[1][1]);
+          const v8bf bD0 = pack8(DS[0][0], DS[0][1]), bD1 = pack8(DS[1][0], DS[1][1]);
+#pragma unroll
+          for (int dt = 0; dt < HD / 16; ++dt) {
+            v8s ot, qtr;
+            ot.lo = lds_tr(Oi + 2 * qs * T + L2.tr[dt]);
+            ot.hi = lds_tr(Oi + (2 * qs + 1) * T + L2.tr[dt]);
+            qtr.lo = lds_tr(Qi + 2 * qs * T + L2.tr[dt]);
+            qtr.hi = lds_tr(Qi + (2 * qs + 1) * T + L2.tr[dt]);
+            dv[0][dt] = mfma(__builtin_bit_cast(v8bf, ot), bP0, dv[0][dt]);
+            dk[0][dt] = mfma(__builtin_bit_cast(v8bf, qtr), bD0, dk[0][dt]);
+            if (t1_valid) {
+              dv[1][dt] = mfma(__builtin_bit_cast(v8bf, ot), bP1, dv[1][dt]);
+              dk[1][dt] = mfma(__builtin_bit_cast(v8bf, qtr), bD1, dk[1][dt]);
+            }
+          }
+        } else {  // one query tile: the 16-deep MFMA on tile 2qs alone
+          const v4s bP0 = pack4(Pm[0][0]), bP1 = pack4(Pm[1][0]);
+          const v4s bD0 = pack4(DS[0][0]), bD1 = pack4(DS[1][0]);
+#pragma unroll
+          for (int dt = 0; dt < HD / 16; ++dt) {
+            const v4s ot = lds_tr(Oi + 2 * qs * T + L2.tr[dt]);
+            const v4s qtr = lds_tr(Qi + 2 * qs * T + L2.tr[dt]);
+            dv[0][dt] = mfma16(ot, bP0, dv[0][dt]);
+            dk[0][dt] = mfma16(qtr, bD0, dk[0][dt]);
+            if (t1_valid) {
+              dv[1][dt] = mfma16(ot, bP1, dv[1][dt]);
+              dk[1][dt] = mfma16(qtr, bD1, dk[1][dt]);
+            }
+          }
+        }
+      }
+      uint2 pk[2][HD / 16], pv[2][HD / 16];
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int dt = 0; dt < HD / 16; ++dt) {
+          pk[t][dt] = pack4bf(dk[t][dt], scale);
+          pv[t][dt] = pack4bf(dv[t][dt], 1.0f);
+        }
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {  // rows past N are dropped by the descriptors
+        const __amdgpu_buffer_rsrc_t rk = rows_rsrc(dqb + D, rs, (2 * kp + t) * 16, N, hd);
+        const __amdgpu_buffer_rsrc_t rv = rows_rsrc(dqb + 2 * D, rs, (2 * kp + t) * 16, N, hd);
+#pragma unroll
+        for (int dt = 0; dt < HD / 16; ++dt)
+          if (dt * 16 < hd) {
+            st_b64(rk, offs + dt * 32, pk[t][dt]);
+            st_b64(rv, offs + dt * 32, pv[t][dt]);
+          }
+      }
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int dt = 0; dt < HD / 16; ++dt) {
+          keep_live2(pk[t][dt]);
+          keep_live2(pv[t][dt]);
+        }
+      if (bias_partial) {
+#pragma unroll
+        for (int dt = 0; dt < HD / 16; ++dt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {  // invalid keys hold exact zeros (P = 0)
+            bk4[dt][r] = dk[0][dt][r] + dk[1][dt][r];
+            bv4[dt][r] = dv[0][dt][r] + dv[1][dt][r];
+          }
+      }
+    }
+    STAMP(5);
+
+    // ---- bias partials: per-wave column sums, then a fixed-order sum over the waves ----
+    if (bias_partial) {
+      lds_barrier();  // stage 2 is done with this item's Q / dO slot: it is scratch now
+      float* bsum = reinterpret_cast<float*>(SLOT ? qo1_s : qo0_s);  // [NW][3][HD]
+      if (4 * (i >> 2) < HD / 4) {  // lane 16 g + 4 dt + r holds column 16 dt + 4 g + r
+        const int dt = i >> 2, r = i & 3;
+        bsum[(wave * 3 + 0) * HD + dt * 16 + 4 * g + r] = bq1 * scale;
+      }
+#pragma unroll
+      for (int dt = 0; dt < HD / 16; ++dt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float sk = row_sum16_to15(bk4[dt][r]), sv = row_sum16_to15(bv4[dt][r]);
+          if (i == 15) {
+            const int d = dt * 16 + 4 * g + r;
+            bsum[(wave * 3 + 1) * HD + d] = sk * scale;
+            bsum[(wave * 3 + 2) * HD + d] = sv;
+          }
+        }
+      lds_barrier();
+      for (int e = threadIdx.x; e < 3 * HD; e += NW * 64) {
+        const int z = e / HD, d = e % HD;
+        if (d >= hd) continue;
+        float acc = 0.f;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) acc += bsum[(w * 3 + z) * HD + d];
+        bias_partial[(long)b * 3 * D + z * D + h * hd + d] = acc;
+      }
+    }
+    STAMP(6);
+    item = next;
+    ++it;
+  };
+  while (true) {
+    body(std::integral_constant<int, 0>{});
+    if (item >= nitems) break;
+    body(std::integral_constant<int, 1>{});
+    if (item >= nitems) break;
+  }
+}
+
+template <int HD, int NKT>
+constexpr size_t pers_lds() {
+  constexpr size_t img2 = (size_t)2 * NKT * 16 * HD * 2, bsum = (size_t)PB_NW * 3 * HD * 4;
+  return img2 + 2 * (img2 > bsum ? img2 : bsum) + 2 * ((NKT * 16 * 4 + 1023) / 1024 * 1024) + NKT * 16 * 4;
+}
+
+template <int HD, int NKT>
+hipError_t launch_pers(const bf16_t* qkv, const bf16_t* dout, const float* lse, bf16_t* dqkv, float* bias_partial,
+                       int B, int N, int H, int hd, float scale, int nq, hipStream_t s) {
+  static_assert(pers_lds<HD, NKT>() <= 160 * 1024, "LDS budget");
+  auto kern = attn_bwd_pers_kernel<HD, NKT>;
+  int cus = 256;
+  {
+    int dev = 0;
+    if (hipGetDevice(&dev) == hipSuccess) {
+      int n = 0;
+      if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0) cus = n;
+    }
+  }
+  const int items = B * H;
+  const int grid = items < cus ? items : cus;
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(PB_NW * 64), 0, s, qkv, dout, lse, dqkv, bias_partial, items, N, H, hd,
+                     scale, nq);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+// LDS bytes of the persistent backward for (N, head width), 0 when it does not apply (the two-stage
+// kernel of attention.hip then runs)
+size_t vit_attn_bwd_pers_lds(int N, int hd) {
+  if (hd > 64) return 0;
+  const int HD = hd <= 32 ? 32 : 64;
+  const int np = (N + 15) / 16 * 16;
+  const size_t img2 = (size_t)2 * np * HD * 2, bsum = (size_t)PB_NW * 3 * HD * 4;
+  const size_t lds = img2 + 2 * (img2 > bsum ? img2 : bsum) + 2 * ((np * 4 + 1023) / 1024 * 1024) + np * 4;
+  return lds <= 160 * 1024 ? lds : 0;
+}
+
+#ifdef VIT_ATTN_STAMPS
+extern "C" int vit_attn_stamps(unsigned long long* out) {  // 64 values: [wave 0 / 7][item][point]
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_attn_stamps), sizeof(g_attn_stamps));
+}
+#endif
+
+hipError_t vit_attn_bwd_pers(const void* qkv, const void* dout, const float* lse, void* dqkv, float* bias_partial,
+                             int B, int N, int H, int hd, float scale, int nq, hipStream_t s) {
+  const bf16_t *q = (const bf16_t*)qkv, *d = (const bf16_t*)dout;
+  bf16_t* dq = (bf16_t*)dqkv;
+  const int nkt = (N + 15) / 16;
+  if (hd <= 32) {
+    switch (nkt) {
+#define C(n) \
+  case n: return launch_pers<32, n>(q, d, lse, dq, bias_partial, B, N, H, hd, scale, nq, s);
+      C(1) C(2) C(3) C(4) C(5) C(6) C(7) C(8) C(9) C(10) C(11) C(12) C(13) C(14) C(15) C(16) C(17) C(18) C(19) C(20)
+#undef C
+    }
+  } else {
+    switch (nkt) {
+#define C(n) \
+  case n: return launch_pers<64, n>(q, d, lse, dq, bias_partial, B, N, H, hd, scale, nq, s);
+      C(1) C(2) C(3) C(4) C(5) C(6) C(7) C(8) C(9) C(10) C(11) C(12) C(13)
+#undef C
+    }
+  }
+  return hipErrorInvalidValue;
+}
