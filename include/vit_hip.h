@@ -184,12 +184,13 @@ int vit_attention_fwd_rows(const void* qkv, void* o, float* lse, int64_t B, int6
 int vit_attention_bwd_rows(const void* qkv, const void* o, const void* dout, const float* lse, void* dqkv,
                            float* bias_partial, int64_t B, int64_t N, int64_t H, int64_t hd, float scale,
                            int64_t q_rows, vit_stream_t stream);
-/* Path-explicit forms. bias_partial of the backward holds vit_attention_bias_rows(N, path) rows per
- * image ([B * rows][3*H*hd], reduce all B * rows rows with vit_colsum): 1 on path 1, ceil(N / 64) on
+/* Path-explicit forms. bias_partial of the backward holds vit_attention_bias_rows(N, hd, path) rows per
+ * image ([B * rows][3*H*hd], reduce all B * rows rows with vit_colsum): on path 1 one per wave of the
+ * persistent kernel (8; hd <= 64 and N <= 208 at hd 64) or 1 (the two-stage kernel), ceil(N / 64) on
  * path 2 (one per 64-row block). The tiled backward needs `workspace`, >= vit_attention_workspace_elems
  * floats (the exact per-query delta = sum_j P dP handed from its dQ kernel to its dK/dV kernel);
  * path 1 needs none (NULL). q_rows as for the *_rows forms (path 2 rounds it up to 64-row blocks). */
-int64_t vit_attention_bias_rows(int64_t N, int32_t path);
+int64_t vit_attention_bias_rows(int64_t N, int64_t hd, int32_t path);
 int64_t vit_attention_workspace_elems(int64_t B, int64_t N, int64_t H, int32_t path);
 int vit_attention_fwd_ex(const void* qkv, void* o, float* lse, int64_t B, int64_t N, int64_t H, int64_t hd,
                          float scale, int64_t q_rows, int32_t path, vit_stream_t stream);

@@ -234,7 +234,7 @@ def test_attention(B, N, H, hd, path):
     assert rel(lse, lref.detach()) < 1e-4
     dout = torch.randn(B * N, D, device=DEV).bfloat16()
     dqkv = torch.full((B * N, 3 * D), float("nan"), device=DEV, dtype=torch.bfloat16)
-    rows = ops.attention_bias_rows(N, path)
+    rows = ops.attention_bias_rows(N, hd, path)
     bpart = torch.full((B * rows, 3 * D), float("nan"), device=DEV)
     ops.attention_bwd(qkv.detach(), o, dout, lse, dqkv, B, N, H, hd, 1.0 / math.sqrt(hd), bias_partial=bpart,
                       path=path)
@@ -268,7 +268,7 @@ def test_attention_backward_saturated_scores_finite(N, B):
     assert float(lse.min()) < -100.0
     dout = torch.randn(B * N, D, device=DEV).bfloat16()
     dqkv = torch.zeros(B * N, 3 * D, device=DEV, dtype=torch.bfloat16)
-    bp = torch.zeros(B, 3 * D, device=DEV)
+    bp = torch.zeros(B * ops.attention_bias_rows(N, hd), 3 * D, device=DEV)
     ops.attention_bwd(qkv, o, dout, lse, dqkv, B, N, H, hd, 1.0 / math.sqrt(hd), bias_partial=bp)
     assert torch.isfinite(o.float()).all() and torch.isfinite(dqkv.float()).all() and torch.isfinite(bp).all()
 
@@ -465,7 +465,8 @@ def test_attention_query_rows_match_full(B, N, H, hd, path):
     l_f, l_r = torch.empty(B, H, N, device=DEV), torch.full((B, H, N), float("nan"), device=DEV)
     ops.attention_fwd(qkv, o_f, l_f, B, N, H, hd, sc, path=path)
     ops.attention_fwd(qkv, o_r, l_r, B, N, H, hd, sc, q_rows=1, path=path)
-    rows = min(N, 32 if ops.attention_bias_rows(N, path) == 1 else 64)  # whole query pairs / 64-row blocks
+    tiled = path == 2 or (path == 0 and N > 320)
+    rows = min(N, 64 if tiled else 32)  # whole 64-row blocks (tiled) / query pairs (resident)
     ov_f, ov_r = o_f.view(B, N, D)[:, :rows], o_r.view(B, N, D)[:, :rows]
     assert torch.equal(ov_f, ov_r) and torch.equal(l_f[:, :, :rows], l_r[:, :, :rows])
     dout = torch.zeros(B, N, D, device=DEV)
@@ -474,7 +475,7 @@ def test_attention_query_rows_match_full(B, N, H, hd, path):
     outs = []
     for qr in (None, 1):
         dqkv = torch.full((B * N, 3 * D), float("nan"), device=DEV, dtype=torch.bfloat16)
-        bpart = torch.full((B * ops.attention_bias_rows(N, path), 3 * D), float("nan"), device=DEV)
+        bpart = torch.full((B * ops.attention_bias_rows(N, hd, path), 3 * D), float("nan"), device=DEV)
         ops.attention_bwd(qkv, o_f, dout, l_f, dqkv, B, N, H, hd, sc, bias_partial=bpart, q_rows=qr, path=path)
         outs.append((dqkv, bpart))
     (g_f, b_f), (g_r, b_r) = outs

@@ -35,7 +35,7 @@ def run(B, N, H, hd, path):
     lse = torch.empty(B * H * N, device="cuda")
     do = torch.randn(B * N, D, device="cuda").bfloat16()
     dqkv = torch.empty_like(qkv)
-    bp = torch.empty(B * ops.attention_bias_rows(N, path), 3 * D, device="cuda")
+    bp = torch.empty(B * ops.attention_bias_rows(N, hd, path), 3 * D, device="cuda")
     ws = torch.empty(max(1, ops.attention_workspace_elems(B, N, H, path)), device="cuda")
     fl = 4 * B * H * N * N * hd
     by_f = (3 + 1) * B * N * D * 2

@@ -31,11 +31,12 @@ for B, N, H, hd, amp, nq in CASES:
     oref = (p @ v).permute(0, 2, 1, 3).reshape(B * N, D)
     dout = torch.randn(B * N, D, device="cuda").bfloat16()
     dqkv = torch.full((B * N, 3 * D), float("nan"), device="cuda", dtype=torch.bfloat16)
-    bpart = torch.full((B, 3 * D), float("nan"), device="cuda")
+    bpart = torch.full((B * ops.attention_bias_rows(N, hd), 3 * D), float("nan"), device="cuda")
     if nq is not None:
         dout.view(B, N, D)[:, nq:] = 0
     ops.attention_bwd(qkv, o, dout, lse, dqkv, B, N, H, hd, 1.0 / math.sqrt(hd), bias_partial=bpart, q_rows=nq)
     gref, = torch.autograd.grad(oref, qf, dout.float())
+    bpart = bpart.view(B, -1, 3 * D).sum(1)
     m = dqkv.float().view(B * N, 3, D)
     gr = gref.view(B * N, 3, D)
     bref = gref.view(B, N, 3 * D).sum(1)

@@ -19,7 +19,7 @@ o = torch.empty(B * N, D, device="cuda", dtype=torch.bfloat16)
 lse = torch.empty(B * H * N, device="cuda")
 do = torch.randn(B * N, D, device="cuda").bfloat16()
 dqkv = torch.empty_like(qkv)
-bp = torch.empty(B, 3 * D, device="cuda")
+bp = torch.empty(B * ops.attention_bias_rows(N, hd), 3 * D, device="cuda")
 ops.attention_fwd(qkv, o, lse, B, N, H, hd, hd ** -0.5)
 for _ in range(3):
     ops.attention_bwd(qkv, o, do, lse, dqkv, B, N, H, hd, hd ** -0.5, bias_partial=bp, q_rows=nq)

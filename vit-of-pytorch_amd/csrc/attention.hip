@@ -782,11 +782,14 @@ hipError_t vit_attn_tiled_fwd(const void* qkv, void* o, float* lse, int B, int N
 hipError_t vit_attn_tiled_bwd(const void* qkv, const void* dout, const float* lse, float* delta, void* dqkv,
                               float* bias_partial, int B, int N, int H, int hd, float scale, int nq, hipStream_t s);
 size_t vit_attn_bwd_pers_lds(int N, int hd);
+int vit_attn_bwd_pers_bias_rows();
 hipError_t vit_attn_bwd_pers(const void* qkv, const void* dout, const float* lse, void* dqkv, float* bias_partial,
                              int B, int N, int H, int hd, float scale, int nq, hipStream_t s);
 
-extern "C" int64_t vit_attention_bias_rows(int64_t N, int32_t path) {
-  return resolve_path(path, N) == 1 ? 1 : (N + 63) / 64;
+extern "C" int64_t vit_attention_bias_rows(int64_t N, int64_t hd, int32_t path) {
+  if (resolve_path(path, N) == 2) return (N + 63) / 64;  // one per 64-row block
+  // persistent kernel: one per wave; two-stage kernel: one per image
+  return vit_attn_bwd_pers_lds((int)N, (int)hd) > 0 ? vit_attn_bwd_pers_bias_rows() : 1;
 }
 
 extern "C" int64_t vit_attention_workspace_elems(int64_t B, int64_t N, int64_t H, int32_t path) {

@@ -18,11 +18,11 @@
 //   stage 2  each wave owns one pair of 16-key tiles, K / V rows taken from the images into registers;
 //            S, dP recomputed against the Q / dO images, dV = P^T dO, dK = dS^T Q accumulated in
 //            registers (no atomics: deterministic);
-//   bias     per-wave column sums of dQ, dK, dV -> a fixed-order sum over the waves through the item's
-//            (now dead) Q / dO slot -> bias_partial[b][3 D] (q|k|v bias-gradient partials, one row per image).
+//   bias     per-wave column sums of dQ, dK, dV (DPP row sums) -> row (b, wave) of bias_partial[b][PB_NW][3 D]
+//            (q|k|v bias-gradient partials; no cross-wave step, so no barrier: the column reduction that
+//            finishes the bias gradients sums the PB_NW rows of each image).
 // LDS: K / V images, Q / dO slot 0, Q / dO slot 1 ([NP][HD] bf16, NP = 16 * ceil(N / 16), 16-B-chunk XOR
-// swizzle of attn_common.h), lse slot 0 / 1 and delta rows: 6 * NP * HD * 2 + 12 * NP bytes (162 KB at
-// N = 197, hd 64). Separate LDS objects per slot and a slot-templated item body: hipcc then proves that an
+// swizzle of attn_common.h), lse slot 0 / 1 (whole 1-KiB DMA pieces) and delta rows (162 KB at N = 197, hd 64). Separate LDS objects per slot and a slot-templated item body: hipcc then proves that an
 // in-flight LDS-DMA into one slot cannot alias the accesses to another and inserts no vmcnt wait for it.
 #include "attn_common.h"
 #include <type_traits>
@@ -61,16 +61,6 @@ __device__ __forceinline__ T* uniform_ptr(T* p) {
   return (T*)(((unsigned long long)hi << 32) | lo);
 }
 
-// sum over the 16 lanes of a DPP row (lanes sharing lane >> 4), fixed order (inclusive prefix by row_shr
-// 1, 2, 4, 8): the total lands in lane 15 of the row
-__device__ __forceinline__ float row_sum16_to15(float v) {
-  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x111, 0xf, 0xf, true));
-  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x112, 0xf, 0xf, true));
-  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x114, 0xf, 0xf, true));
-  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x118, 0xf, 0xf, true));
-  return v;
-}
-
 // Workgroup barrier for LDS hand-offs only. __syncthreads() also waits vmcnt(0) (global-store visibility),
 // which would stall every wave on the LDS-DMA prefetches in flight; LDS-DMA completion is handled explicitly
 // (each wave drains its own vmcnt before the item-start barrier).
@@ -81,23 +71,30 @@ __device__ __forceinline__ void lds_barrier() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
-// Gather the row totals left in lane 15 of each DPP row by row_sum16_to15 for 16 values v[0..15] into one
-// register: lane 16 g + k receives v[k]'s total of row g. row_ror:n gives lane j the row's lane (j - n) mod 16,
-// so n = k + 1 brings lane 15 to lane k.
-template <int K>
-__device__ __forceinline__ void gather_step(const float (&v)[16], int i, float& out) {
-  if constexpr (K < 16) {
-    float m = v[K];
-    if constexpr (K < 15)
-      m = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v[K]), 0x121 + K, 0xf, 0xf, false));
-    out = i == K ? m : out;
-    gather_step<K + 1>(v, i, out);
+// Column sums over the 16 lanes of a DPP row for 16 values at once: v[k] of every lane of the row summed, the
+// total of v[k] landing in lane k of the row (a fixed-order butterfly, deterministic). Each step halves the
+// values a lane holds: the lane keeps the half selected by one bit of its row index and adds what its
+// partner (ror 8, half-mirror, xor 2, xor 1: partners differ in that bit and agree on the bits already
+// used) sends of the same half: 8 + 4 + 2 + 1 DPP moves instead of 16 x 4 row-sum steps.
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov(float x) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), CTRL, 0xf, 0xf, false));
+}
+template <int NV, int CTRL>
+__device__ __forceinline__ void butterfly_step(float* v, bool upper) {
+#pragma unroll
+  for (int k = 0; k < NV / 2; ++k) {
+    const float keep = upper ? v[k + NV / 2] : v[k];
+    const float send = upper ? v[k] : v[k + NV / 2];
+    v[k] = keep + dpp_mov<CTRL>(send);
   }
 }
-__device__ __forceinline__ float gather_row_totals(const float (&v)[16], int i) {
-  float out = 0.f;
-  gather_step<0>(v, i, out);
-  return out;
+__device__ __forceinline__ float reduce16(float (&v)[16], int i) {
+  butterfly_step<16, 0x128>(v, (i & 8) != 0);  // row_ror:8 (lane ^ 8)
+  butterfly_step<8, 0x141>(v, (i & 4) != 0);   // row_half_mirror (j <-> 7 - j within 8 lanes)
+  butterfly_step<4, 0x4E>(v, (i & 2) != 0);    // quad_perm [2,3,0,1] (lane ^ 2)
+  butterfly_step<2, 0xB1>(v, (i & 1) != 0);    // quad_perm [1,0,3,2] (lane ^ 1)
+  return v[0];
 }
 
 // the lane index, recomputed where it is used (opaque to CSE): lane-derived offsets of a later phase are
@@ -172,11 +169,9 @@ __global__ void __launch_bounds__(PB_NW * 64, 1) attn_bwd_pers_kernel(const bf16
   constexpr int KK = HD / 32;
   constexpr int T = ImgLane<HD>::TILE;
   constexpr int LSEB = (NP * 4 + 1023) / 1024 * 1024;  // lse slot bytes (whole DMA pieces)
-  // a Q / dO slot is also the item's bias-sum scratch ([NW][3][HD] floats) once stage 2 is done
-  constexpr int QOB = 2 * IMG > NW * 3 * HD * 4 ? 2 * IMG : NW * 3 * HD * 4;
-  __shared__ __attribute__((aligned(16))) char kv_s[2 * IMG];  // K | V images
-  __shared__ __attribute__((aligned(16))) char qo0_s[QOB];     // Q | dO images, slot 0
-  __shared__ __attribute__((aligned(16))) char qo1_s[QOB];     // Q | dO images, slot 1
+  __shared__ __attribute__((aligned(16))) char kv_s[2 * IMG];   // K | V images
+  __shared__ __attribute__((aligned(16))) char qo0_s[2 * IMG];  // Q | dO images, slot 0
+  __shared__ __attribute__((aligned(16))) char qo1_s[2 * IMG];  // Q | dO images, slot 1
   __shared__ __attribute__((aligned(16))) char ls0_s[LSEB];      // lse rows (natural log), slot 0
   __shared__ __attribute__((aligned(16))) char ls1_s[LSEB];      // lse rows, slot 1
   __shared__ __attribute__((aligned(16))) float dlt_s[NP];       // delta rows of the item
@@ -241,8 +236,9 @@ __global__ void __launch_bounds__(PB_NW * 64, 1) attn_bwd_pers_kernel(const bf16
     if (next < nitems) dma_qo(Qn, Ln, next);
 
     // ---- stage 1: delta, dS, dQ per 16-query strip ----
-    // the wave's dQ column sums, packed in one register: lane 16 g + 4 dt + r holds column 16 dt + 4 g + r
-    float bq1 = 0.f;
+    float bq16[16];  // the wave's dQ column partials: [4 dt + r] for column 16 dt + 4 g + r (summed over lanes i later)
+#pragma unroll
+    for (int k = 0; k < 16; ++k) bq16[k] = 0.f;
     for (int qt = wave; qt < nqt; qt += NW) {
       const int q = qt * 16 + i;
       const __amdgpu_buffer_rsrc_t rdq = rows_rsrc(dqb, rs, qt * 16, N, hd);
@@ -329,15 +325,15 @@ __global__ void __launch_bounds__(PB_NW * 64, 1) attn_bwd_pers_kernel(const bf16
 #pragma unroll
         for (int dt = 0; dt < HD / 16; ++dt) keep_live2(pk[dt]);
       }
-      if (bias_partial) {  // the strip's column sums (padded queries: dS = 0)
-        float t16[16];
+      if (bias_partial) {  // padded queries: dS = 0
 #pragma unroll
-        for (int dt = 0; dt < 4; ++dt)
+        for (int dt = 0; dt < HD / 16; ++dt)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) t16[dt * 4 + r] = dt < HD / 16 ? row_sum16_to15(dq[dt][r]) : 0.f;
-        bq1 += gather_row_totals(t16, i);
+          for (int r = 0; r < 4; ++r) bq16[dt * 4 + r] += dq[dt][r];
       }
     }
+    // lane 16 g + 4 dt + r: the wave's sum of dQ column 16 dt + 4 g + r
+    const float bq1 = bias_partial ? reduce16(bq16, i) : 0.f;
     STAMP(3);
     lds_barrier();  // delta complete
     STAMP(4);
@@ -374,16 +370,16 @@ __global__ void __launch_bounds__(PB_NW * 64, 1) attn_bwd_pers_kernel(const bf16
 #pragma unroll
         for (int dt = 0; dt < HD / 16; ++dt) dv[t][dt] = dk[t][dt] = v4f{0.f, 0.f, 0.f, 0.f};
       const bool kv0 = (2 * kp) * 16 + i < N, kv1 = (2 * kp + 1) * 16 + i < N;
-      for (int qs = 0; qs < npair_q; ++qs) {
-        const bool half = last_half && qs == npair - 1;  // tile 2qs+1 is wholly padding (not in the images)
+      // one (key pair, query pair) unit; FULL = false: the query pair's second tile is wholly padding (past
+      // the images), so only tile 2 qs is used, with the 16-deep MFMA. Both key tiles are always computed (an
+      // invalid second tile has zero K / V rows and P masked to 0), so the unit has no branch.
+      auto unit = [&](int qs, auto full) {
+        constexpr bool FULL = decltype(full)::value;
+        constexpr int NU = FULL ? 2 : 1;
         v4f Pm[2][2], DS[2][2];  // [key tile][query tile]
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
+        for (int u = 0; u < NU; ++u) {
           const int qt = 2 * qs + u;
-          if (u == 1 && half) {
-            Pm[0][1] = Pm[1][1] = DS[0][1] = DS[1][1] = v4f{0.f, 0.f, 0.f, 0.f};
-            continue;
-          }
           v8bf qr[KK], orow[KK];
 #pragma unroll
           for (int kk = 0; kk < KK; ++kk) {
@@ -396,10 +392,6 @@ __global__ void __launch_bounds__(PB_NW * 64, 1) attn_bwd_pers_kernel(const bf16
           const v4f dq4 = *reinterpret_cast<const v4f*>(dlt_s + qt * 16 + 4 * g);
 #pragma unroll
           for (int t = 0; t < 2; ++t) {
-            if (t == 1 && !t1_valid) {
-              Pm[1][u] = DS[1][u] = v4f{0.f, 0.f, 0.f, 0.f};
-              continue;
-            }
             v4f sv = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
             for (int kk = 0; kk < KK; ++kk) {
@@ -409,13 +401,14 @@ __global__ void __launch_bounds__(PB_NW * 64, 1) attn_bwd_pers_kernel(const bf16
             const bool kvalid = t == 0 ? kv0 : kv1;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-              const float p = kvalid ? ex2(sv[r] * c - lq[r]) : 0.f;
+              const float pr = ex2(sv[r] * c - lq[r]);
+              const float p = kvalid ? pr : 0.f;
               Pm[t][u][r] = p;
               DS[t][u][r] = p * (dp[r] - dq4[r]);
             }
           }
         }
-        if (!half) {
+        if constexpr (FULL) {
           const v8bf bP0 = pack8(Pm[0][0], Pm[0][1]), bP1 = pack8(Pm[1][0], Pm[1][1]);
           const v8bf bD0 = pack8(DS[0][0], DS[0][1]), bD1 = pack8(DS[1][0], DS[1][1]);
 #pragma unroll
@@ -427,12 +420,10 @@ __global__ void __launch_bounds__(PB_NW * 64, 1) attn_bwd_pers_kernel(const bf16
             qtr.hi = lds_tr(Qi + (2 * qs + 1) * T + L2.tr[dt]);
             dv[0][dt] = mfma(__builtin_bit_cast(v8bf, ot), bP0, dv[0][dt]);
             dk[0][dt] = mfma(__builtin_bit_cast(v8bf, qtr), bD0, dk[0][dt]);
-            if (t1_valid) {
-              dv[1][dt] = mfma(__builtin_bit_cast(v8bf, ot), bP1, dv[1][dt]);
-              dk[1][dt] = mfma(__builtin_bit_cast(v8bf, qtr), bD1, dk[1][dt]);
-            }
+            dv[1][dt] = mfma(__builtin_bit_cast(v8bf, ot), bP1, dv[1][dt]);
+            dk[1][dt] = mfma(__builtin_bit_cast(v8bf, qtr), bD1, dk[1][dt]);
           }
-        } else {  // one query tile: the 16-deep MFMA on tile 2qs alone
+        } else {
           const v4s bP0 = pack4(Pm[0][0]), bP1 = pack4(Pm[1][0]);
           const v4s bD0 = pack4(DS[0][0]), bD1 = pack4(DS[1][0]);
 #pragma unroll
@@ -441,13 +432,14 @@ __global__ void __launch_bounds__(PB_NW * 64, 1) attn_bwd_pers_kernel(const bf16
             const v4s qtr = lds_tr(Qi + 2 * qs * T + L2.tr[dt]);
             dv[0][dt] = mfma16(ot, bP0, dv[0][dt]);
             dk[0][dt] = mfma16(qtr, bD0, dk[0][dt]);
-            if (t1_valid) {
-              dv[1][dt] = mfma16(ot, bP1, dv[1][dt]);
-              dk[1][dt] = mfma16(qtr, bD1, dk[1][dt]);
-            }
+            dv[1][dt] = mfma16(ot, bP1, dv[1][dt]);
+            dk[1][dt] = mfma16(qtr, bD1, dk[1][dt]);
           }
         }
-      }
+      };
+      const int nfull = last_half && npair_q == npair ? npair_q - 1 : npair_q;
+      for (int qs = 0; qs < nfull; ++qs) unit(qs, std::true_type{});
+      if (nfull < npair_q) unit(nfull, std::false_type{});
       uint2 pk[2][HD / 16], pv[2][HD / 16];
 #pragma unroll
       for (int t = 0; t < 2; ++t)
@@ -486,33 +478,24 @@ __global__ void __launch_bounds__(PB_NW * 64, 1) attn_bwd_pers_kernel(const bf16
     }
     STAMP(5);
 
-    // ---- bias partials: per-wave column sums, then a fixed-order sum over the waves ----
+    // ---- bias partials: the wave's column sums of dQ, dK, dV -> its own row of bias_partial (every wave
+    // writes its row, zeros when it had no strip / pair; vit_colsum_batch sums the PB_NW rows per image)
     if (bias_partial) {
-      lds_barrier();  // stage 2 is done with this item's Q / dO slot: it is scratch now
-      float* bsum = reinterpret_cast<float*>(SLOT ? qo1_s : qo0_s);  // [NW][3][HD]
-      if (4 * (i >> 2) < HD / 4) {  // lane 16 g + 4 dt + r holds column 16 dt + 4 g + r
-        const int dt = i >> 2, r = i & 3;
-        bsum[(wave * 3 + 0) * HD + dt * 16 + 4 * g + r] = bq1 * scale;
-      }
+      float tk[16], tv[16];
 #pragma unroll
-      for (int dt = 0; dt < HD / 16; ++dt)
+      for (int dt = 0; dt < 4; ++dt)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float sk = row_sum16_to15(bk4[dt][r]), sv = row_sum16_to15(bv4[dt][r]);
-          if (i == 15) {
-            const int d = dt * 16 + 4 * g + r;
-            bsum[(wave * 3 + 1) * HD + d] = sk * scale;
-            bsum[(wave * 3 + 2) * HD + d] = sv;
-          }
+          tk[dt * 4 + r] = dt < HD / 16 ? bk4[dt][r] : 0.f;
+          tv[dt * 4 + r] = dt < HD / 16 ? bv4[dt][r] : 0.f;
         }
-      lds_barrier();
-      for (int e = threadIdx.x; e < 3 * HD; e += NW * 64) {
-        const int z = e / HD, d = e % HD;
-        if (d >= hd) continue;
-        float acc = 0.f;
-#pragma unroll
-        for (int w = 0; w < NW; ++w) acc += bsum[(w * 3 + z) * HD + d];
-        bias_partial[(long)b * 3 * D + z * D + h * hd + d] = acc;
+      const float bk1 = reduce16(tk, i), bv1 = reduce16(tv, i);
+      const int dcol = 16 * (i >> 2) + 4 * g + (i & 3);  // this lane's column (see reduce16)
+      if (dcol < hd) {
+        float* row = bias_partial + ((long)b * NW + wave) * 3 * D + h * hd + dcol;
+        row[0] = bq1 * scale;
+        row[D] = bk1 * scale;
+        row[2 * D] = bv1;
       }
     }
     STAMP(6);
@@ -529,8 +512,7 @@ __global__ void __launch_bounds__(PB_NW * 64, 1) attn_bwd_pers_kernel(const bf16
 
 template <int HD, int NKT>
 constexpr size_t pers_lds() {
-  constexpr size_t img2 = (size_t)2 * NKT * 16 * HD * 2, bsum = (size_t)PB_NW * 3 * HD * 4;
-  return img2 + 2 * (img2 > bsum ? img2 : bsum) + 2 * ((NKT * 16 * 4 + 1023) / 1024 * 1024) + NKT * 16 * 4;
+  return (size_t)6 * NKT * 16 * HD * 2 + 2 * ((NKT * 16 * 4 + 1023) / 1024 * 1024) + NKT * 16 * 4;
 }
 
 template <int HD, int NKT>
@@ -561,8 +543,7 @@ size_t vit_attn_bwd_pers_lds(int N, int hd) {
   if (hd > 64) return 0;
   const int HD = hd <= 32 ? 32 : 64;
   const int np = (N + 15) / 16 * 16;
-  const size_t img2 = (size_t)2 * np * HD * 2, bsum = (size_t)PB_NW * 3 * HD * 4;
-  const size_t lds = img2 + 2 * (img2 > bsum ? img2 : bsum) + 2 * ((np * 4 + 1023) / 1024 * 1024) + np * 4;
+  const size_t lds = (size_t)6 * np * HD * 2 + 2 * ((np * 4 + 1023) / 1024 * 1024) + np * 4;
   return lds <= 160 * 1024 ? lds : 0;
 }
 
@@ -571,6 +552,8 @@ extern "C" int vit_attn_stamps(unsigned long long* out) {  // 64 values: [wave 0
   return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_attn_stamps), sizeof(g_attn_stamps));
 }
 #endif
+
+int vit_attn_bwd_pers_bias_rows() { return PB_NW; }
 
 hipError_t vit_attn_bwd_pers(const void* qkv, const void* dout, const float* lse, void* dqkv, float* bias_partial,
                              int B, int N, int H, int hd, float scale, int nq, hipStream_t s) {

@@ -17,7 +17,7 @@ c_i32 = ctypes.c_int32
 c_f32 = ctypes.c_float
 c_vp = ctypes.c_void_p
 
-ABI_VERSION = 7  # vit_abi_version() of the library these prototypes describe
+ABI_VERSION = 8  # vit_abi_version() of the library these prototypes describe
 
 # enum vit_layout / vit_epilogue (include/vit_hip.h)
 K_CONTIG, MN_CONTIG = 0, 1
@@ -72,7 +72,7 @@ _SIGS = {
     "vit_attention_fwd_rows": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_f32, c_i64, c_vp]),
     "vit_attention_bwd_rows": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_f32, c_i64,
                                        c_vp]),
-    "vit_attention_bias_rows": (c_i64, [c_i64, c_i32]),
+    "vit_attention_bias_rows": (c_i64, [c_i64, c_i64, c_i32]),
     "vit_attention_workspace_elems": (c_i64, [c_i64, c_i64, c_i64, c_i32]),
     "vit_attention_fwd_ex": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_f32, c_i64, c_i32, c_vp]),
     "vit_attention_bwd_ex": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_f32, c_i64,

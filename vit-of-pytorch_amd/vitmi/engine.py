@@ -174,7 +174,7 @@ class _Acts:
         self.gelu_parts = [z(-(-T // 128), M, dt=f) for _ in range(_NBUF)]  # per-M-tile column sums of dU (fc1 bias)
         # column sums of dq|dk|dv (q/k/v bias grads): per image (LDS-resident attention, N <= 320) or per
         # image and 64-row block (K/V-tiled attention, longer sequences)
-        self.attn_bias_rows = ops.attention_bias_rows(N)
+        self.attn_bias_rows = ops.attention_bias_rows(N, D // H)
         self.qkv_bparts = [z(b * self.attn_bias_rows, 3 * D, dt=f) for _ in range(_NBUF)]
         nws = ops.attention_workspace_elems(b, N, H)
         self.attn_ws = z(nws, dt=f) if nws else None

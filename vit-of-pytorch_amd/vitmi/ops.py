@@ -120,9 +120,10 @@ def layernorm_bwd(dy, lddy, x, ldx, mean, rstd, gamma, dx, lddx, partial, rows, 
 ATTN_AUTO, ATTN_RESIDENT, ATTN_TILED = 0, 1, 2
 
 
-def attention_bias_rows(N, path=ATTN_AUTO):
-    """rows of the backward's bias_partial per image (1 resident, ceil(N/64) tiled)."""
-    return int(lib().vit_attention_bias_rows(N, path))
+def attention_bias_rows(N, hd, path=ATTN_AUTO):
+    """rows of the backward's bias_partial per image (resident: 8 on the persistent kernel, else 1;
+    tiled: ceil(N/64))."""
+    return int(lib().vit_attention_bias_rows(N, hd, path))
 
 
 def attention_workspace_elems(B, N, H, path=ATTN_AUTO):
@@ -142,7 +143,7 @@ def attention_fwd(qkv, o, lse, B, N, H, hd, scale, q_rows=None, path=ATTN_AUTO):
 def attention_bwd(qkv, o, dout, lse, dqkv, B, N, H, hd, scale, bias_partial=None, q_rows=None, path=ATTN_AUTO,
                   workspace=None):
     """q_rows: dout is zero outside queries [0, q_rows) (None: all N). bias_partial:
-    [B * attention_bias_rows(N, path)][3D] f32. workspace: >= attention_workspace_elems floats
+    [B * attention_bias_rows(N, hd, path)][3D] f32. workspace: >= attention_workspace_elems floats
     (allocated here when None and the path needs one)."""
     _chk(workspace, F32, "workspace")
     need = attention_workspace_elems(B, N, H, path)
