@@ -25,7 +25,7 @@ for _ in range(3):
     ops.attention_bwd(qkv, o, do, lse, dqkv, B, N, H, hd, hd ** -0.5, bias_partial=bp, q_rows=nq)
 torch.cuda.synchronize()
 lib = _lib.load()
-buf = (ctypes.c_ulonglong * 64)()
+buf = (ctypes.c_ulonglong * 128)()
 lib.vit_attn_stamps(buf)
 names = ["wait_vm", "barrier_a", "stage1", "barrier_1_2", "stage2_prologue", "stage2", "bias", "next"]
 for w in range(2):
@@ -36,3 +36,11 @@ for w in range(2):
         d = [seq[k + 1] - seq[k] for k in range(7)]
         nxt = buf[w * 32 + (it + 1) * 8] - t[6] if it < 3 else 0
         print(f"wave {'0' if w == 0 else '7'} item {it}: " + " ".join(f"{n}={v}" for n, v in zip(names, d + [nxt])))
+names1 = ["q_do_lse_reads", "s_dp_products", "delta", "dq_products"]
+for w in range(2):
+    for it in range(4):
+        t = [buf[64 + w * 32 + it * 8 + k] for k in range(5)]
+        t2 = buf[w * 32 + it * 8 + 2]  # after barrier (a)
+        t7 = buf[64 + w * 32 + it * 8 + 7]  # after the DMA issue
+        print(f"wave {'0' if w == 0 else '7'} item {it} first strip: dma_issue={t7 - t2} to_strip={t[0] - t7} " +
+              " ".join(f"{n}={t[k + 1] - t[k]}" for k, n in enumerate(names1)))

@@ -46,9 +46,24 @@ __device__ unsigned long long g_attn_stamps[2][4][8];
       if (lane == 0) g_attn_stamps[wave == 7][it][k] = t_;                                                  \
     }                                                                                                       \
   } while (0)
+// sub-phases of the wave's first strip of each item (stage 1)
+__device__ unsigned long long g_attn_stamps2[2][4][8];
+#define STAMP1(k)                                                                                           \
+  do {                                                                                                      \
+    if (blockIdx.x == 0 && (wave == 0 || wave == 7) && it < 4 && qt == wave) {                              \
+      unsigned long long t_;                                                                                \
+      __builtin_amdgcn_sched_barrier(0);                                                                    \
+      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");                          \
+      __builtin_amdgcn_sched_barrier(0);                                                                    \
+      if (lane == 0) g_attn_stamps2[wave == 7][it][k] = t_;                                                 \
+    }                                                                                                       \
+  } while (0)
 #else
 #define STAMP(k) \
   do {           \
+  } while (0)
+#define STAMP1(k) \
+  do {            \
   } while (0)
 #endif
 
@@ -223,7 +238,7 @@ __global__ void __launch_bounds__(PB_NW * 64, 1) attn_bwd_pers_kernel(const bf16
     lds_t* const Ln = (lds_t*)(SLOT ? ls0_s : ls1_s);
     const int b = item / H, h = item % H;
     bf16_t* const dqb = dqkv + (long)b * N * rs + (long)h * hd;
-    const int next = item + gridDim.x;
+    const int next = __builtin_amdgcn_readfirstlane(item + (int)gridDim.x);
 
     // (a) this item's K / V, Q / dO, lse landed (every wave drains its own DMAs, then the barrier), and
     // every wave is past the previous item's stage 2 / bias sums (the last readers of the other slot)
@@ -234,6 +249,12 @@ __global__ void __launch_bounds__(PB_NW * 64, 1) attn_bwd_pers_kernel(const bf16
     STAMP(2);
     // (b) the next item's Q / dO / lse into the other slot
     if (next < nitems) dma_qo(Qn, Ln, next);
+#ifdef VIT_ATTN_STAMPS
+    {
+      const int qt = wave;  // (STAMP1's first-strip filter)
+      STAMP1(7);
+    }
+#endif
 
     // ---- stage 1: delta, dS, dQ per 16-query strip ----
     float bq16[16];  // the wave's dQ column partials: [4 dt + r] for column 16 dt + 4 g + r (summed over lanes i later)
@@ -248,6 +269,7 @@ __global__ void __launch_bounds__(PB_NW * 64, 1) attn_bwd_pers_kernel(const bf16
           if (dt * 16 < hd) st_b64(rdq, offs + dt * 32, uint2{0u, 0u});
         continue;
       }
+      STAMP1(0);
       v8bf qf[KK], df[KK];
 #pragma unroll
       for (int kk = 0; kk < KK; ++kk) {
@@ -255,6 +277,7 @@ __global__ void __launch_bounds__(PB_NW * 64, 1) attn_bwd_pers_kernel(const bf16
         df[kk] = __builtin_bit_cast(v8bf, lds_ld<v8s>(Oi + qt * T + L.row[kk]));
       }
       const float ls = q < N ? lse_s[q] * LOG2E : 1e30f;  // padded queries: P = 2^-1e30 = 0
+      STAMP1(1);
       v4f P[NKT], DP[NKT];
       float dlr[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -282,11 +305,13 @@ __global__ void __launch_bounds__(PB_NW * 64, 1) attn_bwd_pers_kernel(const bf16
         }
         DP[kt] = dpt;
       }
+      STAMP1(2);
       float dl = (dlr[0] + dlr[1]) + (dlr[2] + dlr[3]);
       dl += __shfl_xor(dl, 16, 64);
       dl += __shfl_xor(dl, 32, 64);
       if (q >= N) dl = 0.f;
       if (g == 0) dlt_s[q] = dl;
+      STAMP1(3);
       v4f dq[HD / 16];
 #pragma unroll
       for (int dt = 0; dt < HD / 16; ++dt) dq[dt] = v4f{0.f, 0.f, 0.f, 0.f};
@@ -315,6 +340,7 @@ __global__ void __launch_bounds__(PB_NW * 64, 1) attn_bwd_pers_kernel(const bf16
 #pragma unroll
         for (int dt = 0; dt < HD / 16; ++dt) dq[dt] = mfma16(lds_tr(Ki + (NKT - 1) * T + L.tr[dt]), bD, dq[dt]);
       }
+      STAMP1(4);
       {
         uint2 pk[HD / 16];
 #pragma unroll
@@ -499,7 +525,7 @@ __global__ void __launch_bounds__(PB_NW * 64, 1) attn_bwd_pers_kernel(const bf16
       }
     }
     STAMP(6);
-    item = next;
+    item = __builtin_amdgcn_readfirstlane(next);  // (uniform: scalar branches and addresses)
     ++it;
   };
   while (true) {
@@ -548,8 +574,10 @@ size_t vit_attn_bwd_pers_lds(int N, int hd) {
 }
 
 #ifdef VIT_ATTN_STAMPS
-extern "C" int vit_attn_stamps(unsigned long long* out) {  // 64 values: [wave 0 / 7][item][point]
-  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_attn_stamps), sizeof(g_attn_stamps));
+extern "C" int vit_attn_stamps(unsigned long long* out) {  // 128 values: [2][wave 0 / 7][item][point]
+  int e = (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_attn_stamps), sizeof(g_attn_stamps));
+  if (e) return e;
+  return (int)hipMemcpyFromSymbol(out + 64, HIP_SYMBOL(g_attn_stamps2), sizeof(g_attn_stamps2));
 }
 #endif
 
