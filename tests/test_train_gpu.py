@@ -249,3 +249,37 @@ def test_train_n_gpu_2_starts_two_ranks():
     assert r.stdout.count("val_acc1") == 2  # 2 epochs, printed by rank 0 only
     losses = [float(l.split("Loss: ")[1].split()[0]) for l in r.stdout.splitlines() if l.startswith("Train Epoch")]
     assert len(losses) == 2 and all(math.isfinite(v) for v in losses)
+
+
+def test_eval_accuracy_matches_oracle_at_577_tokens():
+    """vitmi.eval.evaluate's top-1 / top-5 (src/eval.py:56-75 with src/utils.py:28-41's accuracy) against the
+    oracle's accuracy() on the oracle's fp32 logits: a 577-token model (96 px / patch 4, the 384-px token
+    count, so the K/V-tiled attention runs), the exact fp32 forward, 3 batches of 8 over 10 classes.
+    The seeded inputs are checked to hold no near-tie at the top-1 / top-5 cut (margin > 1e-3 of the
+    logit scale), so the hit counts must agree exactly."""
+    from oracle.vit_oracle import ViTConfig, accuracy, forward, init_params, tame_params
+    from vitmi.eval import evaluate
+    from vitmi.model import VisionTransformer
+    cfg = ViTConfig(image_size=96, patch_size=4, emb_dim=64, mlp_dim=128, num_heads=2, num_layers=2, num_classes=10)
+    params = tame_params(init_params(cfg, seed=7))
+    torch.manual_seed(7)
+    m = VisionTransformer(image_size=(96, 96), patch_size=(4, 4), emb_dim=64, mlp_dim=128, num_heads=2,
+                          num_layers=2, num_classes=10, attn_dropout_rate=0.0, dropout_rate=0.0)
+    m.load_state_dict(params)
+    m = m.cuda()
+    m.precision = "fp32"
+    g = torch.Generator().manual_seed(3)
+    batches = [(torch.randn(8, 3, 96, 96, generator=g), torch.randint(0, 10, (8,), generator=g)) for _ in range(3)]
+    acc1, acc5 = evaluate(m, batches, "cuda")
+    r1, r5 = [], []
+    for x, y in batches:
+        logits = forward(params, x, cfg)
+        top = logits.sort(dim=1, descending=True).values
+        scale = float(logits.abs().max())
+        for k in (1, 5):
+            assert float((top[:, k - 1] - top[:, k]).min()) > 1e-3 * scale, "near-tie in the seeded inputs"
+        a1, a5 = accuracy(logits, y, topk=(1, 5))
+        r1.append(float(a1))
+        r5.append(float(a5))
+    ref1, ref5 = sum(r1) / 3, sum(r5) / 3
+    assert abs(acc1 - ref1) < 1e-4 and abs(acc5 - ref5) < 1e-4, (acc1, acc5, ref1, ref5)
