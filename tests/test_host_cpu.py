@@ -83,3 +83,17 @@ def test_cpu_submodule_forwards_refuse():
         MlpBlock(64, 128, 64, dropout_rate=0.0)(torch.randn(1, 5, 64))
     with pytest.raises(RuntimeError, match="MI355X HIP path only"):
         LinearGeneral((64,), (2, 32))(torch.randn(1, 5, 64), dims=([2], [0]))
+
+
+def test_splitk_factor_one_wave_splits_and_h14_tail():
+    """split-K choice of the weight gradients (engine._splitk / ops.wgrad): the ViT-B/16 and L/16 splits the
+    sweeps picked (one wave of 256 x 256 workgroups), and ViT-H/14 bs 128's fc1 / fc2 weight gradients
+    (100 tiles) at 5 splits = 500 workgroups rather than 3 = 300 (a second wave 17% full)."""
+    from vitmi.ops import splitk_factor as f
+    assert [f(3072, 768, 50432), f(768, 3072, 50432), f(2304, 768, 50432), f(768, 768, 50432)] == [7, 7, 9, 28]
+    assert [f(4096, 1024, 12608), f(3072, 1024, 12608), f(1024, 1024, 12608)] == [4, 5, 16]
+    assert [f(5120, 1280, 32896), f(1280, 5120, 32896), f(3840, 1280, 32896)] == [5, 5, 3]
+    assert f(768, 768, 256) == 1 and f(768, 768, 64) == 1        # at least 8 k-tiles per split
+    for M, N, K in [(768, 768, 50432), (64, 64, 1 << 20), (5120, 1280, 32896)]:
+        s = f(M, N, K)
+        assert 1 <= s <= 32 and (s == 1 or K // 64 // s >= 8)

@@ -384,12 +384,10 @@ class ViTEngine:
         return a
 
     def _splitk(self, M, N, K, z=1):
-        """split-K factor for a weight-gradient GEMM (K = tokens) on the 256x256 ping-pong tile
-        (one workgroup per CU): one wave of tiles x splits over the 256 CUs, at least 8 k-tiles per
-        split (tools/gemm_bench.py: fc1/fc2 wgrad at split 7 = 36 x 7 = 252 workgroups)."""
-        tiles = ((M + 255) // 256) * ((N + 255) // 256) * z
-        nkt = K // 64
-        return max(1, min(round(_WGRAD_TARGET / tiles), nkt // 8, 32))
+        """split-K factor for a weight-gradient GEMM (K = tokens) on the 256x256 ping-pong tile (one
+        workgroup per CU): ops.splitk_factor over _WGRAD_TARGET CUs (tools/gemm_bench.py: fc1/fc2 wgrad
+        at split 7 = 36 x 7 = 252 workgroups)."""
+        return ops.splitk_factor(M, N, K, z, _WGRAD_TARGET)
 
     def _workspace(self, numel):
         if self._ws is None or self._ws.numel() < numel:

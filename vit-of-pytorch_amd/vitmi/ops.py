@@ -347,16 +347,34 @@ def zero_(t):
     check(lib().vit_zero(_p(t), t.numel() * t.element_size(), _stream()), "vit_zero")
 
 
+def splitk_factor(M, N, K, batch=1, cus=256):
+    """split-K factor of a weight-gradient GEMM (K = tokens) on `cus` compute units: the split with the
+    least modelled time, ceil(tiles*s / slots) waves of 1/s of a tile's k-range each plus the f32 slab
+    traffic (write + fixed-order reduce) of s slabs; at least 8 k-tiles per split, at most 32. One
+    256 x 256 workgroup per CU (128 x 128 below 256 rows or columns: two). ViT-B/16 keeps its one-wave
+    splits (fc1 / fc2 7, qkv 9, out-proj 28); ViT-H/14 at bs 128 (fc1 / fc2: 100 tiles) takes 5 (500
+    workgroups, 1.95 waves) instead of 3 (300 workgroups: a second wave 17% full)."""
+    tile = 256 if M >= 256 and N >= 256 else 128
+    slots = cus if tile == 256 else 2 * cus
+    tiles = -(-M // tile) * -(-N // tile) * batch
+    smax = max(1, min((K // 64) // 8, 32))
+    t_tile = 2.0 * tile * tile * K / 4.0e12        # one tile's k-range on one CU at ~0.4 of the MFMA peak
+    slab = 2.0 * M * N * 4 * batch / 5.0e12        # one f32 slab written and read back
+    best, best_t = 1, None
+    for s in range(1, smax + 1):
+        t = -(-tiles * s // slots) * t_tile / s + s * slab
+        if best_t is None or t < best_t * (1 - 1e-9):
+            best, best_t = s, t
+    return best
+
+
 def wgrad(A, lda, B, ldb, M, N, K, out, ldo, accumulate=False, batch=1, a_bs=0, b_bs=0, out_bs=0, target=256):
     """Weight gradient out[z] ([M][N] f32, row stride ldo) (+)= sum_t A[t][m] B[t][n] over K token rows
     (both operands token-major, i.e. M/N-contiguous; K a multiple of 64, rows past the data zero):
-    split-K over the tokens into f32 slabs sized to about one wave of `target` workgroups, then the
-    fixed-order vit_splitk_reduce (deterministic; accumulate adds into `out`)."""
+    split-K over the tokens into f32 slabs (splitk_factor over `target` CUs), then the fixed-order
+    vit_splitk_reduce (deterministic; accumulate adds into `out`)."""
     from ._lib import EPI_SPLITK, MN_CONTIG
-    tile = 256 if M >= 256 and N >= 256 else 128
-    tiles = -(-M // tile) * -(-N // tile) * batch
-    nkt = K // 64
-    s = max(1, min(round(target / tiles), max(1, nkt // 8), 32))
+    s = splitk_factor(M, N, K, batch, target)
     ws = torch.empty(batch * s * M * N, device=out.device, dtype=F32)
     gemm(A, B, ws, M, N, K, a_layout=MN_CONTIG, b_layout=MN_CONTIG, lda=lda, ldb=ldb, ldc=N, epilogue=EPI_SPLITK,
          batch=batch, a_bs=a_bs, b_bs=b_bs, split_k=s)
