@@ -1,7 +1,7 @@
 // Standalone GEMM diagnostic (not part of the product library): times vit_gemm_bf16 on one shape
 // and, in the stamped build, prints the per-slot timeline of one ping-pong workgroup.
 //   hipcc -O3 -std=c++17 --offload-arch=gfx950 -DVIT_GEMM_STAMPS tools/gemm_diag.hip -o tools/gemm_diag
-//   tools/gemm_diag M N K tile [epi] [wg] [a_layout b_layout]
+//   tools/gemm_diag M N K tile [epi] [wg] [a_layout b_layout] [split]
 #include "../vit-of-pytorch_amd/csrc/capi.hip"
 #include "../vit-of-pytorch_amd/csrc/gemm.hip"
 #include "../vit-of-pytorch_amd/csrc/gemm_e0.hip"
@@ -42,7 +42,7 @@ __global__ void fill_kernel(unsigned short* p, long n, unsigned seed) {
 
 int main(int argc, char** argv) {
   if (argc < 5) {
-    fprintf(stderr, "usage: %s M N K tile [epi=1] [wg=-1] [a_layout=0] [b_layout=0]\n", argv[0]);
+    fprintf(stderr, "usage: %s M N K tile [epi=1] [wg=-1] [a_layout=0] [b_layout=0] [split=1]\n", argv[0]);
     return 2;
   }
   const long M = atol(argv[1]), N = atol(argv[2]), K = atol(argv[3]);
@@ -50,11 +50,12 @@ int main(int argc, char** argv) {
   const int epi = argc > 5 ? atoi(argv[5]) : VIT_EPI_BF16;
   const int wg = argc > 6 ? atoi(argv[6]) : -1;
   const int al = argc > 7 ? atoi(argv[7]) : VIT_K_CONTIG, bl = argc > 8 ? atoi(argv[8]) : VIT_K_CONTIG;
+  const int split = argc > 9 ? atoi(argv[9]) : 1;
   unsigned short *A, *B, *C, *C2;
   float* bias;
   CK(hipMalloc(&A, M * K * 2));
   CK(hipMalloc(&B, N * K * 2));
-  CK(hipMalloc(&C, M * N * 4));
+  CK(hipMalloc(&C, M * N * 4 * (long)split));
   CK(hipMalloc(&C2, M * N * 2));
   CK(hipMalloc(&bias, N * 4));
   CK(hipMemset(bias, 0, N * 4));
@@ -66,7 +67,7 @@ int main(int argc, char** argv) {
   a.A = A; a.lda = al == VIT_K_CONTIG ? K : M; a.a_layout = al;
   a.B = B; a.ldb = bl == VIT_K_CONTIG ? K : N; a.b_layout = bl;
   a.C = C; a.ldc = N; a.C2 = C2; a.ldc2 = N; a.bias = bias;
-  a.batch = 1; a.split_k = 1; a.epilogue = epi; a.tile = tile;
+  a.batch = 1; a.split_k = split; a.epilogue = epi; a.tile = tile;
   for (int i = 0; i < 5; ++i)
     if (vit_gemm_bf16(&a, 0)) { fprintf(stderr, "gemm: %s\n", vit_last_error()); return 1; }
   hipEvent_t e0, e1;

@@ -93,6 +93,33 @@ __device__ __forceinline__ v8s read_frag(const char* smem, int lds_off, int r0, 
   }
 }
 
+// M/N-contiguous fragment reads of gemm_pp_kernel by inline asm. With the k-tile buffers in one LDS
+// array indexed at run time, hipcc cannot tell a ds_read_b64_tr_b16 of k-tile j from the LDS-DMA of
+// k-tile j+1 just issued into the other buffer, and its waitcnt pass put an s_waitcnt vmcnt(0) in
+// front of the reads: every read slot waited for the DMA it had just issued to land (tools/gemm_diag
+// stamps of the split-K weight gradient: ~2 550 of ~3 900 cycles per k-tile). The asm reads are not
+// tracked by that pass; the caller ends its read phase with an explicit lgkmcnt(0) and a
+// sched_barrier before any use. `a` = the fragment's lane address without the k offset (swz_mn of
+// rows 8g + q and 8g + q + 4 + 32 kk is the same for every kk, so kk and the hi half are immediates).
+template <int ROWS>
+__device__ __forceinline__ uint32_t frag_tr_lane_off(int r0, int lane) {
+  constexpr int RB = ROWS * 2;
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  const int ra = 8 * g + q;
+  return (uint32_t)(ra * RB + (((r0 + 4 * p) * 2) ^ (swz_mn(ra) << 5)));
+}
+template <int ROWS, int KKI>
+__device__ __forceinline__ v8s read_frag_tr_asm(uint32_t a) {
+  constexpr int RB = ROWS * 2;
+  v4s lo, hi;
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(lo) : "v"(a), "i"(KKI * 32 * RB));
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(hi) : "v"(a), "i"(KKI * 32 * RB + 4 * RB));
+  v8s r;
+  r.lo = lo;
+  r.hi = hi;
+  return r;
+}
+
 template <int N>
 __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
@@ -790,10 +817,10 @@ __global__ void __launch_bounds__(WM* WN * 64, (gemm_min_waves<BM, BN, BK, STAGE
 // slots separated by workgroup barriers. In every slot one group reads the fragments of a 64-deep
 // k-tile from LDS while the other group multiplies the fragments it read in the previous slot, so on
 // each SIMD (one wave of each group) LDS reads and MFMA chains of the two waves alternate instead of
-// serialising. Two LDS k-tile buffers: the LDS-DMA of k-tile u+1 is issued at the start of the slot
-// in which group 0 starts on k-tile u (both groups are done reading k-tile u-1 from that buffer) and
-// is waited for at the end of the following slot, before group 0 first reads it: two slots of flight,
-// raw s_barrier (no vmcnt(0) drain at the barriers in between).
+// serialising. Two LDS k-tile buffers: each group issues its half of the LDS-DMA of k-tile u+1 at
+// the end of its read slot of k-tile u (group 0 in slot 2u, group 1 in slot 2u-1 ... k-tile u-1's
+// buffer, which both groups have finished reading), and it is waited for at the end of slot 2u+1,
+// before group 0 first reads it; raw s_barrier (no vmcnt(0) drain at the barriers in between).
 // Epilogue: wave-private fp32 staging in the then idle LDS (32 rows per pass), 8-column chunks.
 // Outstanding-DMA wait with a runtime count of younger k-tiles (0 .. L-1) and compile-time vmcnt.
 template <int LPT, int L>
@@ -908,16 +935,43 @@ __global__ void __launch_bounds__(512) gemm_pp_kernel(const GemmDev p) {
     stage_tile<BM, BK, AK, NWAVE>(smem, buf, rsA, p.lda, kt0 + t, wave, lane);
     stage_tile<BN, BK, BKC, NWAVE>(smem, buf + A_BYTES, rsB, p.ldb, kt0 + t, wave, lane);
   };
+  // both operands M/N-contiguous (the weight gradients): asm transpose reads (frag_tr_lane_off)
+  constexpr bool TR_ASM = !AK && !BKC && BK == 64;
+  uint32_t a_lane[FM], b_lane[FN];
+  if constexpr (TR_ASM) {
+    const uint32_t s0 = (uint32_t)(uintptr_t)LDS_PTR(char, smem);
+#pragma unroll
+    for (int i = 0; i < FM; ++i) a_lane[i] = s0 + frag_tr_lane_off<BM>(wm0 + i * 16, lane);
+#pragma unroll
+    for (int jn = 0; jn < FN; ++jn) b_lane[jn] = s0 + A_BYTES + frag_tr_lane_off<BN>(wn0 + jn * 16, lane);
+  }
   auto mem = [&](int j) {
     const int cur = (j % NBUF) * STAGE;
+    if constexpr (TR_ASM) {
+      const uint32_t c = __builtin_amdgcn_readfirstlane(cur);
 #pragma unroll
-    for (int kk = 0; kk < KK; ++kk) {
+      for (int jn = 0; jn < FN; ++jn) {
+        bfr[0][jn] = read_frag_tr_asm<BN, 0>(b_lane[jn] + c);
+        bfr[1][jn] = read_frag_tr_asm<BN, 1>(b_lane[jn] + c);
+      }
 #pragma unroll
-      for (int jn = 0; jn < FN; ++jn) bfr[kk][jn] = read_frag<BN, BK, BKC>(smem, cur + A_BYTES, wn0 + jn * 16, kk, lane);
+      for (int i = 0; i < FM; ++i) {
+        af[0][i] = read_frag_tr_asm<BM, 0>(a_lane[i] + c);
+        af[1][i] = read_frag_tr_asm<BM, 1>(a_lane[i] + c);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+    } else {
 #pragma unroll
-      for (int i = 0; i < FM; ++i) af[kk][i] = read_frag<BM, BK, AK>(smem, cur, wm0 + i * 16, kk, lane);
+      for (int kk = 0; kk < KK; ++kk) {
+#pragma unroll
+        for (int jn = 0; jn < FN; ++jn)
+          bfr[kk][jn] = read_frag<BN, BK, BKC>(smem, cur + A_BYTES, wn0 + jn * 16, kk, lane);
+#pragma unroll
+        for (int i = 0; i < FM; ++i) af[kk][i] = read_frag<BM, BK, AK>(smem, cur, wm0 + i * 16, kk, lane);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   };
   auto compute = [&]() {
     if (p.prio) __builtin_amdgcn_s_setprio(1);  // the MFMA cluster ahead of the partner group's issue
@@ -941,15 +995,16 @@ __global__ void __launch_bounds__(512) gemm_pp_kernel(const GemmDev p) {
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
 
-  // slot s: group g reads k-tile j in slot 2j+g and multiplies it in slot 2j+g+1. At the start of
-  // slot 2u, k-tile u+L goes into the buffer k-tile u-1 used (read by group 1 in slot 2u-1); at the
-  // end of slot 2u+1 k-tile u+1 has landed (group 0 reads it in slot 2u+2). The two groups run
+  // slot s: group g reads k-tile j in slot 2j+g and multiplies it in slot 2j+g+1. After its reads of
+  // k-tile j, a group issues its half of k-tile j+L into the buffer of k-tile j+L-NBUF (group 1: of
+  // k-tile j+1+L into k-tile j's buffer, which group 0 read in slot 2j); at the end of slot 2u+1
+  // k-tile u+1 has landed (group 0 reads it in slot 2u+2). The two groups run
   // separate straight-line loops (a slot-role branch inside one loop makes the compiler copy the
   // accumulators at every join).
-  auto end_odd = [&](int u) {  // end of slot 2u+1
-    const int issued = u + L < nk ? u + L : nk - 1;
+  auto end_odd = [&](int u, int ahead) {  // end of slot 2u+1; this wave has issued k-tiles up to u + ahead
+    const int issued = u + ahead < nk ? u + ahead : nk - 1;
     __builtin_amdgcn_sched_barrier(0);
-    wait_tiles<LPT, L>(issued - u - 1);
+    wait_tiles<LPT, L + 1>(issued - u - 1);
     asm volatile("s_barrier" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
   };
@@ -959,15 +1014,20 @@ __global__ void __launch_bounds__(512) gemm_pp_kernel(const GemmDev p) {
     __builtin_amdgcn_sched_barrier(0);
   };
   PP_STAMP();
+  // Both groups issue their DMA half at the END of their read slot (after the fragment reads): the
+  // buffer they refill held the k-tile both groups have finished reading. Issued at the start of a
+  // slot instead, group 1's half queued behind group 0's in the same slot and held group 1's MFMAs
+  // back ~1 200 cycles per k-tile (tools/gemm_diag stamps, profiles/r03/wgrad_slots_summary.txt:
+  // split-K fc1 weight gradient 3 780 -> 3 130 cycles per k-tile, step +3.5%).
   if (grp == 0) {
     for (int j = 0; j < nk; ++j) {
-      if (j + L < nk) issue(j + L);  // slot 2j
-      mem(j);
+      mem(j);  // slot 2j
+      if (j + L < nk) issue(j + L);
       PP_STAMP();
       end_even();
       PP_STAMP();
       compute();  // slot 2j+1
-      end_odd(j);
+      end_odd(j, L);
       PP_STAMP();
     }
   } else if (nk > 0) {
@@ -976,16 +1036,16 @@ __global__ void __launch_bounds__(512) gemm_pp_kernel(const GemmDev p) {
     PP_STAMP();
     for (int j = 0; j < nk - 1; ++j) {
       mem(j);  // slot 2j+1
+      if (j + 1 + L < nk) issue(j + 1 + L);
       PP_STAMP();
-      end_odd(j);
+      end_odd(j, L + 1);
       PP_STAMP();
-      if (j + 1 + L < nk) issue(j + 1 + L);  // slot 2j+2
-      compute();
+      compute();  // slot 2j+2
       end_even();
       PP_STAMP();
     }
     mem(nk - 1);  // slot 2nk-1
-    end_odd(nk - 1);
+    end_odd(nk - 1, L);
     compute();  // slot 2nk: LDS is free from here on
   }
   PP_STAMP();
