@@ -157,9 +157,9 @@ extern "C" int vit_gemm_bf16(const vit_gemm_args* a, vit_stream_t stream) {
       return e ? atoi(e) : 1;
     }();
     d.split_xcd = env_sx;
-    static const int env_prio = [] {
+    static const int env_prio = [] {  // on by default since round 3: +0.35% step (profiles/r03/wgrad_cfg_prio_ab.txt)
       const char* e = getenv("VIT_GEMM_PRIO");
-      return e ? atoi(e) : 0;
+      return e ? atoi(e) : 1;
     }();
     d.prio = env_prio;
   }

@@ -936,7 +936,7 @@ __global__ void __launch_bounds__(512) gemm_pp_kernel(const GemmDev p) {
     stage_tile<BN, BK, BKC, NWAVE>(smem, buf + A_BYTES, rsB, p.ldb, kt0 + t, wave, lane);
   };
   // both operands M/N-contiguous (the weight gradients): asm transpose reads (frag_tr_lane_off)
-  constexpr bool TR_ASM = !AK && !BKC && BK == 64;
+  constexpr bool TR_ASM = !AK && !BKC;
   uint32_t a_lane[FM], b_lane[FN];
   if constexpr (TR_ASM) {
     const uint32_t s0 = (uint32_t)(uintptr_t)LDS_PTR(char, smem);
@@ -952,12 +952,12 @@ __global__ void __launch_bounds__(512) gemm_pp_kernel(const GemmDev p) {
 #pragma unroll
       for (int jn = 0; jn < FN; ++jn) {
         bfr[0][jn] = read_frag_tr_asm<BN, 0>(b_lane[jn] + c);
-        bfr[1][jn] = read_frag_tr_asm<BN, 1>(b_lane[jn] + c);
+        if constexpr (KK > 1) bfr[KK - 1][jn] = read_frag_tr_asm<BN, 1>(b_lane[jn] + c);
       }
 #pragma unroll
       for (int i = 0; i < FM; ++i) {
         af[0][i] = read_frag_tr_asm<BM, 0>(a_lane[i] + c);
-        af[1][i] = read_frag_tr_asm<BM, 1>(a_lane[i] + c);
+        if constexpr (KK > 1) af[KK - 1][i] = read_frag_tr_asm<BM, 1>(a_lane[i] + c);
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
