@@ -135,10 +135,11 @@ __device__ __forceinline__ void st_b64(__amdgpu_buffer_rsrc_t r, int off, const 
 // Each piece gets its own (scalar) descriptor based at its first row, so every piece uses the same one
 // lane-offset VGPR (per-piece offsets get spilled, and hipcc then waits vmcnt(0) on each reload, i.e. on
 // every earlier piece); the record count clips rows past N and columns past hd of row N - 1 to zero.
+// nwv = 1: this wave issues every piece (first ignored).
 template <int HD>
 __device__ __forceinline__ void dma_pair(lds_t* imga, const bf16_t* basea, long stridea, lds_t* imgb,
                                          const bf16_t* baseb, long strideb, int rows, int N, int hd, int first,
-                                         int wave, int lane) {
+                                         int wave, int lane, int nwv = PB_NW) {
   constexpr int RPP = 1024 / (HD * 2);  // image rows per piece
   constexpr int CPR = HD / 8;           // 16-B chunks per row
   static_assert(RPP % 8 == 0, "the swizzle period divides a piece");
@@ -150,9 +151,9 @@ __device__ __forceinline__ void dma_pair(lds_t* imga, const bf16_t* basea, long 
   const bool colok = ch * 8 < hd;
   const int offa = colok ? (int)(lr * stridea * 2 + ch * 16) : 0x40000000;
   const int offb = colok ? (int)(lr * strideb * 2 + ch * 16) : 0x40000000;
-  int p = wave - first;
+  int p = nwv == 1 ? 0 : wave - first;
   if (p < 0) p += PB_NW;
-  for (; p < 2 * npc; p += PB_NW) {
+  for (; p < 2 * npc; p += nwv) {
     const bool isb = p >= npc;
     const int q = isb ? p - npc : p;
     const long stride = isb ? strideb : stridea;
@@ -165,10 +166,16 @@ __device__ __forceinline__ void dma_pair(lds_t* imga, const bf16_t* basea, long 
 
 // LDS-DMA of n (<= NP) consecutive floats (an item's lse row) into dst; past n reads zero
 template <int NP>
-__device__ __forceinline__ void dma_floats(lds_t* dst, const float* src, int n, int wave, int lane) {
+__device__ __forceinline__ void dma_floats(lds_t* dst, const float* src, int n, int wave, int lane, bool all = false) {
   constexpr int PCS = (NP * 4 + 1023) / 1024;
   const __amdgpu_buffer_rsrc_t r = make_rsrc(uniform_ptr(src), (uint32_t)n * 4);
-  if (wave < PCS) __builtin_amdgcn_raw_ptr_buffer_load_lds(r, dst + wave * 1024, 16, wave * 1024 + lane * 16, 0, 0, 0);
+  if (all) {
+#pragma unroll
+    for (int k = 0; k < PCS; ++k)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(r, dst + k * 1024, 16, k * 1024 + lane * 16, 0, 0, 0);
+  } else if (wave < PCS) {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, dst + wave * 1024, 16, wave * 1024 + lane * 16, 0, 0, 0);
+  }
 }
 
 template <int HD, int NKT>
@@ -215,10 +222,14 @@ __global__ void __launch_bounds__(PB_NW * 64, 1) attn_bwd_pers_kernel(const bf16
   auto qkv_of = [&](int it_) { return qkv + (long)(it_ / H) * N * rs + (long)(it_ % H) * hd; };
   auto dout_of = [&](int it_) { return dout + (long)(it_ / H) * N * D + (long)(it_ % H) * hd; };
   // Q / dO / lse of item it_ into a Q / dO slot (waves 0.. take the pieces; the lse piece goes to the last)
-  auto dma_qo = [&](lds_t* qo, lds_t* ls, int it_) {
-    dma_floats<NP>(ls, lse + (long)it_ * N, N, wave, lane);
-    dma_pair<HD>(qo, qkv_of(it_), rs, qo + IMG, dout_of(it_), D, qrows, N, hd, 0, wave, lane);
+  auto dma_qo = [&](lds_t* qo, lds_t* ls, int it_, bool single) {
+    dma_floats<NP>(ls, lse + (long)it_ * N, N, wave, lane, single);
+    dma_pair<HD>(qo, qkv_of(it_), rs, qo + IMG, dout_of(it_), D, qrows, N, hd, 0, wave, lane, single ? 1 : NW);
   };
+  // N <= 16 * NKT leaves at most (16 NKT + 31) / 32 key pairs for stage 2: below NW the last wave has none,
+  // and it alone issues the next item's Q / dO / lse DMA during stage 2 instead of every wave at the start
+  // of the item (where ~7 DMAs per wave cost 2 500-4 000 cycles of stage 1: attention stamps, round 3)
+  constexpr bool IDLE_LAST = (NKT * 16 + 31) / 32 < NW;
   auto dma_kv = [&](int it_) {
     const bf16_t* bq = qkv_of(it_);
     // all NP rows: the padding rows N.. of the images must be zeros (the last key tile reads them)
@@ -226,7 +237,7 @@ __global__ void __launch_bounds__(PB_NW * 64, 1) attn_bwd_pers_kernel(const bf16
   };
   // ---- prologue: everything of the first item
   dma_kv(item);
-  dma_qo((lds_t*)qo0_s, (lds_t*)ls0_s, item);
+  dma_qo((lds_t*)qo0_s, (lds_t*)ls0_s, item, false);
 
   int it = 0;
   auto body = [&](auto slot) {
@@ -248,7 +259,7 @@ __global__ void __launch_bounds__(PB_NW * 64, 1) attn_bwd_pers_kernel(const bf16
     lds_barrier();
     STAMP(2);
     // (b) the next item's Q / dO / lse into the other slot
-    if (next < nitems) dma_qo(Qn, Ln, next);
+    if (!IDLE_LAST && next < nitems) dma_qo(Qn, Ln, next, false);
 #ifdef VIT_ATTN_STAMPS
     {
       const int qt = wave;  // (STAMP1's first-strip filter)
@@ -383,6 +394,7 @@ __global__ void __launch_bounds__(PB_NW * 64, 1) attn_bwd_pers_kernel(const bf16
     // every wave has its K / V rows: the next item's K / V into the images, landing during stage 2
     lds_barrier();  // (its lgkmcnt(0): this wave's K / V reads are back)
     if (next < nitems) dma_kv(next);
+    if (IDLE_LAST && wave == NW - 1 && next < nitems) dma_qo(Qn, Ln, next, true);  // (b) of IDLE_LAST
     STAMP(7);
     float bk4[HD / 16][4], bv4[HD / 16][4];
 #pragma unroll
