@@ -198,8 +198,8 @@ def main():
     backend = None
     if world > 1:
         import torch.distributed as dist
-        backend = os.environ.get("VITMI_DIST_BACKEND", "nccl")
-        dist.init_process_group(backend, **({"device_id": dev} if backend == "nccl" else {}))
+        from vitmi.dist import init_process_group
+        backend = init_process_group(device=dev)
     # torch's "nccl" backend is RCCL on ROCm; any other backend is named as itself
     comm = {None: None, "nccl": "RCCL"}.get(backend, backend)
     if args.arch == "resvit_b16":

@@ -217,7 +217,10 @@ ATTN_CASES = [(2, 2, 2, 64, 0),  # (config C1: 2 tokens)
               (2, 577, 3, 64, 0), (1, 730, 2, 80, 0), (1, 321, 2, 64, 0),
               # more (image, head) items than CUs: the persistent backward's workgroups walk several items
               # (its Q / dO slots double as bias scratch: tiny N exercises the padded slot size)
-              (24, 197, 12, 64, 0), (23, 50, 12, 64, 0), (32, 2, 12, 64, 0), (30, 17, 12, 32, 0)]
+              (24, 197, 12, 64, 0), (23, 50, 12, 64, 0), (32, 2, 12, 64, 0), (30, 17, 12, 32, 0),
+              # hd <= 32 past 256 tokens: more key pairs than the persistent backward's 8 waves (two-stage
+              # kernel), and exactly 8 pairs (the persistent kernel with no idle wave)
+              (1, 300, 2, 32, 0), (2, 256, 2, 32, 0)]
 
 
 @pytest.mark.parametrize("B,N,H,hd,path", ATTN_CASES)

@@ -175,6 +175,43 @@ def test_flat_params_keep_grad_views_and_skip_unused():
     assert torch.allclose(a.grad, torch.full_like(a, 3.0))
 
 
+def test_adamw_state_dict_round_trip_and_gate_or():
+    """AdamW.state_dict() is torch.optim.AdamW's format (so it loads into torch's AdamW and back), and
+    load_state_dict() lands in the flat moment buffers that step() uses: a resumed optimizer continues the
+    trajectory of the original bit for bit. flat.gate ORs the flags of repeated forwards before a step."""
+    from vitmi.flat import _take_gate, gate
+    from vitmi.optim import AdamW
+    g = torch.Generator(device="cuda").manual_seed(3)
+    shapes = [(5, 7), (3,), (130,)]
+    ps = [torch.nn.Parameter(torch.randn(s, device="cuda", generator=g)) for s in shapes]
+    grads = [[torch.randn(s, device="cuda", generator=g) for s in shapes] for _ in range(4)]
+    opt = AdamW(ps, lr=1e-2, weight_decay=0.05)
+    for k in range(2):
+        opt.zero_grad()
+        for p, gr in zip(ps, grads[k]):
+            (p * gr).sum().backward()
+        opt.step()
+    sd = opt.state_dict()
+    ref = torch.optim.AdamW([torch.nn.Parameter(p.detach().clone()) for p in ps], lr=1e-2, weight_decay=0.05)
+    ref.load_state_dict(sd)  # torch accepts the format
+    qs = [torch.nn.Parameter(p.detach().clone()) for p in ps]
+    opt2 = AdamW(qs, lr=1e-2, weight_decay=0.05)
+    opt2.load_state_dict(sd)
+    for k in (2, 3):
+        for o, params in ((opt, ps), (opt2, qs)):
+            o.zero_grad()
+            for p, gr in zip(params, grads[k]):
+                (p * gr).sum().backward()
+            o.step()
+    for p, q in zip(ps, qs):
+        assert torch.equal(p.detach(), q.detach())
+    assert float(opt2.state_dict()["state"][0]["step"]) == 4.0
+    x = torch.nn.Parameter(torch.zeros(2, device="cuda"))
+    gate([x], torch.tensor(True, device="cuda"))
+    gate([x], torch.tensor(False, device="cuda"))
+    assert bool(_take_gate(x))
+
+
 def test_resvit_data_parallel_two_ranks(tmp_path):
     """Res-ViT DP (new: the reference is single-device): 2 ranks on one GPU over gloo, 4 images each,
     FlatGradAllReducer on the LoRA / router / approximator / head gradients, vitmi AdamW with the clip

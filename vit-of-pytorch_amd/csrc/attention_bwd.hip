@@ -579,6 +579,8 @@ hipError_t launch_pers(const bf16_t* qkv, const bf16_t* dout, const float* lse, 
 // kernel of attention.hip then runs)
 size_t vit_attn_bwd_pers_lds(int N, int hd) {
   if (hd > 64) return 0;
+  // stage 2 gives each wave one pair of 16-key tiles (kp = wave): keys past 32 * PB_NW would get no dK / dV
+  if ((N + 31) / 32 > PB_NW) return 0;
   const int HD = hd <= 32 ? 32 : 64;
   const int np = (N + 15) / 16 * 16;
   const size_t lds = (size_t)6 * np * HD * 2 + 2 * ((np * 4 + 1023) / 1024 * 1024) + np * 4;
@@ -600,11 +602,12 @@ hipError_t vit_attn_bwd_pers(const void* qkv, const void* dout, const float* lse
   const bf16_t *q = (const bf16_t*)qkv, *d = (const bf16_t*)dout;
   bf16_t* dq = (bf16_t*)dqkv;
   const int nkt = (N + 15) / 16;
+  if ((N + 31) / 32 > PB_NW) return hipErrorInvalidValue;  // see vit_attn_bwd_pers_lds
   if (hd <= 32) {
     switch (nkt) {
 #define C(n) \
   case n: return launch_pers<32, n>(q, d, lse, dq, bias_partial, B, N, H, hd, scale, nq, s);
-      C(1) C(2) C(3) C(4) C(5) C(6) C(7) C(8) C(9) C(10) C(11) C(12) C(13) C(14) C(15) C(16) C(17) C(18) C(19) C(20)
+      C(1) C(2) C(3) C(4) C(5) C(6) C(7) C(8) C(9) C(10) C(11) C(12) C(13) C(14) C(15) C(16)
 #undef C
     }
   } else {

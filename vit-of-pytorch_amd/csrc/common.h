@@ -1,5 +1,6 @@
 // Shared device helpers for the gfx950 (CDNA4) ViT training kernels.
 #pragma once
+#include <stdlib.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <string.h>
@@ -123,6 +124,17 @@ __device__ __forceinline__ float drop_mult1(const DropDev& d, long row, int col)
 namespace vit {
 void set_error(const char* fmt, ...);
 int check_hip(hipError_t e, const char* what);
+// Tuning / diagnostic knobs: the shipped library always takes the default; a build with
+// -DVIT_DIAG_KNOBS (tools/, never the product) reads them from the environment instead.
+inline int knob(const char* name, int dflt) {
+#ifdef VIT_DIAG_KNOBS
+  const char* e = getenv(name);
+  return e ? atoi(e) : dflt;
+#else
+  (void)name;
+  return dflt;
+#endif
+}
 }  // namespace vit
 
 #define VIT_CHECK_ARG(cond, ...)                 \

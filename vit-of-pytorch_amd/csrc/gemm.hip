@@ -36,10 +36,7 @@ int pick_tile(const vit_gemm_args* a) {
   //    it loses to the plain ping-pong, so those keep config 5 / 3.
   const bool ak = a->a_layout == VIT_K_CONTIG, bk = a->b_layout == VIT_K_CONTIG;
   if (a->epilogue == VIT_EPI_SPLITK && a->M >= 256 && a->N >= 256) {
-    static const int env_sk = [] {  // tuning override for the split-K weight gradients (5 .. 8)
-      const char* e = getenv("VIT_GEMM_SPLITK_CFG");
-      return e ? atoi(e) : 5;
-    }();
+    static const int env_sk = vit::knob("VIT_GEMM_SPLITK_CFG", 5);
     return env_sk == 6 || env_sk == 7 || env_sk == 8 || env_sk == 9 ? env_sk : 5;
   }
   if (a->M >= 1024 && a->N >= 256) {
@@ -49,10 +46,7 @@ int pick_tile(const vit_gemm_args* a) {
     // (short-K f32 residual outputs — the out-projection — also run here: 7418 vs 7385 img/s over
     // the 256x128 two-workgroup kernel, profiles/r02/gemm_epilogue_diag.txt; VIT_GEMM_RESID_PP2=0
     // restores that)
-    static const int env_rs = [] {
-      const char* e = getenv("VIT_GEMM_RESID_PP2");
-      return e ? atoi(e) : 1;
-    }();
+    static const int env_rs = vit::knob("VIT_GEMM_RESID_PP2", 1);
     if (ak && bk && (env_rs || !(a->epilogue == VIT_EPI_BIAS_RESID_F32 && a->K < 2048))) return 9;
     if (a->N >= 2048 && a->epilogue != VIT_EPI_GELU_BWD && a->epilogue != VIT_EPI_MUL_BF16) return 5;
     if (!bk && a->K >= 3072) return 5;
@@ -137,30 +131,15 @@ extern "C" int vit_gemm_bf16(const vit_gemm_args* a, vit_stream_t stream) {
     // tile order: groups of 8 tile rows, column-major inside, so the workgroups resident at once
     // share A row panels and B column panels in L2 (fc1 fwd 326 -> 306 us; VIT_GEMM_GROUP_M=1:
     // row-major)
-    static const int env_gm = [] {
-      const char* e = getenv("VIT_GEMM_GROUP_M");
-      return e ? atoi(e) : 8;
-    }();
-    static const int env_nt = [] {
-      const char* e = getenv("VIT_GEMM_NT");
-      return e ? atoi(e) : 0;
-    }();
+    static const int env_gm = vit::knob("VIT_GEMM_GROUP_M", 8);
+    static const int env_nt = vit::knob("VIT_GEMM_NT", 0);
     d.group_m = env_gm;
     d.nt = env_nt;
-    static const int env_diag = [] {
-      const char* e = getenv("VIT_GEMM_DIAG");
-      return e ? atoi(e) : 0;
-    }();
+    static const int env_diag = vit::knob("VIT_GEMM_DIAG", 0);
     d.diag = env_diag;
-    static const int env_sx = [] {
-      const char* e = getenv("VIT_GEMM_SPLIT_XCD");
-      return e ? atoi(e) : 1;
-    }();
+    static const int env_sx = vit::knob("VIT_GEMM_SPLIT_XCD", 1);
     d.split_xcd = env_sx;
-    static const int env_prio = [] {  // on by default since round 3: +0.35% step (profiles/r03/wgrad_cfg_prio_ab.txt)
-      const char* e = getenv("VIT_GEMM_PRIO");
-      return e ? atoi(e) : 1;
-    }();
+    static const int env_prio = vit::knob("VIT_GEMM_PRIO", 1);
     d.prio = env_prio;
   }
   if (a->col_partial) {
@@ -231,10 +210,7 @@ extern "C" int vit_gemm_bf16(const vit_gemm_args* a, vit_stream_t stream) {
         if (d.aux) g2.aux = (const char*)d.aux + r0 * a->ldaux * (a->epilogue == VIT_EPI_BIAS_RESID_F32 ? 4 : 2);
         g2.drop.row0 = (int)r0;  // dropout masks are indexed by the absolute row
         hipError_t e = run(cfg, g1);
-        static const int rem_cfg = [] {
-          const char* e = getenv("VIT_GEMM_REM_CFG");
-          return e ? atoi(e) : 0;
-        }();
+        static const int rem_cfg = vit::knob("VIT_GEMM_REM_CFG", 0);
         if (e == hipSuccess) e = run(rem_cfg >= 0 && rem_cfg <= 9 && rem_cfg != 1 ? rem_cfg : 0, g2);
         return vit::check_hip(e, "vit_gemm_bf16 launch");
       }

@@ -256,8 +256,8 @@ extern "C" int vit_layernorm_fwd(const float* x, int64_t ldx, const float* gamma
 
 static int64_t ln_bwd_blocks(int64_t rows) {
   static const int64_t cap = [] {
-    const char* e = getenv("VIT_LN_BWD_BLOCKS");
-    return e && atoi(e) > 0 ? (int64_t)atoi(e) : (int64_t)LN_BWD_MAX_BLOCKS;
+    const int k = vit::knob("VIT_LN_BWD_BLOCKS", 0);
+    return k > 0 ? (int64_t)k : (int64_t)LN_BWD_MAX_BLOCKS;
   }();
   int64_t b = (rows + 3) / 4;
   if (b > cap) b = cap;

@@ -173,8 +173,9 @@ extern "C" int vit_sqnorm_partial(const float* g, int64_t n, double* partial, in
 extern "C" int vit_adamw_prep(const double* partial, int32_t nparts, const float* used, float* steps, int32_t nseg,
                               float lr, float beta1, float beta2, float max_norm, float* table, float* norm_out,
                               vit_stream_t stream) {
-  VIT_CHECK_ARG(nseg >= 0 && (nseg == 0 || (used && steps && table)) && (partial == nullptr || nparts > 0),
-                "vit_adamw_prep: bad args");
+  VIT_CHECK_ARG(nseg >= 0 && (nseg == 0 || (used && steps && table)) &&
+                    (partial ? nparts > 0 && nparts <= 65536 : nparts == 0),
+                "vit_adamw_prep: bad args (partial needs nparts in 1..65536, no partial needs nparts 0)");
   VIT_CHECK_ARG(beta1 >= 0.0f && beta1 < 1.0f && beta2 >= 0.0f && beta2 < 1.0f, "vit_adamw_prep: betas must be in [0, 1)");
   hipLaunchKernelGGL(adamw_prep_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, partial, (int)nparts, used, steps,
                      (int)nseg, lr, beta1, beta2, max_norm, (float4*)table, norm_out);

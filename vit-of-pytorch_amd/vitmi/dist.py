@@ -22,8 +22,39 @@ the trade the reference's DataParallel never offered; off by default.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.distributed as dist
+
+# Stream priority of the gradient exchange (torch: lower value = higher priority; -1 is the highest HIP
+# exposes). The compute stream runs GEMMs of one 160 KiB-LDS workgroup per CU and a persistent attention
+# backward sized to every CU, so an all-reduce queued at normal priority can find no free CU until the
+# running kernel drains. At high priority the dispatcher hands the exchange's workgroups the first CUs that
+# free up: the bucket of layer l goes out between the backward kernels of layer l-1 instead of behind them.
+EXCHANGE_PRIORITY = -1
+
+
+def init_process_group(backend=None, device=None):
+    """torch.distributed.init_process_group for the training entry points (src/train.py:128-129's
+    DataParallel replaced by one process per GPU). backend defaults to VITMI_DIST_BACKEND or "nccl"
+    (= RCCL on ROCm); for RCCL its internal streams are created high-priority (EXCHANGE_PRIORITY) and the
+    communicator is bound to `device` up front."""
+    backend = backend or os.environ.get("VITMI_DIST_BACKEND", "nccl")
+    kw = {}
+    if backend == "nccl":
+        if device is not None:
+            kw["device_id"] = device
+        opts = dist.ProcessGroupNCCL.Options()
+        opts.is_high_priority_stream = True
+        kw["pg_options"] = opts
+    dist.init_process_group(backend, **kw)
+    return backend
+
+
+def exchange_stream(device):
+    """the side stream the reducers issue their exchange work on (casts, widening, gloo / RCCL calls)"""
+    return torch.cuda.Stream(device=device, priority=EXCHANGE_PRIORITY)
 
 
 class GradAllReducer:
@@ -41,7 +72,7 @@ class GradAllReducer:
         self.native_avg = average and backend == "nccl"
         self._to_scale = []
         self.cuda = engine.dev.type == "cuda"
-        self.stream = torch.cuda.Stream(device=engine.dev) if self.cuda else None
+        self.stream = exchange_stream(engine.dev) if self.cuda else None
         self.min_bucket = min_bucket_elems
         self._pending = None  # (buf, start) of a bucket being coalesced with the next one
         self._works = []
@@ -138,7 +169,7 @@ class FlatGradAllReducer:
         self.average = average
         self.native_avg = average and dist.is_initialized() and dist.get_backend(group) == "nccl"
         self.cuda = flat.device.type == "cuda"
-        self.stream = torch.cuda.Stream(device=flat.device) if self.cuda else None
+        self.stream = exchange_stream(flat.device) if self.cuda else None
         self.buckets, cur, start = [], [], 0
         self.bucket_of = [0] * flat.nseg
         for i, (p, o) in enumerate(zip(flat.params, flat.offsets)):

@@ -235,8 +235,6 @@ class _BiasReducer:
         bias gradient of the layer feeding the residual stream) queued as one reduction."""
         part = self.buf("ln", self.a.lnparts)
         D = self.D
-        if self.eng._diag_skip_lnb and rows > 4096:  # DIAGNOSTIC timing ceiling (the per-layer calls)
-            return
         ops.layernorm_bwd(dy, lddy, x, ldx, mean, rstd, gamma, dx, lddx, part, rows, D, **kw)
         self.reduce(part, ops.layernorm_bwd_blocks(rows), 3 * D, 3 * D, (dgamma_dbeta, dgamma_dbeta[D:], dx_colsum),
                     seg=D)
@@ -300,10 +298,6 @@ class ViTEngine:
         self._pruned = False
         self._side = None
         self._ev_pool, self._ev_next = [], 0
-        # DIAGNOSTIC (timing ceilings only, wrong results): VITMI_DIAG_SKIP_LN=fwd skips the per-layer
-        # LayerNorm forward launches, =bwd the per-layer LayerNorm backward launches (profiles/r03)
-        _skip = os.environ.get("VITMI_DIAG_SKIP_LN", "")
-        self._diag_skip_lnf, self._diag_skip_lnb = "fwd" in _skip, "bwd" in _skip
         self.probe = None  # list: (start, end) HIP events around every fc1 forward GEMM launch
         self.probe_wgrad = None  # list: (start, end, flop, K) around every split-K weight-gradient GEMM launch
         # dropout (nn.Dropout of PositionEmbs / EncoderBlock / MlpBlock, reference src/model.py:19-20,
@@ -452,9 +446,8 @@ class ViTEngine:
         self._pruned = self.prune_last and self._drop is None
         for i in range(L):
             ln = lambda s: self.off(self.lname(i, s))
-            if not self._diag_skip_lnf:
-                ops.layernorm_fwd(a.h[i], D, f[ln("norm1.weight"):], f[ln("norm1.bias"):], a.ln1[i], D, a.mu1[i],
-                                  a.rs1[i], T, D)
+            ops.layernorm_fwd(a.h[i], D, f[ln("norm1.weight"):], f[ln("norm1.bias"):], a.ln1[i], D, a.mu1[i],
+                              a.rs1[i], T, D)
             ops.gemm(a.ln1[i], self.wqkvt[i], a.qkv[i], T, 3 * D, D, a_layout=K_CONTIG, b_layout=K_CONTIG, lda=D,
                      ldb=D, ldc=3 * D, epilogue=EPI_BIAS_BF16, bias=self.bqkv[i])
             last = self._pruned and i == L - 1
@@ -465,9 +458,8 @@ class ViTEngine:
             ops.gemm(a.o[i], self.woutt[i], a.hm[i], T, D, D, a_layout=K_CONTIG, b_layout=K_CONTIG,
                      lda=D, ldb=D, ldc=D, epilogue=EPI_BIAS_RESID_F32, bias=f[ln("attn.out.bias"):], aux=a.h[i],
                      ldaux=D, dropout=dd(1 + 3 * i))
-            if not self._diag_skip_lnf:
-                ops.layernorm_fwd(a.hm[i], D, f[ln("norm2.weight"):], f[ln("norm2.bias"):], a.ln2[i], D, a.mu2[i],
-                                  a.rs2[i], T, D)
+            ops.layernorm_fwd(a.hm[i], D, f[ln("norm2.weight"):], f[ln("norm2.bias"):], a.ln2[i], D, a.mu2[i],
+                              a.rs2[i], T, D)
             if self.probe is not None:
                 ev0 = torch.cuda.Event(enable_timing=True)
                 ev0.record()

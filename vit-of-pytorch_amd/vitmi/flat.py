@@ -35,6 +35,9 @@ def gate(params, flag):
     if len(_GATES) > 4096:  # (gated parameters no flat optimizer collects)
         _GATES.clear()
     for p in params:
+        e = _GATES.get(id(p))
+        if e is not None and e[0]() is p:  # a forward already ran this step (gradient accumulation, a shared
+            flag = torch.logical_or(e[1], flag)  # module): the parameter took part if ANY call routed rows
         _GATES[id(p)] = (weakref.ref(p), flag)
 
 

@@ -114,6 +114,41 @@ class AdamW(torch.optim.AdamW):
             self.state[p] = {"step": self.steps[i], "exp_avg": f.view(self.exp_avg, i),
                              "exp_avg_sq": f.view(self.exp_avg_sq, i)}
 
+    def state_dict(self):
+        """torch.optim.AdamW's format: state[i] = {step, exp_avg, exp_avg_sq} per parameter (copies of the
+        flat moments), param_groups as torch's"""
+        sd = super().state_dict()
+        f = self.flat
+        st = {}
+        for k, p in enumerate(self.param_groups[0]["params"]):  # torch indexes state by group position
+            i = f._index[id(p)]
+            st[k] = {"step": self.steps[i].detach().clone(), "exp_avg": f.view(self.exp_avg, i).clone(),
+                     "exp_avg_sq": f.view(self.exp_avg_sq, i).clone()}
+        sd["state"] = st
+        return sd
+
+    def load_state_dict(self, state_dict):
+        """copy a torch.optim.AdamW-format state into the flat moment / step buffers (the per-parameter
+        state entries stay views of them, so step() keeps using what was loaded)"""
+        f = self.flat
+        groups = state_dict["param_groups"]
+        if len(groups) != 1 or len(groups[0]["params"]) != len(f.params):
+            raise ValueError("vitmi.optim.AdamW.load_state_dict: one group of %d parameters expected" % len(f.params))
+        for k, v in groups[0].items():
+            if k != "params":
+                self.param_groups[0][k] = v
+        for k, p in enumerate(self.param_groups[0]["params"]):
+            i = f._index[id(p)]
+            st = state_dict["state"].get(k, state_dict["state"].get(str(k)))
+            if st is None:  # never stepped: zero moments
+                f.view(self.exp_avg, i).zero_()
+                f.view(self.exp_avg_sq, i).zero_()
+                self.steps[i] = 0.0
+                continue
+            f.view(self.exp_avg, i).copy_(st["exp_avg"].reshape(f.params[i].shape))
+            f.view(self.exp_avg_sq, i).copy_(st["exp_avg_sq"].reshape(f.params[i].shape))
+            self.steps[i] = float(st["step"])
+
     def zero_grad(self, set_to_none: bool = True):
         """zero the flat gradient buffer (the .grad views stay in place; `set_to_none` semantics — a
         parameter without a gradient is skipped by step() — are kept by the used flags)"""

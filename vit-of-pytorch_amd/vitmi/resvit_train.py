@@ -26,6 +26,7 @@ import torch.distributed as dist
 
 from . import resvit
 from .optim import AdamW, clip_grad_norm_, get_cosine_schedule_with_warmup
+from .config import process_config
 from .train import MetricTracker, StepWriter, SyntheticDataLoader, _rank_mean, rank_batch, set_seed
 
 METRICS = ["loss", "c_loss", "a_loss", "d_loss", "router_entropy", "acc1", "acc5", "active_ratio", "lr",
@@ -218,13 +219,24 @@ def get_train_config(argv=None):
     return config
 
 
+def save_model(save_dir, model, best=False):
+    """res-vit/utils.py:149-155: current_model.pth every epoch, best_model.pth on a new best. The reference
+    pickles the whole module (torch.save(model)); here the state_dict is saved, so the file loads with
+    torch.load(weights_only=True) into resvit.Transformer(args).load_state_dict."""
+    torch.save(model.state_dict(), str(save_dir + "current_model.pth"))
+    if best:
+        torch.save(model.state_dict(), str(save_dir + "best_model.pth"))
+
+
 def build_model(config, device):
     args = set_model_architecture(config_to_model_args(config), config.model_arch)
     return resvit.Transformer(args).to(device)
 
 
 def main(argv=None):
-    config = get_train_config(argv)
+    # experiment dirs as res-vit/config.py:183 (process_config); ranks started below share the stamp
+    config = process_config(get_train_config(argv))
+    os.environ.setdefault("VITMI_EXP_STAMP", config.exp_stamp)
     if "WORLD_SIZE" not in os.environ and config.n_gpu > 1:
         rank_batch(config.batch_size, config.n_gpu)
         sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
@@ -242,8 +254,8 @@ def main(argv=None):
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
     if world > 1:
-        backend = os.environ.get("VITMI_DIST_BACKEND", "nccl")
-        dist.init_process_group(backend, **({"device_id": device} if backend == "nccl" else {}))
+        from .dist import init_process_group
+        init_process_group(device=device)
     batch = rank_batch(config.batch_size, world)
     set_seed(config.seed)
     model = build_model(config, device)
@@ -290,7 +302,11 @@ def main(argv=None):
         model.eval()
         res, _, _ = valid_epoch(epoch, model, valid_loader, optimizer, valid_metrics, la, ld, lc, device)
         log.update({"val_" + k: v for k, v in res.items()})
-        best_acc = max(best_acc, log["val_acc1"])
+        best = log["val_acc1"] > best_acc
+        if best:
+            best_acc = log["val_acc1"]
+        if rank == 0 and not config.no_save:
+            save_model(config.checkpoint_dir, model, best)  # res-vit/train.py:335-341
         if rank == 0:
             for key, value in log.items():
                 print("    {:15s}: {}".format(str(key), value), flush=True)

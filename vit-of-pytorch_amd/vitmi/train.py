@@ -342,8 +342,8 @@ def main(argv=None):
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
     if world > 1:
-        backend = os.environ.get("VITMI_DIST_BACKEND", "nccl")
-        dist.init_process_group(backend, **({"device_id": device} if backend == "nccl" else {}))
+        from .dist import init_process_group
+        init_process_group(device=device)
     batch = rank_batch(config.batch_size, world)
 
     model = build_model(config, device)
