@@ -121,19 +121,11 @@ typedef struct vit_gemm_args {
                                  PATCH: C = drop(embedding + pos);  BIAS_RESID_F32: C = drop(acc + bias) + aux;
                                  BIAS_GELU_DGELU: C2 = drop(gelu(u)), C = gelu'(u) * mult (the dropout
                                  backward folded into the saved derivative) */
-  void* workspace;          /* optional (ABI 9): >= vit_gemm_workspace_bytes(), zero-filled once when allocated
-                               and left as the library leaves it (its counters return to zero after each call);
-                               one workspace per stream. The persistent kernel splits the K range of its last
-                               round of tiles over otherwise idle workgroups with it; NULL runs that round
-                               unsplit. */
-  int64_t workspace_bytes;
 } vit_gemm_args;
 
 int vit_gemm_bf16(const vit_gemm_args* args, vit_stream_t stream);
 /* rows of C covered by one workgroup tile for these arguments (sizing of col_partial) */
 int64_t vit_gemm_tile_rows(const vit_gemm_args* args);
-/* bytes of vit_gemm_args.workspace that let any call split its persistent tail (a constant, 64 MiB + 4 KiB) */
-int64_t vit_gemm_workspace_bytes(void);
 
 /* out[z*out_batch_stride + m*ldo + n] (+)= sum_s ws[((z*split + s)*M + m)*N + n]  (f32) */
 int vit_splitk_reduce(const float* ws, int64_t batch, int64_t split, int64_t M, int64_t N,

@@ -19,39 +19,10 @@
 
 namespace {
 using vitg::GemmDev;
-
-int num_cus() {
-  static const int n = [] {
-    int dev = 0, c = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) !=
-                                               hipSuccess)
-      return 256;
-    return c > 0 ? c : 256;
-  }();
-  return n;
-}
 using vitg::EPI_DROP;
 
-// the persistent ping-pong kernel (config 10, gemm_ps.inc): both operands K-contiguous, one batch, no
-// split-K, N a multiple of 256, the register epilogues without dropout, outputs addressable by 32-bit
-// buffer offsets
-constexpr int64_t kPsCounters = 4096;
-constexpr int64_t kPsWsBytes = kPsCounters + (64L << 20);
-bool ps_epilogue(int e) {
-  return e == VIT_EPI_F32 || e == VIT_EPI_BF16 || e == VIT_EPI_BIAS_BF16 || e == VIT_EPI_BIAS_GELU ||
-         e == VIT_EPI_BIAS_GELU_DGELU || e == VIT_EPI_MUL_BF16;
-}
-bool ps_eligible(const vit_gemm_args* a) {
-  if (!(a->a_layout == VIT_K_CONTIG && a->b_layout == VIT_K_CONTIG && a->batch == 1 && a->split_k == 1)) return false;
-  if (!ps_epilogue(a->epilogue) || (a->dropout && a->dropout->p > 0.0f) || a->col_partial) return false;
-  if (a->N % 256 != 0 || a->M < 1024) return false;
-  const int64_t esz = a->epilogue == VIT_EPI_F32 ? 4 : 2;
-  if (a->M * a->ldc * esz >= (1LL << 32) || (a->C2 && a->M * a->ldc2 * 2 >= (1LL << 32))) return false;
-  return true;
-}
-
 int pick_tile(const vit_gemm_args* a) {
-  if (a->tile > 0) return (int)a->tile == 10 && !ps_eligible(a) ? 9 : (int)a->tile;
+  if (a->tile > 0) return (int)a->tile;
   // measured on MI355X (tools/gemm_bench.py, ViT-B/16 bs256 shapes, profiles/r01/gemm_*):
   //  * split-K weight gradients: the 256x256 ping-pong kernel with the split sized to one wave
   //    (fc1/fc2 wgrad 244 us vs 340 us for 256x128 at split 16);
@@ -68,7 +39,6 @@ int pick_tile(const vit_gemm_args* a) {
     static const int env_sk = vit::knob("VIT_GEMM_SPLITK_CFG", 5);
     return env_sk == 6 || env_sk == 7 || env_sk == 8 || env_sk == 9 ? env_sk : 5;
   }
-  if (ps_eligible(a)) return 10;
   if (a->M >= 1024 && a->N >= 256) {
     // (short-K f32 residual outputs keep 2 workgroups per CU; the aux-reading epilogues run on the
     // half-tile kernel since their operand is prefetched a staging pass ahead: fc2 dgrad x GELU'
@@ -86,8 +56,6 @@ int pick_tile(const vit_gemm_args* a) {
 }
 
 }  // namespace
-
-extern "C" int64_t vit_gemm_workspace_bytes(void) { return kPsWsBytes; }
 
 extern "C" int64_t vit_gemm_tile_rows(const vit_gemm_args* a) {
   if (!a) return 0;
@@ -133,10 +101,6 @@ extern "C" int vit_gemm_bf16(const vit_gemm_args* a, vit_stream_t stream) {
     default: break;
   }
   GemmDev d;
-  d.ps_grid = 0;
-  d.ps_split = 1;
-  d.ws = nullptr;
-  d.ps_cnt = nullptr;
   d.M = (int)a->M; d.N = (int)a->N; d.K = (int)a->K;
   d.A = (const char*)a->A; d.lda = a->lda; d.a_bs = a->a_batch_stride; d.a_bytes = (uint32_t)a_bytes;
   d.B = (const char*)a->B; d.ldb = a->ldb; d.b_bs = a->b_batch_stride; d.b_bytes = (uint32_t)b_bytes;
@@ -188,28 +152,7 @@ extern "C" int vit_gemm_bf16(const vit_gemm_args* a, vit_stream_t stream) {
   hipStream_t s = (hipStream_t)stream;
   const int batch = (int)a->batch, split = (int)a->split_k;
   const int cfg = pick_tile(a);
-  if (cfg == 10) {
-    // one workgroup per CU over rounds of whole tiles; the R tiles of the last round split along K into S
-    // parts over the idle workgroups when the workspace allows (S * R <= CUs, >= 2 k-tiles per part)
-    const int ncu = num_cus();
-    const long tiles = ((a->M + 255) / 256) * (a->N / 256);
-    const int G = (int)(tiles < ncu ? tiles : ncu);
-    const long R = tiles % G;
-    int S = 1;
-    // (a part stores and the last part re-reads 256 KiB f32 partial tiles: only worth it for long K, where a
-    // third of a tile's k-loop outweighs that traffic; measured, profiles/r04/gemm_ps_v1.txt)
-    if (R > 0 && a->K >= 2048 && a->workspace && a->workspace_bytes >= kPsWsBytes) {
-      S = (int)(G / R);
-      if (S > 4) S = 4;
-      if (S > a->K / 128) S = (int)(a->K / 128);
-      if (S < 1) S = 1;
-    }
-    d.ps_grid = G;
-    d.ps_split = S;
-    d.ps_cnt = (unsigned*)a->workspace;
-    d.ws = a->workspace ? (float*)((char*)a->workspace + kPsCounters) : nullptr;
-  }
-  VIT_CHECK_ARG(cfg >= 0 && cfg <= 10, "vit_gemm_bf16: bad tile config %d", cfg);
+  VIT_CHECK_ARG(cfg >= 0 && cfg <= 9, "vit_gemm_bf16: bad tile config %d", cfg);
   VIT_CHECK_ARG(cfg != 1 || a->K % 32 == 0, "vit_gemm_bf16: K");
   auto run = [&](int c, const GemmDev& g) -> hipError_t {
     switch (a->epilogue) {

@@ -51,12 +51,6 @@ struct GemmDev {
   int diag;            // diagnostics (VIT_GEMM_DIAG): 1 = skip the half-tile kernel's global stores, 2 = its epilogue
   int split_xcd;       // split-K grids: place each XCD's workgroups on one or two K-chunks (VIT_GEMM_SPLIT_XCD)
   int prio;            // s_setprio(1) around the ping-pong kernels' MFMA clusters (VIT_GEMM_PRIO)
-  // persistent kernel (config 10): workgroups, K-split of the last round's tiles, its f32 partial tiles and
-  // per-tile arrival counters (zero between launches)
-  int ps_grid;
-  int ps_split;
-  float* ws;
-  unsigned* ps_cnt;
 };
 
 // Internal epilogue flag: the dropout variant of PATCH / BIAS_RESID_F32 / BIAS_GELU_DGELU (its own

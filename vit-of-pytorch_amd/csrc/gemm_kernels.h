@@ -1116,7 +1116,6 @@ __global__ void __launch_bounds__(512) gemm_pp_kernel(const GemmDev p) {
 }
 
 #include "gemm_pp2.inc"
-#include "gemm_ps.inc"
 
 template <int BN, int BK, int NBUF, bool AK, bool BKC, int EPI>
 hipError_t launch_pp(const GemmDev& d, int batch, int split, hipStream_t s) {
@@ -1152,9 +1151,6 @@ hipError_t launch_cfg(int cfg, const GemmDev& d, int batch, int split, hipStream
     case 7: return launch_pp<256, 32, 4, AK, BKC, EPI>(d, batch, split, s);
     case 8: return launch_pp<256, 32, 5, AK, BKC, EPI>(d, batch, split, s);
     case 9: return launch_pp2<AK, BKC, EPI>(d, batch, split, s);
-    case 10:  // persistent ping-pong (gemm_ps.inc): both operands K-contiguous
-      if constexpr (AK && BKC) return launch_ps<EPI>(d, s);
-      return hipErrorInvalidValue;
     default: return launch_t<128, 128, 64, 2, 2, 2, AK, BKC, EPI>(d, batch, split, s);
   }
 }

@@ -17,7 +17,7 @@ c_i32 = ctypes.c_int32
 c_f32 = ctypes.c_float
 c_vp = ctypes.c_void_p
 
-ABI_VERSION = 9  # vit_abi_version() of the library these prototypes describe
+ABI_VERSION = 8  # vit_abi_version() of the library these prototypes describe
 
 # enum vit_layout / vit_epilogue (include/vit_hip.h)
 K_CONTIG, MN_CONTIG = 0, 1
@@ -43,7 +43,6 @@ class GemmArgs(ctypes.Structure):
         ("aux", c_vp), ("ldaux", c_i64), ("aux2", c_vp),
         ("batch", c_i64), ("split_k", c_i64), ("tokens", c_i64), ("col_partial", c_vp),
         ("epilogue", c_i32), ("tile", c_i32), ("dropout", ctypes.POINTER(Dropout)),
-        ("workspace", c_vp), ("workspace_bytes", c_i64),
     ]
 
 
@@ -61,7 +60,6 @@ _SIGS = {
     "vit_abi_version": (c_i32, []),
     "vit_gemm_bf16": (c_i32, [ctypes.POINTER(GemmArgs), c_vp]),
     "vit_gemm_tile_rows": (c_i64, [ctypes.POINTER(GemmArgs)]),
-    "vit_gemm_workspace_bytes": (c_i64, []),
     "vit_splitk_reduce": (c_i32, [c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_i64, c_i64, c_i32, c_vp]),
     "vit_layernorm_fwd": (c_i32, [c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_i32, c_vp, c_vp, c_i64, c_i64, c_f32, c_vp]),
     "vit_layernorm_bwd_partial_rows": (c_i64, [c_i64]),

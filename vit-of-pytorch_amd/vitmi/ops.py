@@ -41,7 +41,7 @@ def _chk(t, dtype, name):
 # ---------------------------------------------------------------------------------------------
 def _gemm_args(A, B, C, M, N, K, *, a_layout, b_layout, lda, ldb, ldc, epilogue, bias=None, aux=None, ldaux=0,
                C2=None, ldc2=0, aux2=None, batch=1, a_bs=0, b_bs=0, c_bs=0, bias_bs=0, split_k=1, tokens=0, tile=0,
-               col_partial=None, dropout=None, workspace=True):
+               col_partial=None, dropout=None):
     a = GemmArgs()
     a.M, a.N, a.K = M, N, K
     a.A, a.lda, a.a_batch_stride, a.a_layout = A.data_ptr(), lda, a_bs, a_layout
@@ -55,24 +55,7 @@ def _gemm_args(A, B, C, M, N, K, *, a_layout, b_layout, lda, ldb, ldc, epilogue,
     a.col_partial = col_partial.data_ptr() if col_partial is not None else None
     a.epilogue, a.tile = epilogue, tile
     a.dropout = ctypes.pointer(dropout) if dropout is not None else None
-    ws = gemm_workspace() if workspace is True else workspace
-    a.workspace, a.workspace_bytes = (ws.data_ptr(), ws.numel()) if ws is not None else (None, 0)
     return a
-
-
-_GEMM_WS = {}
-
-
-def gemm_workspace(stream=None):
-    """the zero-initialised GEMM workspace of a stream (vit_gemm_args.workspace: the persistent kernel's
-    split tail; its counters return to zero after every call, so one buffer serves every call on the stream)"""
-    st = stream if stream is not None else torch.cuda.current_stream()
-    key = (st.device, st.cuda_stream)
-    ws = _GEMM_WS.get(key)
-    if ws is None:
-        ws = torch.zeros(int(lib().vit_gemm_workspace_bytes()), dtype=torch.uint8, device=st.device)
-        _GEMM_WS[key] = ws
-    return ws
 
 
 def dropout_desc(p, site, seed, offset, row_stride=1):
