@@ -417,7 +417,7 @@ def bench_resvit(args, world, rank, dev, backend, comm):
     N > 1: one rank per GPU, flat gradient buckets all-reduced during the backward."""
     from vitmi import resvit
     from vitmi.optim import AdamW, get_cosine_schedule_with_warmup
-    from vitmi.resvit_train import train_step
+    from vitmi.resvit_train import GraphedTrainStep, train_step
     b = args.batch or 128
     a = dict(dim=768, mlp_dim=3072, n_layers=12, n_heads=12, n_kv_heads=12, norm_eps=1e-5, lora_rank=8,
              dynamic_active_target=0.6, dynamic_start_layer=2, dynamic_router_hdim=512, dynamic_reserve_initials=1,
@@ -435,10 +435,14 @@ def bench_resvit(args, world, rank, dev, backend, comm):
     x = torch.randn(b, 3, args.image_size, args.image_size, device=dev, generator=g)
     y = torch.randint(0, 100, (b,), device=dev, generator=g)
     ratios = []
+    # one process: forward + backward replayed from a HIP graph (GraphedTrainStep), the optimizer eager;
+    # data parallel: op by op (the gradient all-reduce hooks run during the backward)
+    graphed = GraphedTrainStep(model, x, y, opt, sched, 1e-4, 1e-2, 1.0, True) if reducer is None else None
 
     def step():
-        out = train_step(model, x, y, opt, sched, 1e-4, 1e-2, 1.0, True, reducer)
-        ratios.append(out[5]["non_low_rank_ratio"])
+        out = graphed.step() if graphed is not None else train_step(model, x, y, opt, sched, 1e-4, 1e-2, 1.0, True,
+                                                                    reducer)
+        ratios.append(out[5]["non_low_rank_ratio"].clone())
 
     def barrier():
         if world > 1:
@@ -472,7 +476,7 @@ def bench_resvit(args, world, rank, dev, backend, comm):
         "data": "synthetic (N(0,1) images, uniform labels, seed-42 reference-order random init, Gumbel routing)",
         "config": {"workload": f"Res-ViT-B/16 @{args.image_size} train step (teacher+routed student fwd, 1c+1e-4a+"
                                f"1e-2d loss, bwd, {comm + ' all-reduce, ' if world > 1 else ''}clip 1.0 + AdamW, "
-                               "cosine warm-up)",
+                               "cosine warm-up)" + (", fwd+bwd as one HIP graph" if graphed is not None else ""),
                    "model": "Res-ViT-B/16 (LoRA r8, reslr, block 1, 100 classes)", "image_size": args.image_size,
                    "per_gpu_batch": b, "global_batch": b * world, "seq_len": (args.image_size // 16) ** 2 + 1,
                    "parallelism": f"dp{world}", "dist_backend": backend},

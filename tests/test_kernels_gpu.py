@@ -220,7 +220,10 @@ ATTN_CASES = [(2, 2, 2, 64, 0),  # (config C1: 2 tokens)
               (24, 197, 12, 64, 0), (23, 50, 12, 64, 0), (32, 2, 12, 64, 0), (30, 17, 12, 32, 0),
               # hd <= 32 past 256 tokens: more key pairs than the persistent backward's 8 waves (two-stage
               # kernel), and exactly 8 pairs (the persistent kernel with no idle wave)
-              (1, 300, 2, 32, 0), (2, 256, 2, 32, 0)]
+              (1, 300, 2, 32, 0), (2, 256, 2, 32, 0),
+              # 80-wide images (hd 80, ViT-H/14): odd tile counts (the 16-k P V / dQ / dK-dV steps), a single
+              # tile, 10 key pairs on 8 waves (the second pair's K / V loaded in stage 2), many items
+              (2, 5, 2, 80, 0), (3, 17, 2, 80, 0), (1, 241, 2, 80, 0), (1, 320, 2, 80, 0), (20, 50, 4, 80, 0)]
 
 
 @pytest.mark.parametrize("B,N,H,hd,path", ATTN_CASES)
@@ -254,12 +257,12 @@ def test_attention(B, N, H, hd, path):
     assert rel(mv, gv) < 2e-2
 
 
-@pytest.mark.parametrize("N,B", [(2, 2), (17, 2), (197, 2), (2, 32)])
-def test_attention_backward_saturated_scores_finite(N, B):
+@pytest.mark.parametrize("N,B,hd", [(2, 2, 64), (17, 2, 64), (197, 2, 64), (2, 32, 64), (257, 2, 80), (5, 2, 80)])
+def test_attention_backward_saturated_scores_finite(N, B, hd):
     """scores of |s| ~ 1e3 (the reference's std-1 init, config C1's 2 tokens): the LSE of a query can be far
     below 0, and the zero-padded keys of its last computed key tile must still get P = 0, not 2^-LSE = inf
     (inf * dP 0 = NaN); B = 32 x H = 12 puts several items on each workgroup of the persistent backward"""
-    H, hd = (2, 64) if B == 2 else (12, 64)
+    H = 2 if B == 2 else 12
     D = H * hd
     g = torch.Generator(device=DEV).manual_seed(1)
     qkv = (torch.randn(B * N, 3 * D, device=DEV, generator=g) * 8.0).bfloat16()
@@ -276,11 +279,12 @@ def test_attention_backward_saturated_scores_finite(N, B):
     assert torch.isfinite(o.float()).all() and torch.isfinite(dqkv.float()).all() and torch.isfinite(bp).all()
 
 
-@pytest.mark.parametrize("N,path", [(197, 0), (197, 2), (257, 0), (2, 0), (17, 0)])
-def test_attention_backward_keeps_nan(N, path):
+@pytest.mark.parametrize("N,path,hd", [(197, 0, 64), (197, 2, 64), (257, 0, 64), (2, 0, 64), (17, 0, 64),
+                                       (257, 0, 80), (17, 0, 80)])
+def test_attention_backward_keeps_nan(N, path, hd):
     """a NaN in one query row (a diverging run) must surface as NaN in that row's dQ, not be clamped into a
     finite gradient by the padded-key exponent clamp"""
-    B, H, hd = 2, 2, 64
+    B, H = 2, 2
     D = H * hd
     qkv = torch.randn(B * N, 3 * D, device=DEV).bfloat16()
     qkv[min(5, N - 1), 3] = float("nan")  # image 0, token 5 (or the last), head 0: q

@@ -149,6 +149,57 @@ def test_three_training_steps_match_reference(gold, fused):
     assert not bad, bad
 
 
+@pytest.mark.parametrize("fused,warmup", [(False, 0), (True, 0), (True, 1)])
+def test_graphed_step_matches_eager_and_reference(gold, fused, warmup):
+    """GraphedTrainStep (forward + backward replayed from one HIP graph, optimizer eager) computes what
+    train_step computes: the reference's three recorded steps (Gumbel draws / routing replayed through
+    static buffers the graph reads) give bit-identical losses and parameters to the eager steps, and the
+    eager steps are pinned to the reference by test_three_training_steps_match_reference."""
+    from vitmi.optim import AdamW, get_cosine_schedule_with_warmup
+    from vitmi.resvit_train import GraphedTrainStep, train_step
+    h = hp(gold)
+    runs = []
+    for graphed in (False, True):
+        m = build(gold).train()
+        opt = AdamW(m.parameters(), lr=h["lr"], weight_decay=h["wd"], betas=h["betas"], eps=h["eps"],
+                    max_grad_norm=1.0 if fused else None)
+        sched = get_cosine_schedule_with_warmup(opt, h["warmup"], h["total"])
+        routers = [l.router for l in m.layers if hasattr(l, "router")]
+        hard = [torch.from_numpy(gold[f"s0/router{j}_hard"]).cuda() for j in range(len(routers))]
+        gum = [torch.from_numpy(gold[f"s0/gumbel{j}"]).cuda() for j in range(len(routers))]
+        for r, hh, gg in zip(routers, hard, gum):  # the graph reads these buffers: refilled every step
+            r.hard_override = lambda logits, hh=hh: hh
+            r.gumbel_noise = lambda logits, gg=gg: gg
+        x = torch.from_numpy(gold["s0/x"]).cuda()
+        y = torch.from_numpy(gold["s0/y"]).cuda()
+        # warmup=0: the eager run before it created the device constants (no pageable copy under capture);
+        # warmup=1: one eager step on batch 0 inside the constructor (the eager run takes the same step first)
+        if graphed:
+            g = GraphedTrainStep(m, x, y, opt, sched, h["la"], h["ld"], h["lc"], True, warmup=warmup)
+        else:
+            g = None
+            for _ in range(warmup):
+                train_step(m, x, y, opt, sched, h["la"], h["ld"], h["lc"], clip_grad_norm=True)
+        losses = []
+        for s in range(3):
+            for j in range(len(routers)):
+                hard[j].copy_(torch.from_numpy(gold[f"s{s}/router{j}_hard"]))
+                gum[j].copy_(torch.from_numpy(gold[f"s{s}/gumbel{j}"]))
+            x = torch.from_numpy(gold[f"s{s}/x"]).cuda()
+            y = torch.from_numpy(gold[f"s{s}/y"]).cuda()
+            out = (g.step(x, y) if graphed else
+                   train_step(m, x, y, opt, sched, h["la"], h["ld"], h["lc"], clip_grad_norm=True))
+            losses.append(torch.stack([out[0], out[1], out[3]]).detach().clone())
+            if warmup == 0:
+                assert abs(float(out[1]) - float(gold[f"s{s}/c_loss"])) <= 1e-3 * float(gold[f"s{s}/c_loss"]), s
+        runs.append((torch.stack(losses), [p.detach().clone() for p in opt.flat.params], opt.flat.used.clone()))
+    (le, pe, ue), (lg, pg, ug) = runs
+    assert torch.isfinite(le).all() and le[0, 0] != le[2, 0]  # the graph's gradients reach the parameters
+    assert torch.equal(le, lg)
+    assert torch.equal(ue, ug)
+    assert all(torch.equal(a, b) for a, b in zip(pe, pg))
+
+
 def test_flat_params_keep_grad_views_and_skip_unused():
     """FlatParams: parameters become views of one buffer, autograd accumulates into the preset .grad
     views in place, a parameter outside the graph is marked unused, module.zero_grad() (set_to_none)

@@ -18,6 +18,32 @@
 #include "attn_common.h"
 #include <stdlib.h>
 
+#ifdef VIT_ATTN_STAMPS
+// DIAGNOSTIC build only: s_memtime stamps of the two-stage backward, workgroups 0 and gridDim - 1, their first
+// and last waves, 6 points (start, K / V images in, stage 1 done, Q / dO images in, stage 2 done, end);
+// read back with vit_attn2_stamps()
+__device__ unsigned long long g_attn2_stamps[2][2][8];
+#define A2STAMP(k)                                                                                          \
+  do {                                                                                                      \
+    const int w_ = threadIdx.x >> 6, lw_ = blockDim.x / 64 - 1;                                             \
+    const bool blk_ = blockIdx.x == 0 || blockIdx.x == gridDim.x - 1;                                        \
+    if (blk_ && (w_ == 0 || w_ == lw_)) {                                                                   \
+      unsigned long long t_;                                                                                \
+      __builtin_amdgcn_sched_barrier(0);                                                                    \
+      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");                          \
+      __builtin_amdgcn_sched_barrier(0);                                                                    \
+      if ((threadIdx.x & 63) == 0) g_attn2_stamps[blockIdx.x != 0][w_ != 0][k] = t_;                         \
+    }                                                                                                       \
+  } while (0)
+extern "C" int vit_attn2_stamps(unsigned long long* out) {  // 32 values: [block first/last][wave first/last][point]
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_attn2_stamps), sizeof(g_attn2_stamps));
+}
+#else
+#define A2STAMP(k) \
+  do {             \
+  } while (0)
+#endif
+
 namespace {
 using namespace vit_attn;
 
@@ -139,7 +165,7 @@ __device__ __forceinline__ void load_images_lds(lds_t* imgA, const bf16_t* srcA,
 }
 
 template <int HD, int NKT, int NW>
-__global__ void __launch_bounds__(NW * 64, NW == 8 ? 2 : 3) attn_fwd2_kernel(const bf16_t* __restrict__ qkv,
+__global__ void __launch_bounds__(NW * 64, NW == 8 ? (k_tail<HD> ? 1 : 2) : 3) attn_fwd2_kernel(const bf16_t* __restrict__ qkv,
                                                                bf16_t* __restrict__ o, float* __restrict__ lse,
                                                                int N, int H, int hd, float scale, int nq) {
   constexpr int NP = NKT * 16;
@@ -163,10 +189,13 @@ __global__ void __launch_bounds__(NW * 64, NW == 8 ? 2 : 3) attn_fwd2_kernel(con
   // latency per workgroup instead of one per strip
   constexpr int MAXS = (NKT + NW - 1) / NW;
   v8bf qa[MAXS][HD / 32];
+  v4s qa16[MAXS];  // hd 80: the 16-k tail
 #pragma unroll
-  for (int u = 0; u < MAXS; ++u)
+  for (int u = 0; u < MAXS; ++u) {
 #pragma unroll
     for (int kk = 0; kk < HD / 32; ++kk) qa[u][kk] = gl_row<HD>(base, rs, (wave + u * NW) * 16, kk, N, hd, lane);
+    if constexpr (k_tail<HD>) qa16[u] = gl_row16<HD>(base, rs, (wave + u * NW) * 16, N, hd, lane);
+  }
   __syncthreads();
 #pragma unroll
   for (int u = 0; u < MAXS; ++u) {
@@ -180,6 +209,7 @@ __global__ void __launch_bounds__(NW * 64, NW == 8 ? 2 : 3) attn_fwd2_kernel(con
 #pragma unroll
       for (int kk = 0; kk < HD / 32; ++kk)
         s[kt] = mfma(__builtin_bit_cast(v8bf, lds_ld<v8s>(Ki + kt * T + L.row[kk])), qf[kk], s[kt]);
+      if constexpr (k_tail<HD>) s[kt] = mfma16_add(lds_ld<v4s>(Ki + kt * T + L.row16), qa16[u], s[kt]);
     }
     if (N < NP) {  // only the last tile holds padded keys
 #pragma unroll
@@ -224,7 +254,7 @@ __global__ void __launch_bounds__(NW * 64, NW == 8 ? 2 : 3) attn_fwd2_kernel(con
     if constexpr (NKT % 2 == 1) {
       const v4s pp = pack4(s[NKT - 1]);
 #pragma unroll
-      for (int dt = 0; dt < HD / 16; ++dt) acc[dt] = mfma16(lds_tr(Vi + (NKT - 1) * T + L.tr[dt]), pp, acc[dt]);
+      for (int dt = 0; dt < HD / 16; ++dt) acc[dt] = mfma16_add(lds_tr(Vi + (NKT - 1) * T + L.tr[dt]), pp, acc[dt]);
     }
     const int q = qt * 16 + i;
     if (g == 0 && q < N) lse[(long)bh * N + q] = mx * scale + logf(l);
@@ -241,7 +271,7 @@ __global__ void __launch_bounds__(NW * 64, NW == 8 ? 2 : 3) attn_fwd2_kernel(con
 // Backward, two LDS images at a time (56 KB at N = 197, hd = 64: two workgroups per CU, so one
 // workgroup's image loads overlap the other's MFMA work).
 //   stage 1 (K, V images): each wave owns 16-query strips, Q / dO rows in registers (the next
-//     strip's requested one strip ahead). HD <= 64: P and dP of the strip for all keys are kept in
+//     strip's requested one strip ahead). HD <= 80: P and dP of the strip for all keys are kept in
 //     registers, so delta_q = sum_j P_qj dP_qj (from the recomputed P and dP themselves:
 //     FlashAttention-2's rowsum(dO * O) differs from it by bf16 O's rounding, and dS = P (dP - delta)
 //     is a small difference: that turned into 10-25% errors on the q/k weight gradients under
@@ -252,7 +282,7 @@ __global__ void __launch_bounds__(NW * 64, NW == 8 ? 2 : 3) attn_fwd2_kernel(con
 // Deterministic (no atomics). Optionally writes per-image column sums of dQ | dK | dV (q/k/v bias
 // gradient partials) to bias_partial[b][3*D].
 template <int HD, int NKT, int NW>
-__global__ void __launch_bounds__(NW * 64, 2) attn_bwd_kernel(const bf16_t* __restrict__ qkv,
+__global__ void __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) attn_bwd_kernel(const bf16_t* __restrict__ qkv,
                                                               const bf16_t* __restrict__ dout,
                                                               const float* __restrict__ lse, bf16_t* __restrict__ dqkv,
                                                               float* __restrict__ bias_partial, int N, int H, int hd,
@@ -273,6 +303,7 @@ __global__ void __launch_bounds__(NW * 64, 2) attn_bwd_kernel(const bf16_t* __re
   const bf16_t* dob = dout + (long)b * N * D + (long)h * hd;
   bf16_t* dq_base = dqkv + (long)b * N * rs + (long)h * hd;
 
+  A2STAMP(0);
   load_images<HD, NP, NW * 64>(ImA, base + D, rs, ImB, base + 2 * D, rs, N, hd);
   for (int r = threadIdx.x; r < NP; r += blockDim.x) {
     // padded queries: P = 2^-1e30 = 0 (finite, so that nan_of() of their exponent stays 0)
@@ -280,6 +311,7 @@ __global__ void __launch_bounds__(NW * 64, 2) attn_bwd_kernel(const bf16_t* __re
     dlt_s[r] = 0.f;
   }
   __syncthreads();
+  A2STAMP(1);
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int g = lane >> 4, i = lane & 15;
@@ -289,22 +321,27 @@ __global__ void __launch_bounds__(NW * 64, 2) attn_bwd_kernel(const bf16_t* __re
   // holding them are processed, the other rows get dQ = 0 and contribute nothing to dK / dV
   const int nqa = min(N, (nq + 31) / 32 * 32);
   const int npair_q = (nqa + 31) / 32;
-  float bq[HD / 16][4], bk[HD / 16][4], bv[HD / 16][4];
-#pragma unroll
-  for (int dt = 0; dt < HD / 16; ++dt)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) bq[dt][r] = bk[dt][r] = bv[dt][r] = 0.f;
+  // bias partials: each wave adds the column sums of every dQ strip / dK, dV tile it finishes to its own
+  // LDS rows bsum[wave][3][HD] (nothing long-lived in registers); summed over waves at the end
+  float* bs_w = bsum + wave * 3 * HD;
+  if (bias_partial)
+    for (int e = lane; e < 3 * HD; e += 64) bs_w[e] = 0.f;
 
   // ---- stage 1: delta and dQ ----
-  if constexpr (HD <= 64) {
+  if constexpr (HD != 96) {
     // one 16-query strip at a time with P and dP of ALL keys kept in registers (2 x NKT x 4 f32):
     // delta = sum_j P dP comes out of the same pass, so dS and dQ need no recompute of S / dP
     const int nqt = (N + 15) / 16;
     v8bf qn[HD / 32], dn[HD / 32];  // next strip's Q / dO rows, requested one strip ahead
+    v4s qn16 = {0, 0, 0, 0}, dn16 = {0, 0, 0, 0};  // hd 80: their 16-k tails
 #pragma unroll
     for (int kk = 0; kk < HD / 32; ++kk) {
       qn[kk] = gl_row<HD>(base, rs, wave * 16, kk, N, hd, lane);
       dn[kk] = gl_row<HD>(dob, D, wave * 16, kk, N, hd, lane);
+    }
+    if constexpr (k_tail<HD>) {
+      qn16 = gl_row16<HD>(base, rs, wave * 16, N, hd, lane);
+      dn16 = gl_row16<HD>(dob, D, wave * 16, N, hd, lane);
     }
     for (int qt = wave; qt < nqt; qt += NW) {
       if (qt * 16 >= nqa) {  // no gradient reaches these queries: dQ = 0, delta = 0
@@ -327,6 +364,11 @@ __global__ void __launch_bounds__(NW * 64, 2) attn_bwd_kernel(const bf16_t* __re
         qn[kk] = gl_row<HD>(base, rs, (qt + NW) * 16, kk, N, hd, lane);
         dn[kk] = gl_row<HD>(dob, D, (qt + NW) * 16, kk, N, hd, lane);
       }
+      const v4s qf16 = qn16, df16 = dn16;
+      if constexpr (k_tail<HD>) {
+        qn16 = gl_row16<HD>(base, rs, (qt + NW) * 16, N, hd, lane);
+        dn16 = gl_row16<HD>(dob, D, (qt + NW) * 16, N, hd, lane);
+      }
       const float ls = lse_s[qt * 16 + i];
       v4f P[NKT], DP[NKT];
       float dlr[4] = {0.f, 0.f, 0.f, 0.f};  // four independent chains (one fma chain per row r)
@@ -342,6 +384,10 @@ __global__ void __launch_bounds__(NW * 64, 2) attn_bwd_kernel(const bf16_t* __re
           st = mfma(rd_row<HD>(ImA, kt * 16, kk, lane), qf[kk], st);
           dpt = mfma(rd_row<HD>(ImB, kt * 16, kk, lane), df[kk], dpt);
         }
+        if constexpr (k_tail<HD>) {
+          st = mfma16_add(rd_row16<HD>(ImA, kt * 16, lane), qf16, st);
+          dpt = mfma16_add(rd_row16<HD>(ImB, kt * 16, lane), df16, dpt);
+        }
         // Padded keys (rows N.. of the zero-filled K / V images) need no mask here: their dP = dO V^T
         // is 0, so they add nothing to delta, and their dS only meets the zero K rows in dQ = dS K.
         // Their exponent -LSE is clamped at 0 so that P stays finite whatever the query's LSE (unclamped,
@@ -353,7 +399,8 @@ __global__ void __launch_bounds__(NW * 64, 2) attn_bwd_kernel(const bf16_t* __re
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const float e = st[r] * c - ls;
-          const float pv = ex2(fminf(e, 0.f) + nan_of(e));
+          // only the last two tiles can hold padded keys (N > 16 (NKT - 2)): the others skip the clamp
+          const float pv = kt >= NKT - 2 ? ex2(fminf(e, 0.f) + nan_of(e)) : ex2(e);
           P[kt][r] = pv;
           dlr[r] += pv * dpt[r];
         }
@@ -380,6 +427,14 @@ __global__ void __launch_bounds__(NW * 64, 2) attn_bwd_kernel(const bf16_t* __re
 #pragma unroll
         for (int dt = 0; dt < HD / 16; ++dt) dq[dt] = mfma(rd_tr<HD>(ImA, 2 * ks, 2 * ks + 1, dt * 16, lane), bD, dq[dt]);
       }
+      if constexpr (NKT % 2 == 1) {  // odd tile count (hd 80 images hold ceil(N / 16) tiles): a 16-k step
+        v4f d0;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) d0[r] = P[NKT - 1][r] * (DP[NKT - 1][r] - dl);
+        const v4s bD = pack4(d0);
+#pragma unroll
+        for (int dt = 0; dt < HD / 16; ++dt) dq[dt] = mfma16_add(rd_tr1<HD>(ImA, NKT - 1, dt * 16, lane), bD, dq[dt]);
+      }
       if (q < N) {
         uint2 pk[HD / 16];
 #pragma unroll
@@ -392,12 +447,7 @@ __global__ void __launch_bounds__(NW * 64, 2) attn_bwd_kernel(const bf16_t* __re
 #pragma unroll
         for (int dt = 0; dt < HD / 16; ++dt) keep_live2(pk[dt]);
       }
-      if (bias_partial) {
-#pragma unroll
-        for (int dt = 0; dt < HD / 16; ++dt)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) bq[dt][r] += dq[dt][r];  // padded queries: dS = 0; lanes summed at the end
-      }
+      if (bias_partial) add_colsums<HD>(bs_w, dq, scale, lane);  // padded queries: dS = 0
     }
   } else {
     for (int qp = wave; qp < npair; qp += NW) {
@@ -507,57 +557,83 @@ __global__ void __launch_bounds__(NW * 64, 2) attn_bwd_kernel(const bf16_t* __re
             if (d < hd) store4(dq_base + (long)q * rs + d, dq[u][dt], scale);
           }
         }
-        if (bias_partial) {
-  #pragma unroll
-          for (int dt = 0; dt < HD / 16; ++dt)
-  #pragma unroll
-            for (int r = 0; r < 4; ++r) bq[dt][r] += dq[u][dt][r];  // padded queries: dS = 0
-        }
+        if (bias_partial) add_colsums<HD>(bs_w, dq[u], scale, lane);  // padded queries: dS = 0
       }
     }
 
-  }
-  if (bias_partial) {  // the wave's dQ column sums leave registers before stage 2
-#pragma unroll
-    for (int dt = 0; dt < HD / 16; ++dt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float v = sum16(bq[dt][r]);
-        if (i == 0) bsum[(wave * 3 + 0) * HD + dt * 16 + 4 * g + r] = v * scale;
-      }
   }
   // stage 2's first key pair per wave (kp = wave) takes its K / V rows from the stage-1 images before
   // they are overwritten (rows past N are the images' zero padding): K and V of those pairs are read
   // from HBM once instead of twice; later pairs are requested from HBM one pair ahead as before
   v8bf kn[2][HD / 32], vn[2][HD / 32];  // next pair's K / V rows
+  v4s kn16[2] = {}, vn16[2] = {};       // hd 80: their 16-k tails
   asm volatile("" ::: "memory");
 #pragma unroll
-  for (int t = 0; t < 2; ++t)
+  for (int t = 0; t < 2; ++t) {
+    // an odd image has no tile 2 npair - 1 (its keys are all padding: zeros)
+    const bool in = wave < npair && 2 * wave + t < NKT;
 #pragma unroll
     for (int kk = 0; kk < HD / 32; ++kk) {
-      kn[t][kk] = wave < npair ? rd_row<HD>(ImA, (2 * wave + t) * 16, kk, lane) : v8bf{};
-      vn[t][kk] = wave < npair ? rd_row<HD>(ImB, (2 * wave + t) * 16, kk, lane) : v8bf{};
+      kn[t][kk] = in ? rd_row<HD>(ImA, (2 * wave + t) * 16, kk, lane) : v8bf{};
+      vn[t][kk] = in ? rd_row<HD>(ImB, (2 * wave + t) * 16, kk, lane) : v8bf{};
     }
+    if constexpr (k_tail<HD>) {
+      kn16[t] = in ? rd_row16<HD>(ImA, (2 * wave + t) * 16, lane) : v4s{0, 0, 0, 0};
+      vn16[t] = in ? rd_row16<HD>(ImB, (2 * wave + t) * 16, lane) : v4s{0, 0, 0, 0};
+    }
+  }
+  A2STAMP(2);
   __syncthreads();  // K / V images no longer read; delta complete
 
   // ---- stage 2: dK and dV, key-tile pairs ----
   // Q, dO: only the query pairs stage 2 visits (rows past nqa read as zeros without a memory access)
   load_images<HD, NP, NW * 64>(ImA, base, rs, ImB, dob, D, min(N, 32 * npair_q), hd);
   __syncthreads();
+  A2STAMP(3);
   // the last query pair may hold one wholly padded 16-row tile (N % 32 in 1..16): its S / dP
   // products are skipped (P = dS = 0 there)
   const bool last_half = (2 * npair - 1) * 16 >= N;
-  for (int kp = wave; kp < npair; kp += NW) {
-    v8bf kf[2][HD / 32], vf[2][HD / 32];
+  // 8 waves: at most two pairs a wave at N <= 320; the pair after the first is loaded when it starts
+  // (no prefetch registers)
+  v8bf kf[2][HD / 32], vf[2][HD / 32];
+  v4s kf16[2] = {}, vf16[2] = {};
+  if constexpr (NW == 8) {
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
+    for (int t = 0; t < 2; ++t) {
 #pragma unroll
       for (int kk = 0; kk < HD / 32; ++kk) {
         kf[t][kk] = kn[t][kk];
         vf[t][kk] = vn[t][kk];
-        kn[t][kk] = gl_row<HD>(base + D, rs, (2 * (kp + NW) + t) * 16, kk, N, hd, lane);
-        vn[t][kk] = gl_row<HD>(base + 2 * D, rs, (2 * (kp + NW) + t) * 16, kk, N, hd, lane);
       }
+      kf16[t] = kn16[t];
+      vf16[t] = vn16[t];
+    }
+  }
+  for (int kp = wave; kp < npair; kp += NW) {
+    if constexpr (NW == 4) {
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int kk = 0; kk < HD / 32; ++kk) {
+          kf[t][kk] = kn[t][kk];
+          vf[t][kk] = vn[t][kk];
+          kn[t][kk] = gl_row<HD>(base + D, rs, (2 * (kp + NW) + t) * 16, kk, N, hd, lane);
+          vn[t][kk] = gl_row<HD>(base + 2 * D, rs, (2 * (kp + NW) + t) * 16, kk, N, hd, lane);
+        }
+    } else if (kp != wave) {
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+#pragma unroll
+        for (int kk = 0; kk < HD / 32; ++kk) {
+          kf[t][kk] = gl_row<HD>(base + D, rs, (2 * kp + t) * 16, kk, N, hd, lane);
+          vf[t][kk] = gl_row<HD>(base + 2 * D, rs, (2 * kp + t) * 16, kk, N, hd, lane);
+        }
+        if constexpr (k_tail<HD>) {
+          kf16[t] = gl_row16<HD>(base + D, rs, (2 * kp + t) * 16, N, hd, lane);
+          vf16[t] = gl_row16<HD>(base + 2 * D, rs, (2 * kp + t) * 16, N, hd, lane);
+        }
+      }
+    }
     v4f dv[2][HD / 16], dk[2][HD / 16];
 #pragma unroll
     for (int t = 0; t < 2; ++t)
@@ -581,6 +657,11 @@ __global__ void __launch_bounds__(NW * 64, 2) attn_bwd_kernel(const bf16_t* __re
           qr[kk] = rd_row<HD>(ImA, qt * 16, kk, lane);
           orow[kk] = rd_row<HD>(ImB, qt * 16, kk, lane);
         }
+        v4s qr16 = {0, 0, 0, 0}, or16 = {0, 0, 0, 0};
+        if constexpr (k_tail<HD>) {
+          qr16 = rd_row16<HD>(ImA, qt * 16, lane);
+          or16 = rd_row16<HD>(ImB, qt * 16, lane);
+        }
         // queries 16qt + 4g + r, r = 0..3: one 16-B read each of lse and delta
         const v4f lq = *reinterpret_cast<const v4f*>(lse_s + qt * 16 + 4 * g);
         const v4f dq4 = *reinterpret_cast<const v4f*>(dlt_s + qt * 16 + 4 * g);
@@ -592,6 +673,10 @@ __global__ void __launch_bounds__(NW * 64, 2) attn_bwd_kernel(const bf16_t* __re
             sv = mfma(qr[kk], kf[t][kk], sv);
             dp = mfma(orow[kk], vf[t][kk], dp);
           }
+          if constexpr (k_tail<HD>) {
+            sv = mfma16_add(qr16, kf16[t], sv);
+            dp = mfma16_add(or16, vf16[t], dp);
+          }
           const bool kvalid = (2 * kp + t) * 16 + i < N;
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
@@ -600,6 +685,20 @@ __global__ void __launch_bounds__(NW * 64, 2) attn_bwd_kernel(const bf16_t* __re
             DS[t][u][r] = p * (dp[r] - dq4[r]);
           }
         }
+      }
+      if (NKT % 2 == 1 && qs == npair - 1) {  // odd image: query tile 2 qs alone (a 16-k step)
+        const v4s bP0 = pack4(P[0][0]), bP1 = pack4(P[1][0]);
+        const v4s bD0 = pack4(DS[0][0]), bD1 = pack4(DS[1][0]);
+#pragma unroll
+        for (int dt = 0; dt < HD / 16; ++dt) {
+          const v4s ot = rd_tr1<HD>(ImB, 2 * qs, dt * 16, lane);
+          const v4s qt = rd_tr1<HD>(ImA, 2 * qs, dt * 16, lane);
+          dv[0][dt] = mfma16_add(ot, bP0, dv[0][dt]);
+          dv[1][dt] = mfma16_add(ot, bP1, dv[1][dt]);
+          dk[0][dt] = mfma16_add(qt, bD0, dk[0][dt]);
+          dk[1][dt] = mfma16_add(qt, bD1, dk[1][dt]);
+        }
+        continue;
       }
       const v8bf bP0 = pack8(P[0][0], P[0][1]), bP1 = pack8(P[1][0], P[1][1]);
       const v8bf bD0 = pack8(DS[0][0], DS[0][1]), bD1 = pack8(DS[1][0], DS[1][1]);
@@ -634,14 +733,9 @@ __global__ void __launch_bounds__(NW * 64, 2) attn_bwd_kernel(const bf16_t* __re
           }
         }
       }
-      if (bias_partial) {
-#pragma unroll
-        for (int dt = 0; dt < HD / 16; ++dt)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {  // invalid keys hold exact zeros (P = 0)
-            bk[dt][r] += dk[t][dt][r];
-            bv[dt][r] += dv[t][dt][r];
-          }
+      if (bias_partial) {  // invalid keys hold exact zeros (P = 0)
+        add_colsums<HD>(bs_w + HD, dk[t], scale, lane);
+        add_colsums<HD>(bs_w + 2 * HD, dv[t], 1.0f, lane);
       }
     }
 #pragma unroll
@@ -653,26 +747,8 @@ __global__ void __launch_bounds__(NW * 64, 2) attn_bwd_kernel(const bf16_t* __re
       }
   }
 
+  A2STAMP(4);
   if (bias_partial) {
-    // per-lane partials -> the wave's column sums for d = 16dt + 4g + r (sum over the 16 lanes i),
-    // then a fixed-order sum over waves
-#pragma unroll
-    for (int dt = 0; dt < HD / 16; ++dt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        bk[dt][r] = sum16(bk[dt][r]);
-        bv[dt][r] = sum16(bv[dt][r]);
-      }
-    if (i == 0) {  // the dQ sums were stored after stage 1
-#pragma unroll
-      for (int dt = 0; dt < HD / 16; ++dt)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int d = dt * 16 + 4 * g + r;
-          bsum[(wave * 3 + 1) * HD + d] = bk[dt][r] * scale;
-          bsum[(wave * 3 + 2) * HD + d] = bv[dt][r];
-        }
-    }
     __syncthreads();
     for (int e = threadIdx.x; e < 3 * HD; e += blockDim.x) {
       const int z = e / HD, d = e % HD;
@@ -683,6 +759,7 @@ __global__ void __launch_bounds__(NW * 64, 2) attn_bwd_kernel(const bf16_t* __re
       bias_partial[(long)b * 3 * D + z * D + h * hd + d] = acc;
     }
   }
+  A2STAMP(5);
 }
 
 template <int HD, int NKT, int NW>
@@ -705,28 +782,37 @@ hipError_t launch_fwd2(const bf16_t* qkv, bf16_t* o, float* lse, int B, int N, i
   return hipGetLastError();
 }
 
-// Forward: the lean 8-wave kernel (attn_fwd2_kernel) for head widths up to 64; hd 80 / 96 (ViT-H/14) on
-// the 4-wave kernel, whose registers hold one 16-query strip at a time
+// Forward: the lean 8-wave kernel (attn_fwd2_kernel) for image widths 32, 64 and 80 (ViT-H/14's hd 80:
+// one workgroup per CU); 96 on the 4-wave kernel, whose registers hold one 16-query strip at a time
 template <int HD, int NKT>
 hipError_t launch_fwd(const bf16_t* qkv, bf16_t* o, float* lse, int B, int N, int H, int hd, float scale,
                       int nq, hipStream_t s) {
-  if (HD <= 64) {  // NKT = 2 * ceil(N / 32); the lean kernel takes ceil(N / 16) tiles
+  if constexpr (HD != 96) {  // NKT = 2 * ceil(N / 32); the lean kernel takes ceil(N / 16) tiles
     if ((N + 15) / 16 == NKT) return launch_fwd2<HD, NKT>(qkv, o, lse, B, N, H, hd, scale, nq, s);
     return launch_fwd2<HD, NKT - 1>(qkv, o, lse, B, N, H, hd, scale, nq, s);
+  } else {
+    return launch_fwd_nw<HD, NKT, 4>(qkv, o, lse, B, N, H, hd, scale, nq, s);
   }
-  return launch_fwd_nw<HD, NKT, 4>(qkv, o, lse, B, N, H, hd, scale, nq, s);
 }
 
-// Backward: the two-stage kernel, 4 waves (two workgroups per CU)
+// Backward: the two-stage kernel, 4 waves (two workgroups per CU); 80-wide images (hd 80): 8 waves and
+// ceil(N / 16) tiles (97 KB at N = 257: one workgroup per CU, two waves per SIMD)
 template <int HD, int NKT>
-hipError_t launch_bwd(const bf16_t* qkv, const bf16_t* dout, const float* lse, bf16_t* dqkv, float* bias_partial,
-                      int B, int N, int H, int hd, float scale, int nq, hipStream_t s) {
-  constexpr int NW = 4;
+hipError_t launch_bwd1(const bf16_t* qkv, const bf16_t* dout, const float* lse, bf16_t* dqkv, float* bias_partial,
+                       int B, int N, int H, int hd, float scale, int nq, hipStream_t s) {
+  constexpr int NW = k_tail<HD> ? 8 : 4;
   const size_t lds = (size_t)2 * NKT * 16 * HD * 2 + 2 * NKT * 16 * 4 + (size_t)NW * 3 * HD * 4;
   auto kern = attn_bwd_kernel<HD, NKT, NW>;
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   hipLaunchKernelGGL(kern, dim3(B * H), dim3(NW * 64), lds, s, qkv, dout, lse, dqkv, bias_partial, N, H, hd, scale, nq);
   return hipGetLastError();
+}
+template <int HD, int NKT>
+hipError_t launch_bwd(const bf16_t* qkv, const bf16_t* dout, const float* lse, bf16_t* dqkv, float* bias_partial,
+                      int B, int N, int H, int hd, float scale, int nq, hipStream_t s) {
+  if constexpr (k_tail<HD>)
+    if ((N + 15) / 16 < NKT) return launch_bwd1<HD, NKT - 1>(qkv, dout, lse, dqkv, bias_partial, B, N, H, hd, scale, nq, s);
+  return launch_bwd1<HD, NKT>(qkv, dout, lse, dqkv, bias_partial, B, N, H, hd, scale, nq, s);
 }
 
 #define VIT_NKT_CASES(X) X(2) X(4) X(6) X(8) X(10) X(12) X(14) X(16) X(18) X(20)
@@ -763,9 +849,9 @@ int check_shape(int64_t B, int64_t N, int64_t H, int64_t hd) {
   return VIT_OK;
 }
 
-// LDS image width: the head dim rounded up to the MFMA k-depth (32): 32, 64 or 96 (hd 80 of ViT-H/14
-// runs on 96-wide images whose last 16 columns are zero).
-int image_width(int64_t hd) { return hd <= 32 ? 32 : hd <= 64 ? 64 : 96; }
+// LDS image width: the head dim rounded up to the MFMA k-depth (32): 32, 64 or 96, except hd 80
+// (ViT-H/14), whose 80-wide images take a 16-k tail step (v_mfma_f32_16x16x16_bf16).
+int image_width(int64_t hd) { return hd <= 32 ? 32 : hd <= 64 ? 64 : hd == 80 ? 80 : 96; }
 
 constexpr int64_t RESIDENT_MAX_N = 320;  // all keys of a head in LDS (attn_fwd_kernel / attn_bwd_kernel)
 
@@ -819,6 +905,7 @@ extern "C" int vit_attention_fwd_ex(const void* qkv, void* o, float* lse, int64_
   switch (image_width(hd)) {
     case 32: e = dispatch_fwd<32>(nkt, q, (bf16_t*)o, lse, (int)B, (int)N, (int)H, (int)hd, scale, nq, s); break;
     case 64: e = dispatch_fwd<64>(nkt, q, (bf16_t*)o, lse, (int)B, (int)N, (int)H, (int)hd, scale, nq, s); break;
+    case 80: e = dispatch_fwd<80>(nkt, q, (bf16_t*)o, lse, (int)B, (int)N, (int)H, (int)hd, scale, nq, s); break;
     default: e = dispatch_fwd<96>(nkt, q, (bf16_t*)o, lse, (int)B, (int)N, (int)H, (int)hd, scale, nq, s); break;
   }
   return vit::check_hip(e, "vit_attention_fwd launch");
@@ -867,6 +954,9 @@ extern "C" int vit_attention_bwd_ex(const void* qkv, const void* o, const void* 
       break;
     case 64:
       e = dispatch_bwd<64>(nkt, q, d, lse, (bf16_t*)dqkv, bias_partial, (int)B, (int)N, (int)H, (int)hd, scale, nq, s);
+      break;
+    case 80:
+      e = dispatch_bwd<80>(nkt, q, d, lse, (bf16_t*)dqkv, bias_partial, (int)B, (int)N, (int)H, (int)hd, scale, nq, s);
       break;
     default:
       e = dispatch_bwd<96>(nkt, q, d, lse, (bf16_t*)dqkv, bias_partial, (int)B, (int)N, (int)H, (int)hd, scale, nq, s);

@@ -86,32 +86,6 @@ __device__ __forceinline__ void lds_barrier() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
-// Column sums over the 16 lanes of a DPP row for 16 values at once: v[k] of every lane of the row summed, the
-// total of v[k] landing in lane k of the row (a fixed-order butterfly, deterministic). Each step halves the
-// values a lane holds: the lane keeps the half selected by one bit of its row index and adds what its
-// partner (ror 8, half-mirror, xor 2, xor 1: partners differ in that bit and agree on the bits already
-// used) sends of the same half: 8 + 4 + 2 + 1 DPP moves instead of 16 x 4 row-sum steps.
-template <int CTRL>
-__device__ __forceinline__ float dpp_mov(float x) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), CTRL, 0xf, 0xf, false));
-}
-template <int NV, int CTRL>
-__device__ __forceinline__ void butterfly_step(float* v, bool upper) {
-#pragma unroll
-  for (int k = 0; k < NV / 2; ++k) {
-    const float keep = upper ? v[k + NV / 2] : v[k];
-    const float send = upper ? v[k] : v[k + NV / 2];
-    v[k] = keep + dpp_mov<CTRL>(send);
-  }
-}
-__device__ __forceinline__ float reduce16(float (&v)[16], int i) {
-  butterfly_step<16, 0x128>(v, (i & 8) != 0);  // row_ror:8 (lane ^ 8)
-  butterfly_step<8, 0x141>(v, (i & 4) != 0);   // row_half_mirror (j <-> 7 - j within 8 lanes)
-  butterfly_step<4, 0x4E>(v, (i & 2) != 0);    // quad_perm [2,3,0,1] (lane ^ 2)
-  butterfly_step<2, 0xB1>(v, (i & 1) != 0);    // quad_perm [1,0,3,2] (lane ^ 1)
-  return v[0];
-}
-
 // the lane index, recomputed where it is used (opaque to CSE): lane-derived offsets of a later phase are
 // rebuilt from it instead of being kept live (and spilled) across the register-heavy stage before it
 __device__ __forceinline__ int lane_now() {
@@ -349,7 +323,7 @@ __global__ void __launch_bounds__(PB_NW * 64, 1) attn_bwd_pers_kernel(const bf16
         for (int r = 0; r < 4; ++r) d0[r] = P[NKT - 1][r] * (DP[NKT - 1][r] - dl);
         const v4s bD = pack4(d0);
 #pragma unroll
-        for (int dt = 0; dt < HD / 16; ++dt) dq[dt] = mfma16(lds_tr(Ki + (NKT - 1) * T + L.tr[dt]), bD, dq[dt]);
+        for (int dt = 0; dt < HD / 16; ++dt) dq[dt] = mfma16_add(lds_tr(Ki + (NKT - 1) * T + L.tr[dt]), bD, dq[dt]);
       }
       STAMP1(4);
       {
@@ -468,10 +442,10 @@ __global__ void __launch_bounds__(PB_NW * 64, 1) attn_bwd_pers_kernel(const bf16
           for (int dt = 0; dt < HD / 16; ++dt) {
             const v4s ot = lds_tr(Oi + 2 * qs * T + L2.tr[dt]);
             const v4s qtr = lds_tr(Qi + 2 * qs * T + L2.tr[dt]);
-            dv[0][dt] = mfma16(ot, bP0, dv[0][dt]);
-            dk[0][dt] = mfma16(qtr, bD0, dk[0][dt]);
-            dv[1][dt] = mfma16(ot, bP1, dv[1][dt]);
-            dk[1][dt] = mfma16(qtr, bD1, dk[1][dt]);
+            dv[0][dt] = mfma16_add(ot, bP0, dv[0][dt]);
+            dk[0][dt] = mfma16_add(qtr, bD0, dk[0][dt]);
+            dv[1][dt] = mfma16_add(ot, bP1, dv[1][dt]);
+            dk[1][dt] = mfma16_add(qtr, bD1, dk[1][dt]);
           }
         }
       };

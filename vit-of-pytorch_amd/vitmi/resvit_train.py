@@ -70,6 +70,75 @@ def train_step(model, x, y, optimizer, lr_scheduler=None, lambda_active=10.0, la
     return total, c_loss, a_loss, d_loss, r_entropy, active_metric
 
 
+class GraphedTrainStep:
+    """train_step with its forward + backward captured once in a HIP graph and replayed.
+
+    The Res-ViT step is launch-bound when issued op by op (about 2,300 kernels at Res-ViT-B/16 bs 128, many
+    of them the small routing / selection ops of the reference's model, res-vit/model.py:133-211,336-368):
+    the host's issue rate leaves the GPU idle for a fifth of the step. Captured, the forward (teacher +
+    routed student), the losses and the backward replay as one graph; zero_grad, the clip + AdamW update
+    (three launches) and the LR schedule run eagerly after it, so the optimizer keeps reading its host
+    hyper-parameters. The step's data-dependent decisions are all on the device already (routing masks,
+    the approximators' participation flags of vitmi.flat.gate), so the graph computes exactly what
+    train_step does; its inputs are the static `x` / `y` buffers (copy a new batch in with `step(x, y)`)
+    and its outputs are static tensors overwritten by every replay.
+
+    Single process (no gradient all-reduce hooks: a data-parallel step stays on train_step).
+    """
+
+    def __init__(self, model, x, y, optimizer, lr_scheduler=None, lambda_active=10.0, lambda_distill=1.0,
+                 lambda_class=10.0, clip_grad_norm=True, warmup=1):
+        from . import flat as _flat
+        if not isinstance(optimizer, AdamW):
+            raise TypeError("GraphedTrainStep: vitmi.optim.AdamW (flat gradients at fixed addresses) expected")
+        self.model, self.opt, self.sched = model, optimizer, lr_scheduler
+        self.lambdas = (lambda_active, lambda_distill, lambda_class)
+        self.clip = clip_grad_norm
+        self.x, self.y = x.clone(), y.clone()
+        self._flat = _flat
+        # eager warm-up (lazy initialisation, cached device constants, kernel attributes) on the side stream the
+        # graph is then captured on: autograd runs each parameter's gradient accumulation on the stream its
+        # AccumulateGrad node was created on, and the model keeps the warm-up's graph (and those nodes) alive
+        # through `model.logits`; on any other stream the accumulation would escape the capture
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(warmup):
+                train_step(model, self.x, self.y, optimizer, lr_scheduler, *self.lambdas, clip_grad_norm)
+            optimizer.zero_grad()
+        torch.cuda.current_stream().wait_stream(s)
+        f = optimizer.flat
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph, stream=s):
+            c_loss, a_loss, d_loss, r_entropy, active_metric = model(self.x, self.y)
+            total = total_loss(model, c_loss, a_loss, d_loss, *self.lambdas)
+            total.backward()
+        self.outputs = (total, c_loss, a_loss, d_loss, r_entropy, active_metric)
+        # what the captured pass left on the host: the used flags (post-accumulate hooks) and the gated
+        # parameters' device flags (graph outputs, refreshed by every replay)
+        self.used = list(f.used_host)
+        self.gates = [(p, e[1]) for p in f.params for e in [_flat._GATES.get(id(p))] if e is not None and e[0]() is p]
+
+    def step(self, x=None, y=None):
+        """one training step; returns train_step's tuple (static device tensors: clone what you keep)"""
+        import weakref
+        if x is not None:
+            self.x.copy_(x)
+            self.y.copy_(y)
+        f = self.opt.flat
+        self.opt.zero_grad()
+        self.graph.replay()
+        f.used_host = list(self.used)
+        for p, flag in self.gates:
+            self._flat._GATES[id(p)] = (weakref.ref(p), flag)
+        if self.clip and self.opt.max_grad_norm is None:
+            clip_grad_norm_(None, max_norm=1.0, norm_type=2, flat=self.opt)
+        self.opt.step()
+        if self.sched is not None:
+            self.sched.step()
+        return self.outputs
+
+
 def train_epoch(epoch, model, data_loader, optimizer, metrics, config, lr_scheduler=None, lambda_active=10.0,
                 lambda_distill=1.0, lambda_class=10.0, device=torch.device("cpu"), save_routing_viz=False,
                 reducer=None):
