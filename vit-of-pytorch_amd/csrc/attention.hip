@@ -797,252 +797,6 @@ hipError_t launch_fwd(const bf16_t* qkv, bf16_t* o, float* lse, int B, int N, in
 
 // Backward: the two-stage kernel, 4 waves (two workgroups per CU); 80-wide images (hd 80): 8 waves and
 // ceil(N / 16) tiles (97 KB at N = 257: one workgroup per CU, two waves per SIMD)
-// ------------------------------------------------------------------------------------------------
-// Backward for 80-wide images (hd 80, ViT-H/14), 16 waves. K / V (then Q / dO) of one (image, head) take
-// 87 KB of LDS at N = 257, so one workgroup holds a CU; the 8-wave two-stage kernel above then runs two waves
-// per SIMD with all keys' P and dP of a strip in registers, and its phases ran at ~1/4 of their MFMA time
-// (stamps, round 4: issue and LDS latency with nothing to switch to). Here 16 waves (four per SIMD, 128
-// VGPRs each) and no per-strip key arrays:
-//   stage 1 (K, V images), per 16-query strip: pass A streams the key tiles for delta = sum P dP (exact, as
-//     above), pass B recomputes S and dP tile pair by tile pair for dS = P (dP - delta) and dQ = dS K;
-//   stage 2 (Q, dO images), per 16-key tile (17 tiles at N = 257 on 16 waves): dV = P^T dO, dK = dS^T Q over
-//     query-tile pairs, P and dP recomputed.
-// The 16 columns past hd 80 of a row fragment are a third 32-k MFMA step whose register operand (Q / dO rows
-// in stage 1, K / V rows in stage 2, loaded with zeros past hd) is zero there: the image side reads the next
-// row's first 32 bytes, or 32 zero bytes kept after the second image (finite values times zero). dQ, dK and
-// dV leave through wave-private LDS strips as whole rows; bias partials through the DPP column sums.
-template <int HD, int NKT>
-__global__ void __launch_bounds__(1024, 1) attn_bwd16_kernel(const bf16_t* __restrict__ qkv,
-                                                             const bf16_t* __restrict__ dout,
-                                                             const float* __restrict__ lse, bf16_t* __restrict__ dqkv,
-                                                             float* __restrict__ bias_partial, int N, int H, int hd,
-                                                             float scale, int nq) {
-  constexpr int NW = 16;
-  constexpr int KC = (HD + 31) / 32;  // 32-k steps per row (the last one half zero on the register side)
-  constexpr int NP = NKT * 16;
-  constexpr int IMG = NP * HD * 2;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* ImA = smem;        // K, then Q
-  char* ImB = smem + IMG;  // V, then dO
-  float* pad = reinterpret_cast<float*>(smem + 2 * IMG);  // 32 zero bytes: ImB's last row + 1 fragment
-  float* lse_s = pad + 8;
-  float* dlt_s = lse_s + NP;
-  float* bsum = dlt_s + NP;  // [NW][3][HD]
-  lds_t* strips = (lds_t*)(smem + 2 * IMG + 32 + (2 * NP + NW * 3 * HD) * 4);
-
-  const int bh = blockIdx.x, b = bh / H, h = bh % H;
-  const int D = H * hd;
-  const long rs = 3L * D;
-  const bf16_t* base = qkv + (long)b * N * rs + (long)h * hd;
-  const bf16_t* dob = dout + (long)b * N * D + (long)h * hd;
-  bf16_t* dq_base = dqkv + (long)b * N * rs + (long)h * hd;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int g = lane >> 4, i = lane & 15;
-  const float c = scale * LOG2E;
-  float* bs_w = bsum + wave * 3 * HD;
-  lds_t* so = strips + wave * StripOut<HD>::BYTES;
-
-  A2STAMP(0);
-  load_images<HD, NP, NW * 64>(ImA, base + D, rs, ImB, base + 2 * D, rs, N, hd);
-  if (threadIdx.x < 8) pad[threadIdx.x] = 0.f;
-  for (int r = threadIdx.x; r < NP; r += blockDim.x) {
-    lse_s[r] = r < N ? lse[(long)bh * N + r] * LOG2E : 1e30f;  // padded queries: P = 2^-1e30 = 0
-    dlt_s[r] = 0.f;
-  }
-  if (bias_partial)
-    for (int e = lane; e < 3 * HD; e += 64) bs_w[e] = 0.f;
-  __syncthreads();
-  A2STAMP(1);
-
-  const int nqa = min(N, (nq + 31) / 32 * 32);  // whole query pairs carry a gradient (see attn_bwd_kernel)
-  const int npair_q = (nqa + 31) / 32;
-  // ---- stage 1: delta and dQ, one 16-query strip at a time ----
-  for (int qt = wave; qt < NKT; qt += NW) {
-    const int q = qt * 16 + i;
-    if (qt * 16 >= nqa) {  // no gradient reaches these queries: dQ = 0, delta = 0
-      if (q < N) {
-#pragma unroll
-        for (int dt = 0; dt < HD / 16; ++dt) store4(dq_base + (long)q * rs + dt * 16 + 4 * g, v4f{0.f, 0.f, 0.f, 0.f}, 1.f);
-      }
-      continue;
-    }
-    v8bf qf[KC], df[KC];
-#pragma unroll
-    for (int kk = 0; kk < KC; ++kk) {
-      qf[kk] = gl_row<HD>(base, rs, qt * 16, kk, N, hd, lane);
-      df[kk] = gl_row<HD>(dob, D, qt * 16, kk, N, hd, lane);
-    }
-    const float ls = lse_s[q];
-    // S^T / dP^T of key tile kt against this strip (keys 4g + r of the tile, query i) and P
-    auto tile = [&](int kt, v4f& pv, v4f& dpt) __attribute__((always_inline)) {
-      v4f st = {0.f, 0.f, 0.f, 0.f};
-      dpt = v4f{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int kk = 0; kk < KC; ++kk) {
-        st = mfma(rd_row<HD>(ImA, kt * 16, kk, lane), qf[kk], st);
-        dpt = mfma(rd_row<HD>(ImB, kt * 16, kk, lane), df[kk], dpt);
-      }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float e = st[r] * c - ls;
-        // only the last tile holds padded keys (zero rows): clamp their exponent (see attn_bwd_kernel)
-        pv[r] = kt == NKT - 1 ? ex2(fminf(e, 0.f) + nan_of(e)) : ex2(e);
-      }
-    };
-    float dlr[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll 2
-    for (int kt = 0; kt < NKT; ++kt) {  // pass A: delta
-      v4f pv, dpt;
-      tile(kt, pv, dpt);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) dlr[r] += pv[r] * dpt[r];
-    }
-    float dl = (dlr[0] + dlr[1]) + (dlr[2] + dlr[3]);
-    dl += __shfl_xor(dl, 16, 64);
-    dl += __shfl_xor(dl, 32, 64);
-    if (q >= N) dl = 0.f;
-    if (g == 0) dlt_s[q] = dl;
-    v4f dq[HD / 16];
-#pragma unroll
-    for (int dt = 0; dt < HD / 16; ++dt) dq[dt] = v4f{0.f, 0.f, 0.f, 0.f};
-#pragma unroll 1
-    for (int ks = 0; ks < NKT / 2; ++ks) {  // pass B: dS and dQ = dS K, key tiles in pairs
-      v4f p0, dp0, p1, dp1, d0, d1;
-      tile(2 * ks, p0, dp0);
-      tile(2 * ks + 1, p1, dp1);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        d0[r] = p0[r] * (dp0[r] - dl);
-        d1[r] = p1[r] * (dp1[r] - dl);
-      }
-      const v8bf bD = pack8(d0, d1);
-#pragma unroll
-      for (int dt = 0; dt < HD / 16; ++dt) dq[dt] = mfma(rd_tr<HD>(ImA, 2 * ks, 2 * ks + 1, dt * 16, lane), bD, dq[dt]);
-    }
-    if constexpr (NKT % 2 == 1) {
-      v4f p0, dp0, d0;
-      tile(NKT - 1, p0, dp0);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) d0[r] = p0[r] * (dp0[r] - dl);
-      const v4s bD = pack4(d0);
-#pragma unroll
-      for (int dt = 0; dt < HD / 16; ++dt) dq[dt] = mfma16_add(rd_tr1<HD>(ImA, NKT - 1, dt * 16, lane), bD, dq[dt]);
-    }
-    StripOut<HD>::stage(so, dq, scale, lane);
-    StripOut<HD>::store(so, dq_base + (long)qt * 16 * rs, rs, N - qt * 16, hd, lane);
-    if (bias_partial) add_colsums<HD>(bs_w, dq, scale, lane);  // padded queries: dS = 0
-  }
-
-  A2STAMP(2);
-  // stage 2's first key tile per wave takes its K / V rows from the stage-1 images (the register side of the
-  // third 32-k step must be zero past hd: the image holds the next row there)
-  v8bf kf[KC], vf[KC];
-  asm volatile("" ::: "memory");
-#pragma unroll
-  for (int kk = 0; kk < KC; ++kk) {
-    const bool in = wave < NKT && kk * 32 + 8 * g < hd;
-    kf[kk] = in ? rd_row<HD>(ImA, wave * 16, kk, lane) : v8bf{};
-    vf[kk] = in ? rd_row<HD>(ImB, wave * 16, kk, lane) : v8bf{};
-  }
-  __syncthreads();  // K / V images no longer read; delta complete
-
-  // ---- stage 2: dK and dV, one 16-key tile at a time ----
-  load_images<HD, NP, NW * 64>(ImA, base, rs, ImB, dob, D, min(N, 32 * npair_q), hd);
-  __syncthreads();
-  A2STAMP(3);
-  for (int kt = wave; kt < NKT; kt += NW) {
-    if (kt != wave) {
-#pragma unroll
-      for (int kk = 0; kk < KC; ++kk) {
-        kf[kk] = gl_row<HD>(base + D, rs, kt * 16, kk, N, hd, lane);
-        vf[kk] = gl_row<HD>(base + 2 * D, rs, kt * 16, kk, N, hd, lane);
-      }
-    }
-    const bool kvalid = kt * 16 + i < N;
-    v4f dv[HD / 16], dk[HD / 16];
-#pragma unroll
-    for (int dt = 0; dt < HD / 16; ++dt) dv[dt] = dk[dt] = v4f{0.f, 0.f, 0.f, 0.f};
-    // P and dS of query tile qt against this key tile (queries 4g + r of the tile, key i)
-    auto qtile = [&](int qtq, v4f& P, v4f& DS) __attribute__((always_inline)) {
-      v4f sv = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int kk = 0; kk < KC; ++kk) {
-        sv = mfma(rd_row<HD>(ImA, qtq * 16, kk, lane), kf[kk], sv);
-        dp = mfma(rd_row<HD>(ImB, qtq * 16, kk, lane), vf[kk], dp);
-      }
-      const v4f lq = *reinterpret_cast<const v4f*>(lse_s + qtq * 16 + 4 * g);
-      const v4f dq4 = *reinterpret_cast<const v4f*>(dlt_s + qtq * 16 + 4 * g);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float p = kvalid ? ex2(sv[r] * c - lq[r]) : 0.f;
-        P[r] = p;
-        DS[r] = p * (dp[r] - dq4[r]);
-      }
-    };
-    const int npq = min(npair_q, NKT / 2);  // whole query-tile pairs
-#pragma unroll 1
-    for (int qs = 0; qs < npq; ++qs) {
-      v4f P0, D0, P1, D1;
-      qtile(2 * qs, P0, D0);
-      qtile(2 * qs + 1, P1, D1);
-      const v8bf bP = pack8(P0, P1), bD = pack8(D0, D1);
-#pragma unroll
-      for (int dt = 0; dt < HD / 16; ++dt) {
-        dv[dt] = mfma(rd_tr<HD>(ImB, 2 * qs, 2 * qs + 1, dt * 16, lane), bP, dv[dt]);
-        dk[dt] = mfma(rd_tr<HD>(ImA, 2 * qs, 2 * qs + 1, dt * 16, lane), bD, dk[dt]);
-      }
-    }
-    if constexpr (NKT % 2 == 1) {
-      if (npair_q * 2 > NKT - 1) {  // the odd last query tile, alone (a 16-k step)
-        v4f P0, D0;
-        qtile(NKT - 1, P0, D0);
-        const v4s bP = pack4(P0), bD = pack4(D0);
-#pragma unroll
-        for (int dt = 0; dt < HD / 16; ++dt) {
-          dv[dt] = mfma16_add(rd_tr1<HD>(ImB, NKT - 1, dt * 16, lane), bP, dv[dt]);
-          dk[dt] = mfma16_add(rd_tr1<HD>(ImA, NKT - 1, dt * 16, lane), bD, dk[dt]);
-        }
-      }
-    }
-    StripOut<HD>::stage(so, dk, scale, lane);
-    StripOut<HD>::store(so, dq_base + (long)kt * 16 * rs + D, rs, N - kt * 16, hd, lane);
-    StripOut<HD>::stage(so, dv, 1.0f, lane);
-    StripOut<HD>::store(so, dq_base + (long)kt * 16 * rs + 2 * D, rs, N - kt * 16, hd, lane);
-    if (bias_partial) {  // invalid keys hold exact zeros (P = 0)
-      add_colsums<HD>(bs_w + HD, dk, scale, lane);
-      add_colsums<HD>(bs_w + 2 * HD, dv, 1.0f, lane);
-    }
-  }
-  A2STAMP(4);
-  if (bias_partial) {
-    __syncthreads();
-    for (int e = threadIdx.x; e < 3 * HD; e += blockDim.x) {
-      const int z = e / HD, d = e % HD;
-      if (d >= hd) continue;
-      float acc = 0.f;
-#pragma unroll
-      for (int w = 0; w < NW; ++w) acc += bsum[(w * 3 + z) * HD + d];
-      bias_partial[(long)b * 3 * D + z * D + h * hd + d] = acc;
-    }
-  }
-  A2STAMP(5);
-}
-
-template <int HD, int NKT>
-constexpr size_t bwd16_lds() {
-  return (size_t)2 * NKT * 16 * HD * 2 + 32 + 2 * NKT * 16 * 4 + (size_t)16 * 3 * HD * 4 + (size_t)16 * StripOut<HD>::BYTES;
-}
-template <int HD, int NKT>
-hipError_t launch_bwd16(const bf16_t* qkv, const bf16_t* dout, const float* lse, bf16_t* dqkv, float* bias_partial,
-                        int B, int N, int H, int hd, float scale, int nq, hipStream_t s) {
-  constexpr size_t lds = bwd16_lds<HD, NKT>();
-  static_assert(lds <= 160 * 1024, "attn_bwd16_kernel: LDS over 160 KiB");
-  auto kern = attn_bwd16_kernel<HD, NKT>;
-  (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL(kern, dim3(B * H), dim3(1024), lds, s, qkv, dout, lse, dqkv, bias_partial, N, H, hd, scale, nq);
-  return hipGetLastError();
-}
-
 template <int HD, int NKT>
 hipError_t launch_bwd1(const bf16_t* qkv, const bf16_t* dout, const float* lse, bf16_t* dqkv, float* bias_partial,
                        int B, int N, int H, int hd, float scale, int nq, hipStream_t s) {
@@ -1056,13 +810,9 @@ hipError_t launch_bwd1(const bf16_t* qkv, const bf16_t* dout, const float* lse, 
 template <int HD, int NKT>
 hipError_t launch_bwd(const bf16_t* qkv, const bf16_t* dout, const float* lse, bf16_t* dqkv, float* bias_partial,
                       int B, int N, int H, int hd, float scale, int nq, hipStream_t s) {
-  if constexpr (k_tail<HD>) {  // 80-wide images: the 16-wave kernel on ceil(N / 16) tiles while its LDS fits
-    if ((N + 15) / 16 < NKT) return launch_bwd16<HD, NKT - 1>(qkv, dout, lse, dqkv, bias_partial, B, N, H, hd, scale, nq, s);
-    if constexpr (NKT <= 19) return launch_bwd16<HD, NKT>(qkv, dout, lse, dqkv, bias_partial, B, N, H, hd, scale, nq, s);
-    else return launch_bwd1<HD, NKT>(qkv, dout, lse, dqkv, bias_partial, B, N, H, hd, scale, nq, s);  // N > 304
-  } else {
-    return launch_bwd1<HD, NKT>(qkv, dout, lse, dqkv, bias_partial, B, N, H, hd, scale, nq, s);
-  }
+  if constexpr (k_tail<HD>)
+    if ((N + 15) / 16 < NKT) return launch_bwd1<HD, NKT - 1>(qkv, dout, lse, dqkv, bias_partial, B, N, H, hd, scale, nq, s);
+  return launch_bwd1<HD, NKT>(qkv, dout, lse, dqkv, bias_partial, B, N, H, hd, scale, nq, s);
 }
 
 #define VIT_NKT_CASES(X) X(2) X(4) X(6) X(8) X(10) X(12) X(14) X(16) X(18) X(20)
