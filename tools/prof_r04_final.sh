@@ -40,3 +40,10 @@ rm -rf $O/fetch $O/write $O/mfma
 head -30 $O/kernel_summary.txt; head -4 $O/step_timeline.txt
 python3 -c "import json;[print(k, round(json.load(open('$O/'+k))['traffic_bytes']/1e6,1),'MB') for k in ['wgrad_traffic.json','fc1_traffic.json','attn_bwd_traffic.json']]"
 head -30 $O/kernel_pmc.txt
+# same-box A/B: the whole B/16 step replayed from one HIP graph (VITMI_BENCH_GRAPH=1) vs eager launches
+for r in 1 2; do
+  for gr in 0 1; do
+    VITMI_BENCH_GRAPH=$gr timeout -k 10 300 python3 -u bench.py --steps 20 --warmup 5 --no-cpu-baseline > $O/b16_graph${gr}_$r.json 2> $O/b16_graph${gr}_$r.err || { tail -5 $O/b16_graph${gr}_$r.err; exit 1; }
+    echo "graph=$gr run $r: $(grep -o '"value": [0-9.]*' $O/b16_graph${gr}_$r.json | head -1)"
+  done
+done
