@@ -218,7 +218,7 @@ __global__ void __launch_bounds__(PB_NW * 64, 1) attn_bwd_pers_kernel(const bf16
     constexpr int SLOT = decltype(slot)::value;
     lds_t* const Qi = (lds_t*)(SLOT ? qo1_s : qo0_s);
     lds_t* const Oi = Qi + IMG;
-    const float* const lse_s = reinterpret_cast<const float*>(SLOT ? ls1_s : ls0_s);
+    float* const lse_s = reinterpret_cast<float*>(SLOT ? ls1_s : ls0_s);
     lds_t* const Qn = (lds_t*)(SLOT ? qo0_s : qo1_s);
     lds_t* const Ln = (lds_t*)(SLOT ? ls0_s : ls1_s);
     const int b = item / H, h = item % H;
@@ -262,6 +262,9 @@ __global__ void __launch_bounds__(PB_NW * 64, 1) attn_bwd_pers_kernel(const bf16
         df[kk] = __builtin_bit_cast(v8bf, lds_ld<v8s>(Oi + qt * T + L.row[kk]));
       }
       const float ls = q < N ? lse_s[q] * LOG2E : 1e30f;  // padded queries: P = 2^-1e30 = 0
+      // stage 2 reads the strip's lse in log2 units (one fma per score there); nothing else reads this slot's
+      // lse before the stage 1 / stage 2 barrier
+      if (g == 0) lse_s[q] = ls;
       STAMP1(1);
       v4f P[NKT], DP[NKT];
       float dlr[4] = {0.f, 0.f, 0.f, 0.f};
@@ -382,13 +385,11 @@ __global__ void __launch_bounds__(PB_NW * 64, 1) attn_bwd_pers_kernel(const bf16
 #pragma unroll
         for (int dt = 0; dt < HD / 16; ++dt) dv[t][dt] = dk[t][dt] = v4f{0.f, 0.f, 0.f, 0.f};
       const bool kv0 = (2 * kp) * 16 + i < N, kv1 = (2 * kp + 1) * 16 + i < N;
-      // one (key pair, query pair) unit; FULL = false: the query pair's second tile is wholly padding (past
-      // the images), so only tile 2 qs is used, with the 16-deep MFMA. Both key tiles are always computed (an
-      // invalid second tile has zero K / V rows and P masked to 0), so the unit has no branch.
-      auto unit = [&](int qs, auto full) {
-        constexpr bool FULL = decltype(full)::value;
-        constexpr int NU = FULL ? 2 : 1;
-        v4f Pm[2][2], DS[2][2];  // [key tile][query tile]
+      // P and dS of the (key pair, query tile 2 qs + u) products, u < NU; MASK: the pair holds padded keys
+      // (only the last pair: their P forced to 0). lse_s holds log2 units since stage 1 (padded queries 1e30).
+      auto scores = [&](int qs, auto nu, auto maskc, v4f (&Pm)[2][2], v4f (&DS)[2][2]) __attribute__((always_inline)) {
+        constexpr int NU = decltype(nu)::value;
+        constexpr bool MASK = decltype(maskc)::value;
 #pragma unroll
         for (int u = 0; u < NU; ++u) {
           const int qt = 2 * qs + u;
@@ -398,9 +399,8 @@ __global__ void __launch_bounds__(PB_NW * 64, 1) attn_bwd_pers_kernel(const bf16
             qr[kk] = __builtin_bit_cast(v8bf, lds_ld<v8s>(Qi + qt * T + L2.row[kk]));
             orow[kk] = __builtin_bit_cast(v8bf, lds_ld<v8s>(Oi + qt * T + L2.row[kk]));
           }
-          // padded queries (rows >= N) have zero Q and dO rows: their P is finite and dP = delta = 0, so they
-          // add nothing to dV = P^T dO or dK = dS^T Q whatever their (zero) lse
-          const v4f lq = *reinterpret_cast<const v4f*>(lse_s + qt * 16 + 4 * g) * LOG2E;
+          // padded queries (rows >= N) have zero Q and dO rows and lse 1e30: P = 0
+          const v4f lq = *reinterpret_cast<const v4f*>(lse_s + qt * 16 + 4 * g);
           const v4f dq4 = *reinterpret_cast<const v4f*>(dlt_s + qt * 16 + 4 * g);
 #pragma unroll
           for (int t = 0; t < 2; ++t) {
@@ -410,48 +410,77 @@ __global__ void __launch_bounds__(PB_NW * 64, 1) attn_bwd_pers_kernel(const bf16
               sv = mfma(qr[kk], kf[t][kk], sv);
               dp = mfma(orow[kk], vf[t][kk], dp);
             }
-            const bool kvalid = t == 0 ? kv0 : kv1;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-              const float pr = ex2(sv[r] * c - lq[r]);
-              const float p = kvalid ? pr : 0.f;
+              float p = ex2(fmaf(sv[r], c, -lq[r]));
+              if constexpr (MASK) p = (t == 0 ? kv0 : kv1) ? p : 0.f;
               Pm[t][u][r] = p;
               DS[t][u][r] = p * (dp[r] - dq4[r]);
             }
           }
         }
-        if constexpr (FULL) {
-          const v8bf bP0 = pack8(Pm[0][0], Pm[0][1]), bP1 = pack8(Pm[1][0], Pm[1][1]);
-          const v8bf bD0 = pack8(DS[0][0], DS[0][1]), bD1 = pack8(DS[1][0], DS[1][1]);
+      };
+      struct Packed {
+        v8bf bP0, bP1, bD0, bD1;
+      };
+      // a whole query-tile pair: its products as the B operands of dV / dK (front), then the 16 MFMAs (back)
+      auto front = [&](int qs, auto maskc) __attribute__((always_inline)) {
+        v4f Pm[2][2], DS[2][2];  // [key tile][query tile]
+        scores(qs, std::integral_constant<int, 2>{}, maskc, Pm, DS);
+        Packed o;
+        o.bP0 = pack8(Pm[0][0], Pm[0][1]);
+        o.bP1 = pack8(Pm[1][0], Pm[1][1]);
+        o.bD0 = pack8(DS[0][0], DS[0][1]);
+        o.bD1 = pack8(DS[1][0], DS[1][1]);
+        return o;
+      };
+      auto back = [&](int qs, const Packed& o) __attribute__((always_inline)) {
 #pragma unroll
-          for (int dt = 0; dt < HD / 16; ++dt) {
-            v8s ot, qtr;
-            ot.lo = lds_tr(Oi + 2 * qs * T + L2.tr[dt]);
-            ot.hi = lds_tr(Oi + (2 * qs + 1) * T + L2.tr[dt]);
-            qtr.lo = lds_tr(Qi + 2 * qs * T + L2.tr[dt]);
-            qtr.hi = lds_tr(Qi + (2 * qs + 1) * T + L2.tr[dt]);
-            dv[0][dt] = mfma(__builtin_bit_cast(v8bf, ot), bP0, dv[0][dt]);
-            dk[0][dt] = mfma(__builtin_bit_cast(v8bf, qtr), bD0, dk[0][dt]);
-            dv[1][dt] = mfma(__builtin_bit_cast(v8bf, ot), bP1, dv[1][dt]);
-            dk[1][dt] = mfma(__builtin_bit_cast(v8bf, qtr), bD1, dk[1][dt]);
-          }
-        } else {
-          const v4s bP0 = pack4(Pm[0][0]), bP1 = pack4(Pm[1][0]);
-          const v4s bD0 = pack4(DS[0][0]), bD1 = pack4(DS[1][0]);
+        for (int dt = 0; dt < HD / 16; ++dt) {
+          v8s ot, qtr;
+          ot.lo = lds_tr(Oi + 2 * qs * T + L2.tr[dt]);
+          ot.hi = lds_tr(Oi + (2 * qs + 1) * T + L2.tr[dt]);
+          qtr.lo = lds_tr(Qi + 2 * qs * T + L2.tr[dt]);
+          qtr.hi = lds_tr(Qi + (2 * qs + 1) * T + L2.tr[dt]);
+          dv[0][dt] = mfma(__builtin_bit_cast(v8bf, ot), o.bP0, dv[0][dt]);
+          dk[0][dt] = mfma(__builtin_bit_cast(v8bf, qtr), o.bD0, dk[0][dt]);
+          dv[1][dt] = mfma(__builtin_bit_cast(v8bf, ot), o.bP1, dv[1][dt]);
+          dk[1][dt] = mfma(__builtin_bit_cast(v8bf, qtr), o.bD1, dk[1][dt]);
+        }
+      };
+      // the query pair's second tile wholly padding (past the images): tile 2 qs alone, the 16-deep MFMA
+      auto half_unit = [&](int qs, auto maskc) __attribute__((always_inline)) {
+        v4f Pm[2][2], DS[2][2];
+        scores(qs, std::integral_constant<int, 1>{}, maskc, Pm, DS);
+        const v4s bP0 = pack4(Pm[0][0]), bP1 = pack4(Pm[1][0]);
+        const v4s bD0 = pack4(DS[0][0]), bD1 = pack4(DS[1][0]);
 #pragma unroll
-          for (int dt = 0; dt < HD / 16; ++dt) {
-            const v4s ot = lds_tr(Oi + 2 * qs * T + L2.tr[dt]);
-            const v4s qtr = lds_tr(Qi + 2 * qs * T + L2.tr[dt]);
-            dv[0][dt] = mfma16_add(ot, bP0, dv[0][dt]);
-            dk[0][dt] = mfma16_add(qtr, bD0, dk[0][dt]);
-            dv[1][dt] = mfma16_add(ot, bP1, dv[1][dt]);
-            dk[1][dt] = mfma16_add(qtr, bD1, dk[1][dt]);
-          }
+        for (int dt = 0; dt < HD / 16; ++dt) {
+          const v4s ot = lds_tr(Oi + 2 * qs * T + L2.tr[dt]);
+          const v4s qtr = lds_tr(Qi + 2 * qs * T + L2.tr[dt]);
+          dv[0][dt] = mfma16_add(ot, bP0, dv[0][dt]);
+          dk[0][dt] = mfma16_add(qtr, bD0, dk[0][dt]);
+          dv[1][dt] = mfma16_add(ot, bP1, dv[1][dt]);
+          dk[1][dt] = mfma16_add(qtr, bD1, dk[1][dt]);
         }
       };
       const int nfull = last_half && npair_q == npair ? npair_q - 1 : npair_q;
-      for (int qs = 0; qs < nfull; ++qs) unit(qs, std::true_type{});
-      if (nfull < npair_q) unit(nfull, std::false_type{});
+      // software-pipelined over query pairs: the products of pair qs + 1 (LDS reads, 16 MFMAs, the exp / dS
+      // VALU) sit in one basic block with pair qs's dV / dK MFMAs, so one wave keeps both pipes busy
+      auto run = [&](auto maskc) __attribute__((always_inline)) {
+        if (nfull > 0) {
+          Packed cur = front(0, maskc);
+          for (int qs = 0; qs + 1 < nfull; ++qs) {
+            const Packed nxt = front(qs + 1, maskc);
+            back(qs, cur);
+            cur = nxt;
+          }
+          back(nfull - 1, cur);
+        }
+        if (nfull < npair_q) half_unit(nfull, maskc);
+      };
+      if (kp == npair - 1) run(std::true_type{});
+      else run(std::false_type{});
       uint2 pk[2][HD / 16], pv[2][HD / 16];
 #pragma unroll
       for (int t = 0; t < 2; ++t)
