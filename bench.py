@@ -425,6 +425,10 @@ def bench_resvit(args, world, rank, dev, backend, comm):
              patch_size=(16, 16), num_classes=100, device="cuda")
     torch.manual_seed(42)
     model = resvit.Transformer(resvit.ModelArgs(**a)).to(dev).train()
+    if os.environ.get("VITMI_RESVIT_APPROX_OPS", "0") != "0":  # A/B: the per-op approximator path
+        for l in model.layers:
+            if hasattr(l, "block_path_approximators"):
+                l.block_path_approximators.fused = False
     opt = AdamW(model.parameters(), lr=1e-4, weight_decay=0.05, betas=(0.9, 0.999), eps=1e-8, max_grad_norm=1.0)
     sched = get_cosine_schedule_with_warmup(opt, 500, 15000)
     reducer = None

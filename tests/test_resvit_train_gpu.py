@@ -365,3 +365,37 @@ def test_fused_layer_matches_per_op_path(dims):
     assert rel(dx1, dx0) < 1e-2
     for a, b in zip(g1, g0):
         assert rel(a, b) < 2e-2
+
+
+@pytest.mark.parametrize("B,N,r", [(3, 197, 16), (2, 17, 256), (1, 65, 32)])
+def test_fused_approximator_matches_per_op_path(B, N, r):
+    """vitmi.resvit_fused.approx_step (one node: down GEMM with a bf16 epilogue, unselected rows zeroed, up GEMM
+    with the f32 residual epilogue) against the per-op path it replaces (HipLinear x2 + add + where,
+    res-vit/model.py:349-368): output, input gradient and both weight gradients bit for bit, routed rows mixed
+    with unrouted ones; T = B*N not a multiple of 64."""
+    from vitmi import resvit
+    torch.manual_seed(7)
+    D = 64
+    bpa = resvit.BlockPathApproximators(D, r, 1).cuda()
+    m = bpa.approximators["0"]
+    with torch.no_grad():  # a visible low-rank update
+        m.down_proj.weight.normal_(0.0, 0.2)
+        m.up_proj.weight.normal_(0.0, 0.2)
+    g = torch.Generator(device="cuda").manual_seed(11)
+    x = torch.randn(B, N, D, device="cuda", generator=g)
+    w = torch.randn(B, N, D, device="cuda", generator=g)
+    idx = torch.randint(0, 2, (B, N, 1), device="cuda", generator=g).float()  # router index 0 -> approximator
+    assert 0 < int((idx == 0).sum()) < B * N
+    res = {}
+    for fused in (True, False):
+        bpa.fused = fused
+        xi = x.clone().requires_grad_(True)
+        for p in m.parameters():
+            p.grad = None
+        out = bpa(xi, idx, [0])
+        (out * w).sum().backward()
+        res[fused] = (out.detach(), xi.grad.detach(), m.down_proj.weight.grad.clone(), m.up_proj.weight.grad.clone())
+    for a, b in zip(res[True], res[False]):
+        assert torch.equal(a, b)
+    sel = (idx == 0).expand(B, N, D)
+    assert torch.equal(res[True][0][~sel], x[~sel])  # unrouted rows pass through unchanged

@@ -347,6 +347,7 @@ class BlockPathApproximators(nn.Module):
     def __init__(self, dim: int, rank: int, block_size: int):
         super().__init__()
         self.block_size = block_size
+        self.fused = True  # training: one fused node per approximator (vitmi.resvit_fused.approx_step)
         self.approximators = nn.ModuleDict()
         total = 2 ** block_size
         for key in range(total):
@@ -366,7 +367,10 @@ class BlockPathApproximators(nn.Module):
                     continue
                 sel = (idx == key).unsqueeze(-1)
                 m = self.approximators[str(key)]
-                x = torch.where(sel, HF.add(m(x), x), x)
+                if self.fused and _fused.approx_supported(m, x):
+                    x = _fused.approx_step(m, x, sel)  # same values, no f32 add / where passes
+                else:
+                    x = torch.where(sel, HF.add(m(x), x), x)
                 _flat.gate(m.parameters(), sel.any())
             return x
         for key in keys:

@@ -238,3 +238,98 @@ def full_layer(block, x):
     a = block.attention
     return _FusedLayer.apply(x, a.lora_q.lora_A.weight, a.lora_q.lora_B.weight, a.lora_k.lora_A.weight,
                              a.lora_k.lora_B.weight, a.lora_v.lora_A.weight, a.lora_v.lora_B.weight, block)
+
+
+# ---- routed low-rank approximator step (res-vit/model.py:319-368) ------------------------------------
+class _ApproxStep(torch.autograd.Function):
+    """x_new = where(sel, x + up(down(x)), x) for one approximator of BlockPathApproximators (training path),
+    as one node: x [T][D] f32, down_proj.weight Wd [r][D], up_proj.weight Wu [D][r] (nn.Linear layouts), sel
+    [T] bool. Forward: h = bf16(x) Wd^T written as bf16 by the GEMM epilogue, its unselected rows zeroed, then
+    x + h Wu^T by the bias + f32-residual epilogue — an unselected row gets x + 0 = x, so neither the per-op
+    path's f32 add nor its `where` pass remains. Backward: dh = (dout Wu) masked to the selected rows, dx =
+    dout + dh Wd (residual epilogue), dWu = dout^T h, dWd = dh^T bf16(x) (split-K over tokens). Same
+    operands and roundings as the per-op path (vitmi.functional.HipLinear + add + where), so the results
+    agree bit for bit (tests/test_resvit_train_gpu.py)."""
+
+    @staticmethod
+    def forward(ctx, x, wd, wu, sel):
+        B, N, D = x.shape
+        T = B * N
+        r = wd.shape[0]
+        kp, rp, rk = _rup(D, 64), _rup(max(T, 1), 64), _rup(r, 64)
+        dev = x.device
+        x2 = x.contiguous().float().view(T, D)
+        xb = torch.empty(rp, kp, device=dev, dtype=BF16)
+        ops.cast_pad_rows(x2, T, D, xb, kp)
+        if rp > T:
+            ops.zero_(xb[T:])
+        wdb = torch.empty(r, kp, device=dev, dtype=BF16)  # B(k, n) = Wd[n][k]: K-contiguous
+        ops.cast_pad_rows(wd.detach().float().contiguous(), r, D, wdb, kp)
+        hb = torch.empty(rp, rk, device=dev, dtype=BF16)
+        if rp > T or rk > r:
+            ops.zero_(hb)
+        ops.gemm(xb, wdb, hb, T, r, kp, a_layout=K_CONTIG, b_layout=K_CONTIG, lda=kp, ldb=kp, ldc=rk,
+                 epilogue=EPI_BF16)
+        selb = sel.reshape(T, 1).to(BF16)
+        hb[:T].mul_(selb)  # unselected rows: h = 0 (exact)
+        wub = torch.empty(D, rk, device=dev, dtype=BF16)  # B(k, n) = Wu[n][k]: K-contiguous over r
+        ops.cast_pad_rows(wu.detach().float().contiguous(), D, r, wub, rk)
+        out = torch.empty(T, D, device=dev, dtype=F32)
+        ops.gemm(hb, wub, out, T, D, rk, a_layout=K_CONTIG, b_layout=K_CONTIG, lda=rk, ldb=rk, ldc=D,
+                 epilogue=EPI_BIAS_RESID_F32, bias=_zero_row(D, dev), aux=x2, ldaux=D)
+        ctx.save_for_backward(xb, hb, wd, wu, selb)
+        ctx.dims = (B, N, D, T, r)
+        return out.view(B, N, D)
+
+    @staticmethod
+    def backward(ctx, dout):
+        xb, hb, wd, wu, selb = ctx.saved_tensors
+        B, N, D, T, r = ctx.dims
+        kp, rp, rk = xb.shape[1], xb.shape[0], hb.shape[1]
+        dev = dout.device
+        d2 = dout.contiguous().float().view(T, D)
+        db = torch.empty(rp, kp, device=dev, dtype=BF16)
+        ops.cast_pad_rows(d2, T, D, db, kp)
+        if rp > T:
+            ops.zero_(db[T:])
+        # dh = dout Wu: B(kk = n, n' = j) = Wu[n][j], MN-contiguous [D][r8]
+        r8 = _rup(r, 8)
+        wut = torch.zeros(kp, r8, device=dev, dtype=BF16)
+        ops.cast_pad_rows(wu.detach().float().contiguous(), D, r, wut, r8)
+        dh = torch.empty(T, r, device=dev, dtype=F32)
+        ops.gemm(db, wut, dh, T, r, kp, a_layout=K_CONTIG, b_layout=MN_CONTIG, lda=kp, ldb=r8, ldc=r,
+                 epilogue=EPI_F32)
+        dhb = torch.empty(rp, rk, device=dev, dtype=BF16)
+        ops.cast_pad_rows(dh, T, r, dhb, rk)
+        if rp > T:
+            ops.zero_(dhb[T:])
+        dhb[:T].mul_(selb)
+        dx = dwd = dwu = None
+        if ctx.needs_input_grad[0]:
+            # dx = dout + dh Wd: B(kk = j, n' = k) = Wd[j][k], MN-contiguous [r64][D8]
+            d8 = _rup(D, 8)
+            wdt = torch.zeros(rk, d8, device=dev, dtype=BF16)
+            ops.cast_pad_rows(wd.detach().float().contiguous(), r, D, wdt, d8)
+            dx = torch.empty(T, D, device=dev, dtype=F32)
+            ops.gemm(dhb, wdt, dx, T, D, rk, a_layout=K_CONTIG, b_layout=MN_CONTIG, lda=rk, ldb=d8, ldc=D,
+                     epilogue=EPI_BIAS_RESID_F32, bias=_zero_row(D, dev), aux=d2, ldaux=D)
+            dx = dx.view(B, N, D)
+        if ctx.needs_input_grad[2]:  # dWu [D][r] = dout^T h
+            dwu = torch.empty(D, r, device=dev, dtype=F32)
+            ops.wgrad(db, kp, hb, rk, D, r, rp, dwu, r)
+        if ctx.needs_input_grad[1]:  # dWd [r][D] = dh^T x
+            dwd = torch.empty(r, D, device=dev, dtype=F32)
+            ops.wgrad(dhb, rk, xb, kp, r, D, rp, dwd, D)
+        return dx, dwd, dwu, None
+
+
+def approx_supported(m, x):
+    """the fused approximator step covers the LowRankApproximator as built (no bias, f32 weights, CUDA)"""
+    d, u = m.down_proj, m.up_proj
+    return (x.is_cuda and x.dim() == 3 and d.bias is None and u.bias is None and d.weight.dtype == F32
+            and u.weight.dtype == F32 and d.weight.shape[1] == x.shape[2] and u.weight.shape[0] == x.shape[2])
+
+
+def approx_step(m, x, sel):
+    """where(sel, x + m(x), x) (res-vit/model.py:349-368, training) as one fused node"""
+    return _ApproxStep.apply(x, m.down_proj.weight, m.up_proj.weight, sel)
