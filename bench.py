@@ -429,6 +429,10 @@ def bench_resvit(args, world, rank, dev, backend, comm):
         for l in model.layers:
             if hasattr(l, "block_path_approximators"):
                 l.block_path_approximators.fused = False
+    if os.environ.get("VITMI_RESVIT_ROUTER_OPS", "0") != "0":  # A/B: the per-op router MLP
+        for l in model.layers:
+            if hasattr(l, "router"):
+                l.router.fused_mlp = False
     opt = AdamW(model.parameters(), lr=1e-4, weight_decay=0.05, betas=(0.9, 0.999), eps=1e-8, max_grad_norm=1.0)
     sched = get_cosine_schedule_with_warmup(opt, 500, 15000)
     reducer = None

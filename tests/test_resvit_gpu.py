@@ -55,13 +55,16 @@ def replay(m, golden, tag):
             r.gumbel_noise = lambda logits, g=g: g
 
 
-@pytest.mark.parametrize("tag", ["eval", "train"])
-def test_router_matches_reference(golden, tag):
+@pytest.mark.parametrize("tag,fused", [("eval", False), ("train", False), ("eval", True), ("train", True)])
+def test_router_matches_reference(golden, tag, fused):
     """each router on the reference's recorded input: logits within bf16 tolerance, and the same keep
-    decision for every token / layer whose reference logit margin exceeds 5% of the logit scale."""
+    decision for every token / layer whose reference logit margin exceeds 5% of the logit scale. fused:
+    out_conv as one node (vitmi.resvit_fused.router_mlp), its logits read back from the soft routing
+    probabilities against the reference's softmax."""
     m = build(golden)
     m.train(tag == "train")
     for j, r in enumerate(routers(m)):
+        r.fused_mlp = fused
         x = torch.from_numpy(golden[f"{tag}/router{j}_x"]).cuda()
         ref_logits = torch.from_numpy(golden[f"{tag}/router{j}_logits"])
         if tag == "train":
@@ -72,7 +75,12 @@ def test_router_matches_reference(golden, tag):
         with torch.no_grad():
             hard, idx, ent, soft = r(x)
         h.remove()
-        assert rel(seen["logits"], ref_logits) < 1e-2
+        if fused:
+            assert "logits" not in seen  # out_conv's modules did not run
+            ref_soft = torch.softmax(ref_logits.view(soft.shape).double(), -1)
+            assert rel(soft, ref_soft) < 1e-2
+        else:
+            assert rel(seen["logits"], ref_logits) < 1e-2
         ref_hard = torch.from_numpy(golden[f"{tag}/router{j}_hard"])
         z = ref_logits.view(*ref_logits.shape[:2], -1, 2).double()
         if tag == "train":

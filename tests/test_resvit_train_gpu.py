@@ -399,3 +399,35 @@ def test_fused_approximator_matches_per_op_path(B, N, r):
         assert torch.equal(a, b)
     sel = (idx == 0).expand(B, N, D)
     assert torch.equal(res[True][0][~sel], x[~sel])  # unrouted rows pass through unchanged
+
+
+@pytest.mark.parametrize("B,N,hdim,bs", [(3, 197, 64, 1), (2, 17, 512, 2)])
+def test_fused_router_mlp_matches_per_op_path(B, N, hdim, bs):
+    """vitmi.resvit_fused.router_mlp (RouterModule.out_conv as one node: GELU and GELU' written by the GEMM
+    epilogues, GELU' multiplied in the data-gradient epilogues) against the per-op path (res-vit/model.py:
+    150-156): the routing logits, the input gradient and all six parameter gradients. Not bit-identical:
+    GELU' is rounded to bf16 (as in the ViT engine's MLP) and the hidden-bias gradients sum bf16 dU."""
+    from vitmi import resvit
+    torch.manual_seed(9)
+    r = resvit.RouterModule(64, hdim, 1, 1e-5, block_size=bs).cuda()
+    with torch.no_grad():  # a last layer with visible weights (the reference inits it at std 0.01)
+        r.out_conv[-1].weight.normal_(0.0, 0.2)
+    g = torch.Generator(device="cuda").manual_seed(13)
+    x = torch.randn(B, N, 2 * hdim, device="cuda", generator=g)
+    w = torch.randn(B, N, 2 * bs, device="cuda", generator=g)
+    params = list(r.out_conv.parameters())
+    res = {}
+    for fused in (True, False):
+        r.fused_mlp = fused
+        xi = x.clone().requires_grad_(True)
+        for p in params:
+            p.grad = None
+        from vitmi import resvit_fused
+        out = resvit_fused.router_mlp(r.out_conv, xi) if fused else r.out_conv(xi)
+        (out * w).sum().backward()
+        res[fused] = (out.detach(), xi.grad.detach(), [p.grad.detach().clone() for p in params])
+    (o1, dx1, g1), (o0, dx0, g0) = res[True], res[False]
+    assert rel(o1, o0) < 1e-3
+    assert rel(dx1, dx0) < 2e-2
+    for a, b in zip(g1, g0):
+        assert rel(a, b) < 2e-2, (rel(a, b), a.shape)

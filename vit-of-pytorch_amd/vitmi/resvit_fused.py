@@ -333,3 +333,126 @@ def approx_supported(m, x):
 def approx_step(m, x, sel):
     """where(sel, x + m(x), x) (res-vit/model.py:349-368, training) as one fused node"""
     return _ApproxStep.apply(x, m.down_proj.weight, m.up_proj.weight, sel)
+
+
+# ---- router MLP (RouterModule.out_conv, res-vit/model.py:150-156,190) ----------------------------------
+def _pad_bf16(x2, rows_p, cols_p):
+    rows, cols = x2.shape
+    out = torch.empty(rows_p, cols_p, device=x2.device, dtype=BF16)
+    if rows:
+        ops.cast_pad_rows(x2, rows, cols, out, cols_p)
+    if rows_p > rows:
+        ops.zero_(out[rows:])
+    return out
+
+
+def _colsum(x, rows, cols, ld):
+    out = torch.empty(cols, device=x.device, dtype=F32)
+    part = torch.empty(ops.colsum_partial_rows(max(rows, 1)), cols, device=x.device, dtype=F32)
+    ops.colsum(x, rows, cols, ld, part, out)
+    return out
+
+
+class _RouterMLP(torch.autograd.Function):
+    """Linear -> GELU -> Linear -> GELU -> Linear (the router's out_conv) as one node: each hidden layer is one
+    GEMM whose epilogue writes GELU(u) (the next GEMM's bf16 operand) and GELU'(u) (kept for the backward),
+    the way the ViT engine runs fc1; the backward's data gradients multiply GELU' in their epilogue
+    (EPI_MUL_BF16). Replaces, per hidden layer, the f32 GEMM output, the f32 GELU pass and the cast to the
+    next operand (forward) and the f32 GELU backward and its cast (backward). Rounding differs from the
+    per-op path only in GELU' being bf16 (as in the engine's MLP) and the hidden-bias gradients summing
+    the bf16 dU."""
+
+    @staticmethod
+    def forward(ctx, x, w1, b1, w2, b2, w3, b3):
+        lead = x.shape[:-1]
+        K1 = x.shape[-1]
+        x2 = x.contiguous().float().reshape(-1, K1)
+        T = x2.shape[0]
+        H1, H2, O = w1.shape[0], w2.shape[0], w3.shape[0]
+        kp, rp, h1p, h2p = _rup(K1, 64), _rup(max(T, 1), 64), _rup(H1, 64), _rup(H2, 64)
+        dev = x.device
+        xb = _pad_bf16(x2, rp, kp)
+        ws = []
+        for w, n, k in ((w1, H1, kp), (w2, H2, h1p), (w3, O, h2p)):
+            ws.append(_pad_bf16(w.detach().float().contiguous(), n, k))  # B(k, n) = W[n][k]: K-contiguous
+        acts = []
+        a_in, k_in = xb, kp
+        for (w, b, n, npad), wb in zip(((w1, b1, H1, h1p), (w2, b2, H2, h2p)), ws[:2]):
+            g = torch.zeros(rp, npad, device=dev, dtype=BF16)
+            gp = torch.zeros(rp, npad, device=dev, dtype=BF16)
+            if T:
+                ops.gemm(a_in, wb, gp, T, n, k_in, a_layout=K_CONTIG, b_layout=K_CONTIG, lda=k_in, ldb=k_in, ldc=npad,
+                         epilogue=EPI_BIAS_GELU_DGELU, bias=b.detach().float().contiguous(), C2=g, ldc2=npad)
+            acts.append((g, gp))
+            a_in, k_in = g, npad
+        out = torch.empty(T, O, device=dev, dtype=F32)
+        if T:
+            ops.gemm(a_in, ws[2], out, T, O, k_in, a_layout=K_CONTIG, b_layout=K_CONTIG, lda=k_in, ldb=k_in, ldc=O,
+                     epilogue=EPI_BIAS_RESID_F32, bias=b3.detach().float().contiguous(), aux=_zero_row(O, dev), ldaux=0)
+        (g1, gp1), (g2, gp2) = acts
+        ctx.save_for_backward(xb, g1, gp1, g2, gp2, w1, w2, w3)
+        ctx.dims = (lead, T, K1, H1, H2, O)
+        return out.reshape(*lead, O)
+
+    @staticmethod
+    def backward(ctx, dout):
+        xb, g1, gp1, g2, gp2, w1, w2, w3 = ctx.saved_tensors
+        lead, T, K1, H1, H2, O = ctx.dims
+        dev = dout.device
+        rp, kp, h1p, h2p = xb.shape[0], xb.shape[1], g1.shape[1], g2.shape[1]
+        d2 = dout.contiguous().float().reshape(T, O)
+        op = _rup(O, 64)
+        db3 = _colsum(d2, T, O, O)
+        dlb = _pad_bf16(d2, rp, op)
+        dw3 = torch.empty(O, H2, device=dev, dtype=F32)
+        ops.wgrad(dlb, op, g2, h2p, O, H2, rp, dw3, H2)
+        grads = [db3, dw3]
+
+        def dgrad_mul(dyb, w, n_in, n_out, gp, npad_out):
+            # d(prev hidden) = dy W (B(kk = j, n' = k) = W[j][k], MN-contiguous) times GELU'(u), bf16 out
+            k8 = _rup(n_in, 8)
+            wt = _pad_bf16(w.detach().float().contiguous(), dyb.shape[1], k8)
+            du = torch.zeros(rp, npad_out, device=dev, dtype=BF16)
+            if T:
+                ops.gemm(dyb, wt, du, T, n_in, dyb.shape[1], a_layout=K_CONTIG, b_layout=MN_CONTIG, lda=dyb.shape[1],
+                         ldb=k8, ldc=npad_out, epilogue=EPI_MUL_BF16, aux=gp, ldaux=npad_out)
+            return du
+
+        du2 = dgrad_mul(dlb, w3, H2, O, gp2, h2p)
+        db2 = _colsum(du2, T, H2, h2p)
+        dw2 = torch.empty(H2, H1, device=dev, dtype=F32)
+        ops.wgrad(du2, h2p, g1, h1p, H2, H1, rp, dw2, H1)
+        du1 = dgrad_mul(du2, w2, H1, H2, gp1, h1p)
+        db1 = _colsum(du1, T, H1, h1p)
+        dw1 = torch.empty(H1, K1, device=dev, dtype=F32)
+        ops.wgrad(du1, h1p, xb, kp, H1, K1, rp, dw1, K1)
+        dx = None
+        if ctx.needs_input_grad[0]:
+            k8 = _rup(K1, 8)
+            w1t = _pad_bf16(w1.detach().float().contiguous(), h1p, k8)
+            dx = torch.empty(T, K1, device=dev, dtype=F32)
+            if T:
+                ops.gemm(du1, w1t, dx, T, K1, h1p, a_layout=K_CONTIG, b_layout=MN_CONTIG, lda=h1p, ldb=k8, ldc=K1,
+                         epilogue=EPI_F32)
+            dx = dx.reshape(*lead, K1)
+        return dx, dw1, db1, dw2, db2, dw3, db3
+
+
+def router_mlp_supported(seq, x):
+    """out_conv as built by RouterModule: Linear, GELU (exact), Linear, GELU, Linear, biases present"""
+    from .model import GELU as _GELU, Linear as _Linear
+    if not x.is_cuda or len(seq) != 5:
+        return False
+    lins, gelus = (seq[0], seq[2], seq[4]), (seq[1], seq[3])
+    if not all(type(l) is _Linear and l.bias is not None and l.weight.dtype == F32 for l in lins):
+        return False
+    if not all(type(g) is _GELU and g.approximate == "none" for g in gelus):
+        return False
+    return (lins[0].weight.shape[1] == x.shape[-1] and lins[1].weight.shape[1] == lins[0].weight.shape[0]
+            and lins[2].weight.shape[1] == lins[1].weight.shape[0])
+
+
+def router_mlp(seq, x):
+    """seq(x) for RouterModule.out_conv (Linear, GELU, Linear, GELU, Linear) as one fused node"""
+    l1, l2, l3 = seq[0], seq[2], seq[4]
+    return _RouterMLP.apply(x, l1.weight, l1.bias, l2.weight, l2.bias, l3.weight, l3.bias)
