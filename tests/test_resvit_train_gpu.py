@@ -431,3 +431,38 @@ def test_fused_router_mlp_matches_per_op_path(B, N, hdim, bs):
     assert rel(dx1, dx0) < 2e-2
     for a, b in zip(g1, g0):
         assert rel(a, b) < 2e-2, (rel(a, b), a.shape)
+
+
+@pytest.mark.parametrize("B,N,hdim,reserve", [(3, 197, 64, 1), (2, 17, 512, 0)])
+def test_fused_router_net_matches_per_op_path(B, N, hdim, reserve):
+    """vitmi.resvit_fused.router_net (LN -> Linear -> GELU -> token mean -> concatenation -> out_conv as one node,
+    the concatenated operand built in bf16 by the GEMM epilogue and a broadcast) against the per-op router
+    (res-vit/model.py:186-190): soft routing probabilities and the gradients of the input and of every router
+    parameter (the LayerNorm affine included). Tolerance-level against the fp32 per-op path: x_embed and its
+    token mean enter out_conv as bf16 and GELU' is bf16; the bias gradients are signed sums over every token,
+    so their relative error carries the cancellation (out_conv's first bias measured at 4e-2)."""
+    from vitmi import resvit
+    torch.manual_seed(21)
+    r = resvit.RouterModule(64, hdim, reserve, 1e-5, block_size=1).cuda()
+    with torch.no_grad():
+        r.out_conv[-1].weight.normal_(0.0, 0.2)
+        r.in_conv[0].layer_norm.weight.normal_(1.0, 0.1)
+    g = torch.Generator(device="cuda").manual_seed(23)
+    x = torch.randn(B, N, 64, device="cuda", generator=g)
+    w = torch.randn(B, N, 1, 2, device="cuda", generator=g)
+    params = list(r.parameters())
+    res = {}
+    for fused in (True, False):
+        r.fused_mlp = fused
+        xi = x.clone().requires_grad_(True)
+        for p in params:
+            p.grad = None
+        hard, idx, ent, soft = r(xi)
+        (soft * w).sum().backward()
+        res[fused] = [soft.detach(), xi.grad.detach()] + [p.grad.detach().clone() for p in params]
+    names = ["soft", "dx"] + [n for n, _ in r.named_parameters()]
+    tol = {"soft": 1e-3, "dx": 3e-2}
+    for n, a, b in zip(names, res[True], res[False]):
+        e = rel(a, b)
+        print(f"{n}: {e:.2e}")
+        assert e < tol.get(n, 6e-2), (n, e)

@@ -1,10 +1,10 @@
 #!/bin/bash
-# round 4, call 12: fused router MLP (out_conv): Res-ViT GPU tests, then Res-ViT-B/16 bs 128 bench fused vs per-op
-# router MLP (VITMI_RESVIT_ROUTER_OPS=1), same box
+# round 4, call 13: fused router network (in_conv + token mean + concatenation + out_conv): Res-ViT GPU tests, then Res-ViT-B/16 bs 128 bench fused vs per-op
+# router MLP (VITMI_RESVIT_ROUTER_OPS=1: the per-op router network), same box
 set -o pipefail
 export TMPDIR=/tmp
 O=gpurun_out/r04l; mkdir -p $O
-timeout -k 10 600 python -u -m pytest tests/test_resvit_train_gpu.py tests/test_resvit_gpu.py -x -q --timeout 200 --timeout-method thread > $O/tests.log 2>&1
+timeout -k 10 600 python -u -m pytest tests/test_resvit_train_gpu.py tests/test_resvit_gpu.py -x -q -rP --timeout 200 --timeout-method thread > $O/tests.log 2>&1
 rc=$?; tail -2 $O/tests.log; [ $rc -eq 0 ] || exit $rc
 for r in 1 2; do
   timeout -k 10 300 python3 -u bench.py --arch resvit_b16 --steps 20 --warmup 3 --no-cpu-baseline > $O/fused_$r.json 2> $O/fused_$r.err || { tail -3 $O/fused_$r.err; exit 1; }

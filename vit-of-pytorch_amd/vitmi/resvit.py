@@ -217,7 +217,7 @@ class RouterModule(nn.Module):
         for i in range(block_size):
             self.out_conv[-1].bias.data[i * 2] = 0.0      # approximate
             self.out_conv[-1].bias.data[i * 2 + 1] = 5.0  # keep (full transformer layer)
-        self.fused_mlp = True      # out_conv as one fused node (vitmi.resvit_fused.router_mlp)
+        self.fused_mlp = True      # the router network as one fused node (vitmi.resvit_fused.router_net)
         self.gumbel_noise = None   # callable(logits) -> Gumbel noise (tests replay recorded draws)
         self.hard_override = None  # callable(logits) -> one-hot decisions (tests replay recorded decisions)
 
@@ -230,14 +230,18 @@ class RouterModule(nn.Module):
 
     def forward(self, x):
         B, N, _ = x.shape
-        x_embed = self.in_conv(x)
         r = self.reserve_initials
-        global_feat = (x_embed[:, r:, :] if r > 0 else x_embed).mean(dim=1, keepdim=True)
-        fused = torch.cat([x_embed, global_feat.expand(B, N, -1)], dim=-1)
-        if self.fused_mlp and _fused.router_mlp_supported(self.out_conv, fused):
-            logits = _fused.router_mlp(self.out_conv, fused).view(B, N, self.block_size, 2)
+        if self.fused_mlp and _fused.router_net_supported(self, x):
+            # in_conv, the token mean, the concatenation and out_conv as one node (vitmi.resvit_fused)
+            logits = _fused.router_net(self, x).view(B, N, self.block_size, 2)
         else:
-            logits = self.out_conv(fused).view(B, N, self.block_size, 2)
+            x_embed = self.in_conv(x)
+            global_feat = (x_embed[:, r:, :] if r > 0 else x_embed).mean(dim=1, keepdim=True)
+            fused = torch.cat([x_embed, global_feat.expand(B, N, -1)], dim=-1)
+            if self.fused_mlp and _fused.router_mlp_supported(self.out_conv, fused):
+                logits = _fused.router_mlp(self.out_conv, fused).view(B, N, self.block_size, 2)
+            else:
+                logits = self.out_conv(fused).view(B, N, self.block_size, 2)
         soft = F.softmax(logits, dim=-1)
         probs = soft[:, r:]
         entropy = -torch.sum(probs * torch.log(probs + 1e-8)) / (B * (N - r) * self.block_size)

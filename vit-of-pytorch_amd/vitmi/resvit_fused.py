@@ -353,6 +353,76 @@ def _colsum(x, rows, cols, ld):
     return out
 
 
+def _mlp_forward(xb, T, kp, w1, b1, w2, b2, w3, b3):
+    """the router's out_conv on a bf16 operand xb [rp][kp] (T valid rows): hidden layers as one GEMM each whose
+    epilogue writes GELU(u) (the next operand) and GELU'(u) (kept for the backward); returns (logits f32 [T][O],
+    saved activations)"""
+    rp, dev = xb.shape[0], xb.device
+    H1, H2, O = w1.shape[0], w2.shape[0], w3.shape[0]
+    h1p, h2p = _rup(H1, 64), _rup(H2, 64)
+    ws = [_pad_bf16(w.detach().float().contiguous(), n, k) for w, n, k in ((w1, H1, kp), (w2, H2, h1p), (w3, O, h2p))]
+    acts = []
+    a_in, k_in = xb, kp
+    for (b, n, npad), wb in zip(((b1, H1, h1p), (b2, H2, h2p)), ws[:2]):
+        g = torch.zeros(rp, npad, device=dev, dtype=BF16)
+        gp = torch.zeros(rp, npad, device=dev, dtype=BF16)
+        if T:
+            ops.gemm(a_in, wb, gp, T, n, k_in, a_layout=K_CONTIG, b_layout=K_CONTIG, lda=k_in, ldb=k_in, ldc=npad,
+                     epilogue=EPI_BIAS_GELU_DGELU, bias=b.detach().float().contiguous(), C2=g, ldc2=npad)
+        acts += [g, gp]
+        a_in, k_in = g, npad
+    out = torch.empty(T, O, device=dev, dtype=F32)
+    if T:
+        ops.gemm(a_in, ws[2], out, T, O, k_in, a_layout=K_CONTIG, b_layout=K_CONTIG, lda=k_in, ldb=k_in, ldc=O,
+                 epilogue=EPI_BIAS_RESID_F32, bias=b3.detach().float().contiguous(), aux=_zero_row(O, dev), ldaux=0)
+    return out, acts
+
+
+def _dgrad_mul(dyb, w, n_in, T, gp, npad_out):
+    """dU = (dY W) * GELU'(u): B(kk = j, n' = k) = W[j][k], MN-contiguous; bf16 out [rp][npad_out]"""
+    rp, dev = dyb.shape[0], dyb.device
+    k8 = _rup(n_in, 8)
+    wt = _pad_bf16(w.detach().float().contiguous(), dyb.shape[1], k8)
+    du = torch.zeros(rp, npad_out, device=dev, dtype=BF16)
+    if T:
+        ops.gemm(dyb, wt, du, T, n_in, dyb.shape[1], a_layout=K_CONTIG, b_layout=MN_CONTIG, lda=dyb.shape[1], ldb=k8,
+                 ldc=npad_out, epilogue=EPI_MUL_BF16, aux=gp, ldaux=npad_out)
+    return du
+
+
+def _dgrad_f32(dyb, w, n_in, T):
+    """dX = dY W (f32 [T][n_in]) for W [n_out][n_in]"""
+    k8 = _rup(n_in, 8)
+    wt = _pad_bf16(w.detach().float().contiguous(), dyb.shape[1], k8)
+    dx = torch.empty(T, n_in, device=dyb.device, dtype=F32)
+    if T:
+        ops.gemm(dyb, wt, dx, T, n_in, dyb.shape[1], a_layout=K_CONTIG, b_layout=MN_CONTIG, lda=dyb.shape[1], ldb=k8,
+                 ldc=n_in, epilogue=EPI_F32)
+    return dx
+
+
+def _mlp_backward(d2, T, xb, acts, w1, w2, w3, need_dx):
+    """gradients of _mlp_forward: (dX f32 [T][K1] or None, dW1, db1, dW2, db2, dW3, db3)"""
+    g1, gp1, g2, gp2 = acts
+    rp, kp, h1p, h2p = xb.shape[0], xb.shape[1], g1.shape[1], g2.shape[1]
+    H1, H2, O, K1 = w1.shape[0], w2.shape[0], w3.shape[0], w1.shape[1]
+    dev = d2.device
+    db3 = _colsum(d2, T, O, O)
+    dlb = _pad_bf16(d2, rp, _rup(O, 64))
+    dw3 = torch.empty(O, H2, device=dev, dtype=F32)
+    ops.wgrad(dlb, dlb.shape[1], g2, h2p, O, H2, rp, dw3, H2)
+    du2 = _dgrad_mul(dlb, w3, H2, T, gp2, h2p)
+    db2 = _colsum(du2, T, H2, h2p)
+    dw2 = torch.empty(H2, H1, device=dev, dtype=F32)
+    ops.wgrad(du2, h2p, g1, h1p, H2, H1, rp, dw2, H1)
+    du1 = _dgrad_mul(du2, w2, H1, T, gp1, h1p)
+    db1 = _colsum(du1, T, H1, h1p)
+    dw1 = torch.empty(H1, K1, device=dev, dtype=F32)
+    ops.wgrad(du1, h1p, xb, kp, H1, K1, rp, dw1, K1)
+    dx = _dgrad_f32(du1, w1, K1, T) if need_dx else None
+    return dx, dw1, db1, dw2, db2, dw3, db3
+
+
 class _RouterMLP(torch.autograd.Function):
     """Linear -> GELU -> Linear -> GELU -> Linear (the router's out_conv) as one node: each hidden layer is one
     GEMM whose epilogue writes GELU(u) (the next GEMM's bf16 operand) and GELU'(u) (kept for the backward),
@@ -368,74 +438,87 @@ class _RouterMLP(torch.autograd.Function):
         K1 = x.shape[-1]
         x2 = x.contiguous().float().reshape(-1, K1)
         T = x2.shape[0]
-        H1, H2, O = w1.shape[0], w2.shape[0], w3.shape[0]
-        kp, rp, h1p, h2p = _rup(K1, 64), _rup(max(T, 1), 64), _rup(H1, 64), _rup(H2, 64)
-        dev = x.device
-        xb = _pad_bf16(x2, rp, kp)
-        ws = []
-        for w, n, k in ((w1, H1, kp), (w2, H2, h1p), (w3, O, h2p)):
-            ws.append(_pad_bf16(w.detach().float().contiguous(), n, k))  # B(k, n) = W[n][k]: K-contiguous
-        acts = []
-        a_in, k_in = xb, kp
-        for (w, b, n, npad), wb in zip(((w1, b1, H1, h1p), (w2, b2, H2, h2p)), ws[:2]):
-            g = torch.zeros(rp, npad, device=dev, dtype=BF16)
-            gp = torch.zeros(rp, npad, device=dev, dtype=BF16)
-            if T:
-                ops.gemm(a_in, wb, gp, T, n, k_in, a_layout=K_CONTIG, b_layout=K_CONTIG, lda=k_in, ldb=k_in, ldc=npad,
-                         epilogue=EPI_BIAS_GELU_DGELU, bias=b.detach().float().contiguous(), C2=g, ldc2=npad)
-            acts.append((g, gp))
-            a_in, k_in = g, npad
-        out = torch.empty(T, O, device=dev, dtype=F32)
-        if T:
-            ops.gemm(a_in, ws[2], out, T, O, k_in, a_layout=K_CONTIG, b_layout=K_CONTIG, lda=k_in, ldb=k_in, ldc=O,
-                     epilogue=EPI_BIAS_RESID_F32, bias=b3.detach().float().contiguous(), aux=_zero_row(O, dev), ldaux=0)
-        (g1, gp1), (g2, gp2) = acts
-        ctx.save_for_backward(xb, g1, gp1, g2, gp2, w1, w2, w3)
-        ctx.dims = (lead, T, K1, H1, H2, O)
-        return out.reshape(*lead, O)
+        xb = _pad_bf16(x2, _rup(max(T, 1), 64), _rup(K1, 64))
+        out, acts = _mlp_forward(xb, T, xb.shape[1], w1, b1, w2, b2, w3, b3)
+        ctx.save_for_backward(xb, *acts, w1, w2, w3)
+        ctx.dims = (lead, T, K1)
+        return out.reshape(*lead, w3.shape[0])
 
     @staticmethod
     def backward(ctx, dout):
         xb, g1, gp1, g2, gp2, w1, w2, w3 = ctx.saved_tensors
-        lead, T, K1, H1, H2, O = ctx.dims
+        lead, T, K1 = ctx.dims
+        d2 = dout.contiguous().float().reshape(T, w3.shape[0])
+        dx, *grads = _mlp_backward(d2, T, xb, (g1, gp1, g2, gp2), w1, w2, w3, ctx.needs_input_grad[0])
+        return (dx.reshape(*lead, K1) if dx is not None else None, *grads)
+
+
+class _RouterNet(torch.autograd.Function):
+    """the whole router network up to its logits (res-vit/model.py:186-190): x_embed = GELU(Linear(LN(x))),
+    global = mean of x_embed over the non-reserved tokens, logits = out_conv(cat(x_embed, global)). One node:
+    LN writes its bf16 output as the in_conv GEMM's operand, that GEMM's epilogue writes GELU(u) straight into
+    the left half of the out_conv operand [T][2h] (and GELU'(u) aside), the per-image mean (of those bf16
+    values) is broadcast into the right half, and out_conv runs as in _RouterMLP: no f32 x_embed, GELU pass,
+    concatenation or cast. Backward: out_conv's input gradient splits into the x_embed part and the per-image
+    sum of the global part (spread back over the non-reserved tokens), times GELU', then in_conv and the LN
+    backward."""
+
+    @staticmethod
+    def forward(ctx, x, ln_w, ln_b, w0, b0, w1, b1, w2, b2, w3, b3, reserve, eps):
+        B, N, D = x.shape
+        T = B * N
+        Hh, K1 = w0.shape[0], w1.shape[1]
+        dev = x.device
+        rp, dp, h0p = _rup(max(T, 1), 64), _rup(D, 64), _rup(Hh, 64)
+        kp = _rup(K1, 64)
+        x2 = x.contiguous().float().view(T, D)
+        lnb = torch.zeros(rp, dp, device=dev, dtype=BF16)
+        mean = torch.empty(T, device=dev, dtype=F32)
+        rstd = torch.empty(T, device=dev, dtype=F32)
+        if T:
+            ops.layernorm_fwd(x2, D, ln_w.detach().float().contiguous(), ln_b.detach().float().contiguous(), lnb, dp,
+                              mean, rstd, T, D, eps)
+        w0b = _pad_bf16(w0.detach().float().contiguous(), Hh, dp)
+        xcat = torch.zeros(rp, kp, device=dev, dtype=BF16)  # [x_embed | global] operand of out_conv
+        gp0 = torch.zeros(rp, h0p, device=dev, dtype=BF16)
+        if T:
+            ops.gemm(lnb, w0b, gp0, T, Hh, dp, a_layout=K_CONTIG, b_layout=K_CONTIG, lda=dp, ldb=dp, ldc=h0p,
+                     epilogue=EPI_BIAS_GELU_DGELU, bias=b0.detach().float().contiguous(), C2=xcat, ldc2=kp)
+        xc = xcat[:T].view(B, N, kp)
+        glob = xc[:, reserve:, :Hh].float().mean(dim=1)  # [B][h] (mean of the bf16 x_embed values)
+        xc[:, :, Hh:K1].copy_(glob.to(BF16)[:, None, :])
+        out, acts = _mlp_forward(xcat, T, kp, w1, b1, w2, b2, w3, b3)
+        ctx.save_for_backward(x2, mean, rstd, ln_w, lnb, gp0, xcat, *acts, w0, w1, w2, w3)
+        ctx.dims = (B, N, D, T, Hh, K1, reserve)
+        return out.view(B, N, w3.shape[0])
+
+    @staticmethod
+    def backward(ctx, dout):
+        x2, mean, rstd, ln_w, lnb, gp0, xcat, g1, gp1, g2, gp2, w0, w1, w2, w3 = ctx.saved_tensors
+        B, N, D, T, Hh, K1, reserve = ctx.dims
         dev = dout.device
-        rp, kp, h1p, h2p = xb.shape[0], xb.shape[1], g1.shape[1], g2.shape[1]
-        d2 = dout.contiguous().float().reshape(T, O)
-        op = _rup(O, 64)
-        db3 = _colsum(d2, T, O, O)
-        dlb = _pad_bf16(d2, rp, op)
-        dw3 = torch.empty(O, H2, device=dev, dtype=F32)
-        ops.wgrad(dlb, op, g2, h2p, O, H2, rp, dw3, H2)
-        grads = [db3, dw3]
-
-        def dgrad_mul(dyb, w, n_in, n_out, gp, npad_out):
-            # d(prev hidden) = dy W (B(kk = j, n' = k) = W[j][k], MN-contiguous) times GELU'(u), bf16 out
-            k8 = _rup(n_in, 8)
-            wt = _pad_bf16(w.detach().float().contiguous(), dyb.shape[1], k8)
-            du = torch.zeros(rp, npad_out, device=dev, dtype=BF16)
-            if T:
-                ops.gemm(dyb, wt, du, T, n_in, dyb.shape[1], a_layout=K_CONTIG, b_layout=MN_CONTIG, lda=dyb.shape[1],
-                         ldb=k8, ldc=npad_out, epilogue=EPI_MUL_BF16, aux=gp, ldaux=npad_out)
-            return du
-
-        du2 = dgrad_mul(dlb, w3, H2, O, gp2, h2p)
-        db2 = _colsum(du2, T, H2, h2p)
-        dw2 = torch.empty(H2, H1, device=dev, dtype=F32)
-        ops.wgrad(du2, h2p, g1, h1p, H2, H1, rp, dw2, H1)
-        du1 = dgrad_mul(du2, w2, H1, H2, gp1, h1p)
-        db1 = _colsum(du1, T, H1, h1p)
-        dw1 = torch.empty(H1, K1, device=dev, dtype=F32)
-        ops.wgrad(du1, h1p, xb, kp, H1, K1, rp, dw1, K1)
-        dx = None
-        if ctx.needs_input_grad[0]:
-            k8 = _rup(K1, 8)
-            w1t = _pad_bf16(w1.detach().float().contiguous(), h1p, k8)
-            dx = torch.empty(T, K1, device=dev, dtype=F32)
-            if T:
-                ops.gemm(du1, w1t, dx, T, K1, h1p, a_layout=K_CONTIG, b_layout=MN_CONTIG, lda=h1p, ldb=k8, ldc=K1,
-                         epilogue=EPI_F32)
-            dx = dx.reshape(*lead, K1)
-        return dx, dw1, db1, dw2, db2, dw3, db3
+        rp, dp, h0p = xcat.shape[0], lnb.shape[1], gp0.shape[1]
+        d2 = dout.contiguous().float().view(T, w3.shape[0])
+        dcat, *mlp_grads = _mlp_backward(d2, T, xcat, (g1, gp1, g2, gp2), w1, w2, w3, True)
+        dc = dcat.view(B, N, K1)
+        dxe = dc[:, :, :Hh].clone()
+        dxe[:, reserve:, :] += (dc[:, :, Hh:].sum(dim=1) / (N - reserve))[:, None, :]
+        du0 = dxe.view(T, Hh) * gp0[:T, :Hh].float()
+        du0b = _pad_bf16(du0, rp, h0p)
+        db0 = _colsum(du0b, T, Hh, h0p)
+        dw0 = torch.empty(Hh, D, device=dev, dtype=F32)
+        ops.wgrad(du0b, h0p, lnb, dp, Hh, D, rp, dw0, D)
+        dln = _dgrad_f32(du0b, w0, D, T)
+        dx = torch.empty(T, D, device=dev, dtype=F32)
+        need_ln = ctx.needs_input_grad[1] or ctx.needs_input_grad[2]
+        gb = torch.zeros(2 * D, device=dev, dtype=F32) if need_ln else None
+        if T:
+            part = torch.empty(ops.layernorm_bwd_partial_rows(T), 3 * D, device=dev, dtype=F32)
+            ops.layernorm_bwd(dln, D, x2, D, mean, rstd, ln_w.detach().float().contiguous(), dx, D, part, T, D,
+                              dgamma_dbeta=gb)
+        dg = gb[:D].clone() if need_ln else None
+        dbt = gb[D:].clone() if need_ln else None
+        return (dx.view(B, N, D), dg, dbt, dw0, db0, *mlp_grads, None, None)
 
 
 def router_mlp_supported(seq, x):
@@ -456,3 +539,29 @@ def router_mlp(seq, x):
     """seq(x) for RouterModule.out_conv (Linear, GELU, Linear, GELU, Linear) as one fused node"""
     l1, l2, l3 = seq[0], seq[2], seq[4]
     return _RouterMLP.apply(x, l1.weight, l1.bias, l2.weight, l2.bias, l3.weight, l3.bias)
+
+
+def router_net_supported(router, x):
+    """RouterModule as built: in_conv = (LayerNorm, Linear, GELU exact), out_conv as router_mlp_supported, at least
+    one non-reserved token"""
+    from .model import GELU as _GELU, Linear as _Linear
+    ic = router.in_conv
+    if len(ic) != 3 or not (x.is_cuda and x.dim() == 3 and x.shape[1] > router.reserve_initials):
+        return False
+    ln = getattr(ic[0], "layer_norm", None)
+    if ln is None or ln.weight is None or tuple(ln.normalized_shape) != (x.shape[-1],):
+        return False
+    if not (type(ic[1]) is _Linear and ic[1].bias is not None and type(ic[2]) is _GELU and ic[2].approximate == "none"):
+        return False
+    if ic[1].weight.shape[1] != x.shape[-1]:
+        return False
+    probe = torch.empty(0, 0, 2 * ic[1].weight.shape[0], device=x.device)
+    return router_mlp_supported(router.out_conv, probe)
+
+
+def router_net(router, x):
+    """RouterModule's logits (in_conv, mean, cat, out_conv) as one fused node"""
+    ln, l0 = router.in_conv[0].layer_norm, router.in_conv[1]
+    l1, l2, l3 = router.out_conv[0], router.out_conv[2], router.out_conv[4]
+    return _RouterNet.apply(x, ln.weight, ln.bias, l0.weight, l0.bias, l1.weight, l1.bias, l2.weight, l2.bias,
+                            l3.weight, l3.bias, int(router.reserve_initials), float(ln.eps))
