@@ -221,6 +221,8 @@ def main():
                               num_classes=args.num_classes, attn_dropout_rate=0.0, dropout_rate=0.0).to(dev)
     eng = model.engine()
     eng.refresh_mirror()
+    if os.environ.get("VITMI_ATTN_FWD_PATH"):  # A/B: 3 = the one-shot attention forward instead of the persistent one
+        eng.attn_fwd_path = int(os.environ["VITMI_ATTN_FWD_PATH"])
     cfg = eng.cfg
     b = args.batch
     g = torch.Generator(device=dev).manual_seed(1000 + rank)

@@ -168,7 +168,9 @@ int vit_layernorm_bwd(const void* dy, int64_t lddy, int32_t dy_f32, const float*
  * Two implementations (`path`): 1 = LDS-resident (all keys of a head on chip, exact softmax;
  * N <= 320: 197 tokens for B/16 and L/16 @224, 257 for H/14 @224), 2 = K/V-tiled (64-key blocks
  * streamed through LDS, online softmax; any N: 577 tokens @384 for B/16 and L/16, 730 for H/14,
- * src/config.py:12,37), 0 = pick by N. hd: multiple of 16, <= 96 (hd 80 runs on 96-wide images).
+ * src/config.py:12,37), 0 = pick by N, 3 = path 1 in its one-workgroup-per-(image, head) kernels only (no
+ * persistent forward / backward: same-box A/B and parity checks; 1 bias row per image). hd: multiple of 16,
+ * <= 96 (80-wide LDS images for ViT-H/14's hd 80).
  * ---------------------------------------------------------------------------------------- */
 int vit_attention_fwd(const void* qkv, void* o, float* lse, int64_t B, int64_t N, int64_t H,
                       int64_t hd, float scale, vit_stream_t stream);

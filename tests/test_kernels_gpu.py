@@ -257,6 +257,36 @@ def test_attention(B, N, H, hd, path):
     assert rel(mv, gv) < 2e-2
 
 
+@pytest.mark.parametrize("B,N,H,hd", [(2, 197, 12, 64), (24, 197, 12, 64), (3, 17, 2, 32), (1, 5, 3, 64), (2, 2, 2, 64),
+                                       (23, 50, 12, 64), (2, 208, 3, 64), (1, 197, 2, 48), (7, 300, 4, 32),
+                                       (2, 320, 2, 32), (40, 33, 8, 64)])
+@pytest.mark.parametrize("q_rows", [None, 1])
+def test_attention_persistent_forward_matches_oneshot(B, N, H, hd, q_rows):
+    """the persistent forward (attention_fwd_pers.hip: K / V / Q of the next (image, head) by LDS-DMA while the
+    current one runs) does attn_fwd2_kernel's arithmetic per strip: o and lse bit-identical to the
+    one-workgroup-per-item kernel (ops.ATTN_ONESHOT) and run to run, also past 256 items (several per
+    workgroup), for odd tile counts, hd 48 on 64-wide images, and the cls-only query pair (q_rows = 1). (Run
+    to run is what caught the row max once read from MFMA registers by an inline-asm v_max3 too early:
+    attn_common.h max3f.)"""
+    D = H * hd
+    g = torch.Generator(device=DEV).manual_seed(B * 1000 + N)
+    qkv = (torch.randn(B * N, 3 * D, device=DEV, generator=g) * 1.5).bfloat16()
+    outs = []
+    for path in (ops.ATTN_AUTO, ops.ATTN_ONESHOT, ops.ATTN_AUTO):
+        o = torch.full((B * N, D), float("nan"), device=DEV, dtype=torch.bfloat16)
+        lse = torch.full((B, H, N), float("nan"), device=DEV)
+        ops.attention_fwd(qkv, o, lse, B, N, H, hd, 1.0 / math.sqrt(hd), q_rows=q_rows, path=path)
+        outs.append((o, lse))
+    (o1, l1), (o0, l0), (o2, l2) = outs
+    rows = N if q_rows is None else min(N, 32)
+    for o, lse in ((o0, l0), (o2, l2)):
+        assert torch.equal(o1.view(B, N, D)[:, :rows], o.view(B, N, D)[:, :rows])
+        assert torch.equal(l1[:, :, :rows], lse[:, :, :rows])
+    if q_rows is None:
+        oref, lref = _attn_ref(qkv, B, N, H, hd)
+        assert rel(o1.float(), oref) < 1e-2 and rel(l1, lref) < 1e-4
+
+
 @pytest.mark.parametrize("N,B,hd", [(2, 2, 64), (17, 2, 64), (197, 2, 64), (2, 32, 64), (257, 2, 80), (5, 2, 80)])
 def test_attention_backward_saturated_scores_finite(N, B, hd):
     """scores of |s| ~ 1e3 (the reference's std-1 init, config C1's 2 tokens): the LSE of a query can be far

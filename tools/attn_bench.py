@@ -2,7 +2,7 @@
 """Micro-benchmark of the fused attention kernels (HIP events, warm L2 excluded by size).
 
     python tools/attn_bench.py [B N H hd path] ...      default: ViT-B/16 bs256 (256 197 12 64 0)
-path: 0 auto, 1 LDS-resident, 2 K/V-tiled. Algorithmic FLOPs: 4 B H N^2 hd forward, 2.5x that backward
+path: 0 auto, 1 LDS-resident, 2 K/V-tiled, 3 LDS-resident one-shot (no persistent kernels). Algorithmic FLOPs: 4 B H N^2 hd forward, 2.5x that backward
 (5 products); bytes: q|k|v read + o written forward, q|k|v + dO read + dq|dk|dv written backward.
 """
 import os

@@ -855,9 +855,12 @@ int image_width(int64_t hd) { return hd <= 32 ? 32 : hd <= 64 ? 64 : hd == 80 ? 
 
 constexpr int64_t RESIDENT_MAX_N = 320;  // all keys of a head in LDS (attn_fwd_kernel / attn_bwd_kernel)
 
-// 1: LDS-resident kernels, 2: K/V-tiled kernels (attention_tiled.hip); 0 picks by N
+// 1: LDS-resident kernels, 2: K/V-tiled kernels (attention_tiled.hip); 0 picks by N; 3: the LDS-resident
+// kernels in their one-workgroup-per-item forms only (no persistent forward / backward; A/B and parity checks)
+constexpr int32_t PATH_ONESHOT = 3;
 int resolve_path(int32_t path, int64_t N) {
   if (path == 1 || path == 2) return path;
+  if (path == PATH_ONESHOT) return 1;
   return N <= RESIDENT_MAX_N ? 1 : 2;
 }
 
@@ -871,11 +874,14 @@ size_t vit_attn_bwd_pers_lds(int N, int hd);
 int vit_attn_bwd_pers_bias_rows();
 hipError_t vit_attn_bwd_pers(const void* qkv, const void* dout, const float* lse, void* dqkv, float* bias_partial,
                              int B, int N, int H, int hd, float scale, int nq, hipStream_t s);
+bool vit_attn_fwd_pers_ok(int N, int hd);
+hipError_t vit_attn_fwd_pers(const void* qkv, void* o, float* lse, int B, int N, int H, int hd, float scale, int nq,
+                             hipStream_t s);
 
 extern "C" int64_t vit_attention_bias_rows(int64_t N, int64_t hd, int32_t path) {
   if (resolve_path(path, N) == 2) return (N + 63) / 64;  // one per 64-row block
   // persistent kernel: one per wave; two-stage kernel: one per image
-  return vit_attn_bwd_pers_lds((int)N, (int)hd) > 0 ? vit_attn_bwd_pers_bias_rows() : 1;
+  return path != PATH_ONESHOT && vit_attn_bwd_pers_lds((int)N, (int)hd) > 0 ? vit_attn_bwd_pers_bias_rows() : 1;
 }
 
 extern "C" int64_t vit_attention_workspace_elems(int64_t B, int64_t N, int64_t H, int32_t path) {
@@ -889,7 +895,7 @@ extern "C" int vit_attention_fwd_ex(const void* qkv, void* o, float* lse, int64_
   if (st) return st;
   VIT_CHECK_ARG(qkv && o && lse, "vit_attention_fwd: null pointer");
   VIT_CHECK_ARG(q_rows >= 1 && q_rows <= N, "vit_attention_fwd: q_rows=%lld outside [1, N]", (long long)q_rows);
-  VIT_CHECK_ARG(path >= 0 && path <= 2, "vit_attention_fwd: path %d", (int)path);
+  VIT_CHECK_ARG(path >= 0 && path <= 3, "vit_attention_fwd: path %d", (int)path);
   const int p = resolve_path(path, N);
   VIT_CHECK_ARG(p == 2 || N <= RESIDENT_MAX_N, "vit_attention_fwd: N=%lld > %lld on the LDS-resident path",
                 (long long)N, (long long)RESIDENT_MAX_N);
@@ -900,6 +906,10 @@ extern "C" int vit_attention_fwd_ex(const void* qkv, void* o, float* lse, int64_
   if (p == 2) {
     e = vit_attn_tiled_fwd(qkv, o, lse, (int)B, (int)N, (int)H, (int)hd, scale, nq, s);
     return vit::check_hip(e, "vit_attention_fwd (tiled) launch");
+  }
+  if (path != PATH_ONESHOT && vit_attn_fwd_pers_ok((int)N, (int)hd)) {  // persistent kernel (attention_fwd_pers.hip)
+    e = vit_attn_fwd_pers(qkv, o, lse, (int)B, (int)N, (int)H, (int)hd, scale, nq, s);
+    return vit::check_hip(e, "vit_attention_fwd (persistent) launch");
   }
   const int nkt = (int)((N + 31) / 32) * 2;
   switch (image_width(hd)) {
@@ -928,7 +938,7 @@ extern "C" int vit_attention_bwd_ex(const void* qkv, const void* o, const void* 
   if (st) return st;
   VIT_CHECK_ARG(qkv && o && dout && lse && dqkv, "vit_attention_bwd: null pointer");
   VIT_CHECK_ARG(q_rows >= 1 && q_rows <= N, "vit_attention_bwd: q_rows=%lld outside [1, N]", (long long)q_rows);
-  VIT_CHECK_ARG(path >= 0 && path <= 2, "vit_attention_bwd: path %d", (int)path);
+  VIT_CHECK_ARG(path >= 0 && path <= 3, "vit_attention_bwd: path %d", (int)path);
   const int p = resolve_path(path, N);
   VIT_CHECK_ARG(p == 2 || N <= RESIDENT_MAX_N, "vit_attention_bwd: N=%lld > %lld on the LDS-resident path",
                 (long long)N, (long long)RESIDENT_MAX_N);
@@ -942,7 +952,7 @@ extern "C" int vit_attention_bwd_ex(const void* qkv, const void* o, const void* 
                            s);
     return vit::check_hip(e, "vit_attention_bwd (tiled) launch");
   }
-  if (vit_attn_bwd_pers_lds((int)N, (int)hd) > 0) {  // persistent single-load kernel (attention_bwd.hip)
+  if (path != PATH_ONESHOT && vit_attn_bwd_pers_lds((int)N, (int)hd) > 0) {  // persistent kernel (attention_bwd.hip)
     e = vit_attn_bwd_pers(qkv, dout, lse, dqkv, bias_partial, (int)B, (int)N, (int)H, (int)hd, scale, nq, s);
     return vit::check_hip(e, "vit_attention_bwd (persistent) launch");
   }

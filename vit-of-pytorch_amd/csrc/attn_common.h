@@ -261,12 +261,13 @@ __device__ __forceinline__ float nan_of(float x) {
   asm("v_sub_f32 %0, %1, %1" : "=v"(r) : "v"(x));
   return r;
 }
-// max(a, b, c) in one v_max3_f32 (hipcc splits fmaxf chains into v_max_f32 pairs)
-__device__ __forceinline__ float max3f(float a, float b, float c) {
-  float r;
-  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
-  return r;
-}
+// max(a, b, c): plain fmaxf, which hipcc folds into v_max3_f32 under -mno-amdgpu-ieee -fno-honor-nans (the
+// attention objects' flags). Not inline asm: the operands are MFMA results, and hipcc's hazard recognizer
+// does not pad an asm statement that reads an MFMA's destination registers with the wait states the
+// MFMA -> VALU read needs, so an asm v_max3_f32 placed a few instructions after the MFMA read the
+// register's previous contents (a partial score): a wrong row max, which the shift-invariant softmax
+// turned into last-bit differences between runs (and which could overflow exp2 for a large gap).
+__device__ __forceinline__ float max3f(float a, float b, float c) { return fmaxf(fmaxf(a, b), c); }
 __device__ __forceinline__ v4s pack4(const v4f& a) {
   v4s r;
   r[0] = (short)f2bf(a[0]); r[1] = (short)f2bf(a[1]); r[2] = (short)f2bf(a[2]); r[3] = (short)f2bf(a[3]);

@@ -253,6 +253,8 @@ class ViTEngine:
             raise NotImplementedError("emb_dim and mlp_dim must be multiples of 64")
         self.cfg = cfg
         self.dev = torch.device(device)
+        # attention forward kernel choice (ops.ATTN_AUTO; ops.ATTN_ONESHOT for same-box A/B of the persistent kernel)
+        self.attn_fwd_path = ops.ATTN_AUTO
         self.layout = FlatLayout(cfg)
         n = self.layout.numel
         self.flat = flat if flat is not None else torch.zeros(n, device=self.dev)
@@ -451,7 +453,8 @@ class ViTEngine:
             ops.gemm(a.ln1[i], self.wqkvt[i], a.qkv[i], T, 3 * D, D, a_layout=K_CONTIG, b_layout=K_CONTIG, lda=D,
                      ldb=D, ldc=3 * D, epilogue=EPI_BIAS_BF16, bias=self.bqkv[i])
             last = self._pruned and i == L - 1
-            ops.attention_fwd(a.qkv[i], a.o[i], a.lse[i], b, N, H, hd, scale, q_rows=1 if last else None)
+            ops.attention_fwd(a.qkv[i], a.o[i], a.lse[i], b, N, H, hd, scale, q_rows=1 if last else None,
+                              path=self.attn_fwd_path)
             if last:
                 self._forward_last_cls(a, i, b)
                 break

@@ -117,7 +117,9 @@ def layernorm_bwd(dy, lddy, x, ldx, mean, rstd, gamma, dx, lddx, partial, rows, 
           "vit_layernorm_bwd")
 
 
-ATTN_AUTO, ATTN_RESIDENT, ATTN_TILED = 0, 1, 2
+# ATTN_ONESHOT: the LDS-resident kernels in their one-workgroup-per-(image, head) forms only (no persistent
+# forward / backward); for A/B timing and the persistent kernels' parity tests
+ATTN_AUTO, ATTN_RESIDENT, ATTN_TILED, ATTN_ONESHOT = 0, 1, 2, 3
 
 
 def attention_bias_rows(N, hd, path=ATTN_AUTO):
