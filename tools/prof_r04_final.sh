@@ -2,7 +2,7 @@
 # Round-4 end-of-round evidence for profiles/r04/: the full GPU test suite, smoke(), the default bench line (with
 # the CPU baseline), its kernel trace + step timeline, and separate --pmc passes (FETCH_SIZE; WRITE_SIZE; MFMA
 # busy) for the roofline kernels (split-K weight gradient, fc1 forward) and the attention backward.
-# usage: bash tools/prof_r04_final.sh TAG [skip-tests]
+# usage: bash tools/prof_r04_final.sh TAG [skip-tests|tests] [graph]
 set -o pipefail
 export TMPDIR=/tmp
 TAG=${1:-v1}
@@ -41,6 +41,7 @@ head -30 $O/kernel_summary.txt; head -4 $O/step_timeline.txt
 python3 -c "import json;[print(k, round(json.load(open('$O/'+k))['traffic_bytes']/1e6,1),'MB') for k in ['wgrad_traffic.json','fc1_traffic.json','attn_bwd_traffic.json']]"
 head -30 $O/kernel_pmc.txt
 # same-box A/B: the whole B/16 step replayed from one HIP graph (VITMI_BENCH_GRAPH=1) vs eager launches
+[ "$3" == "graph" ] || exit 0
 for r in 1 2; do
   for gr in 0 1; do
     VITMI_BENCH_GRAPH=$gr timeout -k 10 300 python3 -u bench.py --steps 20 --warmup 5 --no-cpu-baseline > $O/b16_graph${gr}_$r.json 2> $O/b16_graph${gr}_$r.err || { tail -5 $O/b16_graph${gr}_$r.err; exit 1; }
