@@ -29,11 +29,6 @@ using namespace vit_attn;
 template <int NKT>
 constexpr int fp_nw = NKT <= 16 ? 16 : 8;
 
-template <int N_>
-__device__ __forceinline__ void wait_vm_le() {
-  __builtin_amdgcn_s_waitcnt(0x0F70 | N_);  // vmcnt(N_) (N_ < 16), lgkmcnt / expcnt untouched
-}
-
 template <int HD, int NKT>
 __global__ void __launch_bounds__(fp_nw<NKT> * 64, 1) attn_fwd_pers_kernel(const bf16_t* __restrict__ qkv,
                                                                      bf16_t* __restrict__ o, float* __restrict__ lse,
@@ -47,7 +42,7 @@ __global__ void __launch_bounds__(fp_nw<NKT> * 64, 1) attn_fwd_pers_kernel(const
   constexpr int ND = HD / 16;
   constexpr int MAXS = (NKT + NW - 1) / NW;  // strips per wave and item
   constexpr int SPS = ND + 1;                // store instructions per strip: ND O pieces + the lse row
-  static_assert(MAXS <= 3 && MAXS * SPS < 16, "vmcnt immediate");
+  static_assert(MAXS <= 3, "store counts");
   __shared__ __attribute__((aligned(16))) char s0[3 * IMG];  // K | V | Q, slot 0
   __shared__ __attribute__((aligned(16))) char s1[3 * IMG];  // slot 1
 
@@ -88,10 +83,10 @@ __global__ void __launch_bounds__(fp_nw<NKT> * 64, 1) attn_fwd_pers_kernel(const
     // this item's images landed (each wave drains its own DMAs, then the barrier), and every wave is past
     // the previous item (the last reader of the other slot)
     switch (nst / SPS) {
-      case 0: wait_vm_le<0>(); break;
-      case 1: wait_vm_le<SPS>(); break;
-      case 2: wait_vm_le<(2 * SPS < 16 ? 2 * SPS : 15)>(); break;
-      default: wait_vm_le<(3 * SPS < 16 ? 3 * SPS : 15)>(); break;
+      case 0: wait_vmcnt<0>(); break;
+      case 1: wait_vmcnt<SPS>(); break;
+      case 2: wait_vmcnt<2 * SPS>(); break;
+      default: wait_vmcnt<3 * SPS>(); break;
     }
     lds_barrier();
     if (next < nitems) dma_item(Kn, next);

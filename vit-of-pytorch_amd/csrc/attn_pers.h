@@ -24,6 +24,15 @@ __device__ __forceinline__ void lds_barrier() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
+// s_waitcnt vmcnt(N) (0 <= N <= 63; lgkmcnt / expcnt left alone). vmcnt retires a wave's vector memory
+// operations in issue order, so with N = the number of stores issued after a wave's last LDS-DMA the wait
+// covers that DMA and never the stores' own round trip.
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt is 6 bits");
+  __builtin_amdgcn_s_waitcnt(0x0F70 | (N & 15) | ((N >> 4) << 14));
+}
+
 // the lane index, recomputed where it is used (opaque to CSE): lane-derived offsets of a later phase are
 // rebuilt from it instead of being kept live (and spilled) across the register-heavy stage before it
 __device__ __forceinline__ int lane_now() {
