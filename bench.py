@@ -427,6 +427,9 @@ def bench_resvit(args, world, rank, dev, backend, comm):
              patch_size=(16, 16), num_classes=100, device="cuda")
     torch.manual_seed(42)
     model = resvit.Transformer(resvit.ModelArgs(**a)).to(dev).train()
+    if os.environ.get("VITMI_RESVIT_PACK_EACH", "0") != "0":  # A/B: LoRA operands packed on every layer call
+        from vitmi import resvit_fused
+        resvit_fused.SHARE_PACK = False
     if os.environ.get("VITMI_RESVIT_APPROX_OPS", "0") != "0":  # A/B: the per-op approximator path
         for l in model.layers:
             if hasattr(l, "block_path_approximators"):

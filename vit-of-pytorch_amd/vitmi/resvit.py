@@ -427,9 +427,9 @@ class TransformerBlock(nn.Module):
                                            args.norm_eps, block_size=self.block_size, use_lora=args.use_lora)
                 self.block_path_approximators = BlockPathApproximators(args.dim, args.low_rank_dim, self.block_size)
 
-    def _full(self, x):
+    def _full(self, x, packed=False):
         if self.fused and x.dim() == 3 and x.is_cuda and _fused.supported(self):
-            return _fused.full_layer(self, x)  # one fused node (LoRA configuration, vitmi.resvit_fused)
+            return _fused.full_layer(self, x, packed)  # one fused node (LoRA configuration, vitmi.resvit_fused)
         h = HF.add(self.attention(self.attention_norm(x)), x)
         return HF.add(self.feed_forward(self.ffn_norm(h)), h)
 
@@ -464,7 +464,8 @@ class TransformerBlock(nn.Module):
             # .detach() (res-vit/model.py:40-59), so no gradient flows through it: run without autograd
             with torch.no_grad():
                 teacher_out = self._full(x if teacher_x is None else teacher_x)
-            student_out = _select_rows(active, self._full(x), x)
+            # same block, same LoRA weights: the teacher pass's operand pack serves the student pass
+            student_out = _select_rows(active, self._full(x, packed=True), x)
             return teacher_out, approximators(student_out, router_indices, lra_lora), w, block_info
 
         # inference: only the active tokens query (ragged), every token is a key / value

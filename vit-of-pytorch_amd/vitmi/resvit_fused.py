@@ -70,11 +70,43 @@ def supported(block):
     return D % 64 == 0 and M % 64 == 0 and hd % 16 == 0 and hd <= 96 and 3 * _rup(r, 8) <= KX
 
 
+# A/B switch (bench.py VITMI_RESVIT_PACK_EACH=1): False packs the LoRA factors and clears the q|k|v operand on
+# every call, as before round 4's shared pack
+SHARE_PACK = True
+
+
 class _Frozen:
-    """bf16 operand copies of a block's frozen weights, rebuilt when a weight's storage or version changes"""
+    """bf16 operand copies of a block's frozen weights, rebuilt when a weight's storage or version changes; the
+    LoRA operand pack (A_all, the B columns of the q|k|v operand) and a persistent [Tp][D + 64] LN1 | u operand
+    whose padding (columns past D + 3 r8, rows past T) is cleared once"""
 
     def __init__(self):
         self.sig = None
+        self.a_all = None
+        self.a1 = None
+        self.a1_rows = 0
+
+    def pack_lora(self, aq, bq, ak, bk, av, bv):
+        """A_all [64][D] (row z*r8 + i = A_z[i], other rows zero) and B_z into columns D + z*r8 of wcat"""
+        r, D = aq.shape
+        r8 = _rup(r, 8)
+        Kq = D + KX
+        if self.a_all is None or self.a_all.shape != (KX, D) or self.a_all.device != aq.device:
+            self.a_all = torch.zeros(KX, D, device=aq.device, dtype=BF16)
+        for z, A in enumerate((aq, ak, av)):
+            ops.cast_pad_rows(A.detach().float().contiguous(), r, D, self.a_all[z * r8:], D)
+        for z, Bz in enumerate((bq, bk, bv)):
+            ops.pack_cols(Bz.detach().float().contiguous(), 0, r, D, r, 1, self.wcat[z * D:, D + z * r8:], Kq)
+        return self.a_all
+
+    def operand(self, T, Tp, Kq, dev):
+        if self.a1 is None or self.a1.shape != (Tp, Kq) or self.a1.device != dev:
+            self.a1 = torch.empty(Tp, Kq, device=dev, dtype=BF16)
+            ops.zero_(self.a1)
+        elif T != self.a1_rows and Tp > T:
+            ops.zero_(self.a1[T:])  # rows past T (read by the split-K LoRA gradients) back to zero
+        self.a1_rows = T
+        return self.a1
 
     def get(self, block):
         a, ff = block.attention, block.feed_forward
@@ -86,6 +118,7 @@ class _Frozen:
         D, M = block.dim, ff.fc1.weight.shape[0]
         dev = a.wq.weight.device
         Kq = D + KX
+        self.a_all = None  # a new wcat holds no LoRA columns yet: the next call packs
         # q|k|v forward operand [3D][D + 64] (K-contiguous); the LoRA columns are rewritten per call
         self.wcat = torch.zeros(3 * D, Kq, device=dev, dtype=BF16)
         for z, w in enumerate((a.wq.weight, a.wk.weight, a.wv.weight)):
@@ -113,7 +146,7 @@ class _Frozen:
 
 class _FusedLayer(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, aq, bq, ak, bk, av, bv, block):
+    def forward(ctx, x, aq, bq, ak, bk, av, bv, block, packed):
         a, ff = block.attention, block.feed_forward
         fz = block._vitmi_frozen.get(block)
         B, N, D = x.shape
@@ -129,14 +162,16 @@ class _FusedLayer(torch.autograd.Function):
         xf = x.view(T, D)
         eps1, eps2 = block.attention_norm.layer_norm.eps, block.ffn_norm.layer_norm.eps
         n1, n2 = block.attention_norm.layer_norm, block.ffn_norm.layer_norm
-        # LoRA factors as bf16 operands: A_all [64][D] (row z*r8 + i = A_z[i]); B columns of the q|k|v operand
-        a_all = torch.zeros(KX, D, device=dev, dtype=BF16)
-        for z, A in enumerate((aq, ak, av)):
-            ops.cast_pad_rows(A.detach().float().contiguous(), r, D, a_all[z * r8:], D)
-        for z, Bz in enumerate((bq, bk, bv)):
-            ops.pack_cols(Bz.detach().float().contiguous(), 0, r, D, r, 1, fz.wcat[z * D:, D + z * r8:], Kq)
-        a1 = torch.empty(Tp, Kq, device=dev, dtype=BF16)
-        ops.zero_(a1)
+        # LoRA factors as bf16 operands: A_all [64][D] (row z*r8 + i = A_z[i]); B columns of the q|k|v operand.
+        # `packed`: this step's pack is already in place (the teacher pass of the same block packed it)
+        a_all = fz.a_all if packed and SHARE_PACK and fz.a_all is not None else fz.pack_lora(aq, bq, ak, bk, av, bv)
+        if SHARE_PACK:
+            # one operand per block: the teacher pass writes it first, the student pass (saved for the
+            # backward) last; LN1 and the u GEMM rewrite the same region every call, the padding stays zero
+            a1 = fz.operand(T, Tp, Kq, dev)
+        else:
+            a1 = torch.empty(Tp, Kq, device=dev, dtype=BF16)
+            ops.zero_(a1)
         mu1, rs1 = torch.empty(T, device=dev), torch.empty(T, device=dev)
         ops.layernorm_fwd(xf, D, n1.weight, n1.bias, a1, Kq, mu1, rs1, T, D, eps1)
         # u_z = LN1(x) A_z^T -> columns D + z*r8 .. of the same operand
@@ -227,17 +262,19 @@ class _FusedLayer(torch.autograd.Function):
         grads = []
         for z in range(3):
             grads += [dA[z] if need[1 + 2 * z] else None, dB[z] if need[2 + 2 * z] else None]
-        return (dx, *grads, None)
+        return (dx, *grads, None, None)
 
 
-def full_layer(block, x):
+def full_layer(block, x, packed=False):
     """TransformerBlock._full(x) (res-vit/model.py:471-492: attention + residual, FFN + residual) as one
-    fused node; x [B, N, D] f32 -> [B, N, D] f32"""
+    fused node; x [B, N, D] f32 -> [B, N, D] f32. packed: a call on the same block earlier in this forward
+    (the teacher pass) packed the LoRA operands from the same weights"""
     if not hasattr(block, "_vitmi_frozen"):
         block._vitmi_frozen = _Frozen()
     a = block.attention
     return _FusedLayer.apply(x, a.lora_q.lora_A.weight, a.lora_q.lora_B.weight, a.lora_k.lora_A.weight,
-                             a.lora_k.lora_B.weight, a.lora_v.lora_A.weight, a.lora_v.lora_B.weight, block)
+                             a.lora_k.lora_B.weight, a.lora_v.lora_A.weight, a.lora_v.lora_B.weight, block,
+                             bool(packed and block._vitmi_frozen.a_all is not None))
 
 
 # ---- routed low-rank approximator step (res-vit/model.py:319-368) ------------------------------------
