@@ -33,29 +33,32 @@ using namespace vit_attn;
 constexpr int PB_NW = 8;
 
 #ifdef VIT_ATTN_STAMPS
-// DIAGNOSTIC build only (make ... EXTRA=-DVIT_ATTN_STAMPS): s_memtime stamps of workgroup 0's waves 0 and 7,
-// first 4 items, 8 points per item; read back with vit_attn_stamps()
+// DIAGNOSTIC build only (make ... EXTRA=-DVIT_ATTN_STAMPS): s_memtime stamps of workgroup 0's waves 0 and
+// VIT_STAMP_WAVE2 (default 7), first 4 items, 8 points per item; read back with vit_attn_stamps()
+#ifndef VIT_STAMP_WAVE2
+#define VIT_STAMP_WAVE2 7
+#endif
 __device__ unsigned long long g_attn_stamps[2][4][8];
 #define STAMP(k)                                                                                            \
   do {                                                                                                      \
-    if (blockIdx.x == 0 && (wave == 0 || wave == 7) && it < 4) {                                            \
+    if (blockIdx.x == 0 && (wave == 0 || wave == VIT_STAMP_WAVE2) && it < 4) {                                            \
       unsigned long long t_;                                                                                \
       __builtin_amdgcn_sched_barrier(0);                                                                    \
       asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");                            \
       __builtin_amdgcn_sched_barrier(0);                                                                    \
-      if (lane == 0) g_attn_stamps[wave == 7][it][k] = t_;                                                  \
+      if (lane == 0) g_attn_stamps[wave == VIT_STAMP_WAVE2][it][k] = t_;                                                  \
     }                                                                                                       \
   } while (0)
 // sub-phases of the wave's first strip of each item (stage 1)
 __device__ unsigned long long g_attn_stamps2[2][4][8];
 #define STAMP1(k)                                                                                           \
   do {                                                                                                      \
-    if (blockIdx.x == 0 && (wave == 0 || wave == 7) && it < 4 && qt == wave) {                              \
+    if (blockIdx.x == 0 && (wave == 0 || wave == VIT_STAMP_WAVE2) && it < 4 && qt == wave) {                              \
       unsigned long long t_;                                                                                \
       __builtin_amdgcn_sched_barrier(0);                                                                    \
       asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");                          \
       __builtin_amdgcn_sched_barrier(0);                                                                    \
-      if (lane == 0) g_attn_stamps2[wave == 7][it][k] = t_;                                                 \
+      if (lane == 0) g_attn_stamps2[wave == VIT_STAMP_WAVE2][it][k] = t_;                                                 \
     }                                                                                                       \
   } while (0)
 #else
@@ -302,9 +305,12 @@ __global__ void __launch_bounds__(PB_NW * 64, 1) attn_bwd_pers_kernel(const bf16
       const bool kv0 = (2 * kp) * 16 + i < N, kv1 = (2 * kp + 1) * 16 + i < N;
       // P and dS of the (key pair, query tile 2 qs + u) products, u < NU; MASK: the pair holds padded keys
       // (only the last pair: their P forced to 0). lse_s holds log2 units since stage 1 (padded queries 1e30).
-      auto scores = [&](int qs, auto nu, auto maskc, v4f (&Pm)[2][2], v4f (&DS)[2][2]) __attribute__((always_inline)) {
+      // NTK: key tiles of the pair that hold a valid key (1: the last pair's second tile is wholly padding, and
+      // its products are skipped instead of computed and masked to zero)
+      auto scores = [&](int qs, auto nu, auto maskc, auto ntk, v4f (&Pm)[2][2], v4f (&DS)[2][2]) __attribute__((always_inline)) {
         constexpr int NU = decltype(nu)::value;
         constexpr bool MASK = decltype(maskc)::value;
+        constexpr int NTK = decltype(ntk)::value;
 #pragma unroll
         for (int u = 0; u < NU; ++u) {
           const int qt = 2 * qs + u;
@@ -318,7 +324,7 @@ __global__ void __launch_bounds__(PB_NW * 64, 1) attn_bwd_pers_kernel(const bf16
           const v4f lq = *reinterpret_cast<const v4f*>(lse_s + qt * 16 + 4 * g);
           const v4f dq4 = *reinterpret_cast<const v4f*>(dlt_s + qt * 16 + 4 * g);
 #pragma unroll
-          for (int t = 0; t < 2; ++t) {
+          for (int t = 0; t < NTK; ++t) {
             v4f sv = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
             for (int kk = 0; kk < KK; ++kk) {
@@ -339,17 +345,21 @@ __global__ void __launch_bounds__(PB_NW * 64, 1) attn_bwd_pers_kernel(const bf16
         v8bf bP0, bP1, bD0, bD1;
       };
       // a whole query-tile pair: its products as the B operands of dV / dK (front), then the 16 MFMAs (back)
-      auto front = [&](int qs, auto maskc) __attribute__((always_inline)) {
+      auto front = [&](int qs, auto maskc, auto ntk) __attribute__((always_inline)) {
+        constexpr int NTK = decltype(ntk)::value;
         v4f Pm[2][2], DS[2][2];  // [key tile][query tile]
-        scores(qs, std::integral_constant<int, 2>{}, maskc, Pm, DS);
+        scores(qs, std::integral_constant<int, 2>{}, maskc, ntk, Pm, DS);
         Packed o;
         o.bP0 = pack8(Pm[0][0], Pm[0][1]);
-        o.bP1 = pack8(Pm[1][0], Pm[1][1]);
         o.bD0 = pack8(DS[0][0], DS[0][1]);
-        o.bD1 = pack8(DS[1][0], DS[1][1]);
+        if constexpr (NTK == 2) {
+          o.bP1 = pack8(Pm[1][0], Pm[1][1]);
+          o.bD1 = pack8(DS[1][0], DS[1][1]);
+        }
         return o;
       };
-      auto back = [&](int qs, const Packed& o) __attribute__((always_inline)) {
+      auto back = [&](int qs, const Packed& o, auto ntk) __attribute__((always_inline)) {
+        constexpr int NTK = decltype(ntk)::value;
 #pragma unroll
         for (int dt = 0; dt < HD / 16; ++dt) {
           v8s ot, qtr;
@@ -359,43 +369,55 @@ __global__ void __launch_bounds__(PB_NW * 64, 1) attn_bwd_pers_kernel(const bf16
           qtr.hi = lds_tr(Qi + (2 * qs + 1) * T + L2.tr[dt]);
           dv[0][dt] = mfma(__builtin_bit_cast(v8bf, ot), o.bP0, dv[0][dt]);
           dk[0][dt] = mfma(__builtin_bit_cast(v8bf, qtr), o.bD0, dk[0][dt]);
-          dv[1][dt] = mfma(__builtin_bit_cast(v8bf, ot), o.bP1, dv[1][dt]);
-          dk[1][dt] = mfma(__builtin_bit_cast(v8bf, qtr), o.bD1, dk[1][dt]);
+          if constexpr (NTK == 2) {
+            dv[1][dt] = mfma(__builtin_bit_cast(v8bf, ot), o.bP1, dv[1][dt]);
+            dk[1][dt] = mfma(__builtin_bit_cast(v8bf, qtr), o.bD1, dk[1][dt]);
+          }
         }
       };
       // the query pair's second tile wholly padding (past the images): tile 2 qs alone, the 16-deep MFMA
-      auto half_unit = [&](int qs, auto maskc) __attribute__((always_inline)) {
+      auto half_unit = [&](int qs, auto maskc, auto ntk) __attribute__((always_inline)) {
+        constexpr int NTK = decltype(ntk)::value;
         v4f Pm[2][2], DS[2][2];
-        scores(qs, std::integral_constant<int, 1>{}, maskc, Pm, DS);
-        const v4s bP0 = pack4(Pm[0][0]), bP1 = pack4(Pm[1][0]);
-        const v4s bD0 = pack4(DS[0][0]), bD1 = pack4(DS[1][0]);
+        scores(qs, std::integral_constant<int, 1>{}, maskc, ntk, Pm, DS);
+        const v4s bP0 = pack4(Pm[0][0]), bD0 = pack4(DS[0][0]);
 #pragma unroll
         for (int dt = 0; dt < HD / 16; ++dt) {
           const v4s ot = lds_tr(Oi + 2 * qs * T + L2.tr[dt]);
           const v4s qtr = lds_tr(Qi + 2 * qs * T + L2.tr[dt]);
           dv[0][dt] = mfma16_add(ot, bP0, dv[0][dt]);
           dk[0][dt] = mfma16_add(qtr, bD0, dk[0][dt]);
-          dv[1][dt] = mfma16_add(ot, bP1, dv[1][dt]);
-          dk[1][dt] = mfma16_add(qtr, bD1, dk[1][dt]);
+          if constexpr (NTK == 2) {
+            const v4s bP1 = pack4(Pm[1][0]), bD1 = pack4(DS[1][0]);
+            dv[1][dt] = mfma16_add(ot, bP1, dv[1][dt]);
+            dk[1][dt] = mfma16_add(qtr, bD1, dk[1][dt]);
+          }
         }
       };
       const int nfull = last_half && npair_q == npair ? npair_q - 1 : npair_q;
       // software-pipelined over query pairs: the products of pair qs + 1 (LDS reads, 16 MFMAs, the exp / dS
       // VALU) sit in one basic block with pair qs's dV / dK MFMAs, so one wave keeps both pipes busy
-      auto run = [&](auto maskc) __attribute__((always_inline)) {
+      auto run = [&](auto maskc, auto ntk) __attribute__((always_inline)) {
         if (nfull > 0) {
-          Packed cur = front(0, maskc);
+          Packed cur = front(0, maskc, ntk);
           for (int qs = 0; qs + 1 < nfull; ++qs) {
-            const Packed nxt = front(qs + 1, maskc);
-            back(qs, cur);
+            const Packed nxt = front(qs + 1, maskc, ntk);
+            back(qs, cur, ntk);
             cur = nxt;
           }
-          back(nfull - 1, cur);
+          back(nfull - 1, cur, ntk);
         }
-        if (nfull < npair_q) half_unit(nfull, maskc);
+        if (nfull < npair_q) half_unit(nfull, maskc, ntk);
       };
-      if (kp == npair - 1) run(std::true_type{});
-      else run(std::false_type{});
+      // the last pair holds the padded keys (masked); when its second tile is wholly padding (N <= 16 (2 kp + 1))
+      // only the first tile's products are computed: that wave had ~25% more stage-2 work than any other
+      // (stamps: 18.6 k against 15 k cycles at N = 197) and set the item's pace
+      if (kp == npair - 1) {
+        if (t1_valid) run(std::true_type{}, std::integral_constant<int, 2>{});
+        else run(std::true_type{}, std::integral_constant<int, 1>{});
+      } else {
+        run(std::false_type{}, std::integral_constant<int, 2>{});
+      }
       uint2 pk[2][HD / 16], pv[2][HD / 16];
 #pragma unroll
       for (int t = 0; t < 2; ++t)
