@@ -17,7 +17,7 @@ for spec in ${2:-l16:64 h14:128 resvit_b16:128}; do
   S=$(find $O/kt_$n -name "*kernel_stats.csv" | head -1)
   T=$(find $O/kt_$n -name "*kernel_trace.csv" | head -1)
   python3 tools/prof_summary.py $S 8 > $O/summary_$n.txt
-  python3 tools/trace_step.py $T 1 $O/launches_$n.txt > $O/timeline_$n.txt
+  python3 tools/trace_step.py $T 2 $O/launches_$n.txt > $O/timeline_$n.txt
   rm -rf $O/kt_$n
   head -16 $O/timeline_$n.txt
 done

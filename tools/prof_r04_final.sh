@@ -21,7 +21,7 @@ step "ktrace" timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format
 S=$(find $O/ktrace -name "*kernel_stats.csv" | head -1)
 T=$(find $O/ktrace -name "*kernel_trace.csv" | head -1)
 python3 tools/prof_summary.py $S 13 > $O/kernel_summary.txt
-python3 tools/trace_step.py $T 1 $O/step_launches.txt > $O/step_timeline.txt
+python3 tools/trace_step.py $T 2 $O/step_launches.txt > $O/step_timeline.txt
 cp $S $O/kernel_stats.csv
 rm -rf $O/ktrace
 RX='gemm_pp_kernel<256, 64, 2, false, false, 7>|gemm_\w+_kernel<.*, 8>|attn_bwd_pers_kernel'

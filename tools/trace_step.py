@@ -1,7 +1,9 @@
 #!/usr/bin/env python3
 """Per-step timeline view of a rocprofv3 kernel_trace.csv of bench.py.
 
-Splits the trace into steps at the SGD kernel, takes the last step, and reports per stream:
+Splits the trace into steps at the SGD kernel, takes the chosen step (bench.py: 2 = the last timed step; 1 is the
+probe step after the timed region, whose HIP events around the roofline kernels add ~6 us of idle each), and
+reports per stream:
 busy time (union of kernel intervals), and per kernel class the summed duration, plus the step's
 wall span and the time during which NO kernel runs (launch gaps / host waits).
 usage: trace_step.py run_kernel_trace.csv [step_index_from_end=1] [launch_list_out]
