@@ -44,6 +44,21 @@ def _rup(x, m):
 _ZROW = {}
 
 
+def _alloc_pad(rows_p, cols_p, rows, cols, dev, dtype=BF16):
+    """[rows_p][cols_p] buffer whose part outside [rows][cols] is zero; the caller writes the inside (instead of
+    torch.zeros: no full-buffer fill — at Res-ViT-B/16 bs 128, T = 25 216 is a multiple of 64 and most operands
+    have no padding at all)"""
+    out = torch.empty(rows_p, cols_p, device=dev, dtype=dtype)
+    if ZERO_FULL:
+        out.zero_()
+        return out
+    if rows_p > rows:
+        ops.zero_(out[rows:])
+    if cols_p > cols and rows:
+        out[:rows, cols:].zero_()
+    return out
+
+
 def _zero_row(n, dev):
     z = _ZROW.get(dev)
     if z is None or z.numel() < n:
@@ -70,6 +85,8 @@ def supported(block):
     return D % 64 == 0 and M % 64 == 0 and hd % 16 == 0 and hd <= 96 and 3 * _rup(r, 8) <= KX
 
 
+# A/B switch (bench.py VITMI_RESVIT_ZERO_FULL=1): every padded operand cleared whole, as before _alloc_pad
+ZERO_FULL = False
 # A/B switch (bench.py VITMI_RESVIT_PACK_EACH=1): False packs the LoRA factors and clears the q|k|v operand on
 # every call, as before round 4's shared pack
 SHARE_PACK = True
@@ -236,7 +253,7 @@ class _FusedLayer(torch.autograd.Function):
             ops.zero_(dqkv[T:])
         ops.attention_bwd(qkv, o, dO, lse, dqkv, B, N, H, hd, scale)
         # LoRA: v_z = dq_z B_z (batched), dB_z = dq_z^T u_z, dA_z = v_z^T LN1(x)
-        b_all = torch.zeros(3, D, r8, device=dev, dtype=BF16)
+        b_all = torch.empty(3, D, r8, device=dev, dtype=BF16)  # rows written whole (zero-padded to r8) below
         for z, Bz in enumerate((bq, bk, bv)):
             ops.cast_pad_rows(Bz.detach().float().contiguous(), D, r, b_all[z], r8)
         v_all = torch.empty(Tp, KX, device=dev, dtype=BF16)
@@ -331,7 +348,7 @@ class _ApproxStep(torch.autograd.Function):
             ops.zero_(db[T:])
         # dh = dout Wu: B(kk = n, n' = j) = Wu[n][j], MN-contiguous [D][r8]
         r8 = _rup(r, 8)
-        wut = torch.zeros(kp, r8, device=dev, dtype=BF16)
+        wut = _alloc_pad(kp, r8, D, r8, dev)
         ops.cast_pad_rows(wu.detach().float().contiguous(), D, r, wut, r8)
         dh = torch.empty(T, r, device=dev, dtype=F32)
         ops.gemm(db, wut, dh, T, r, kp, a_layout=K_CONTIG, b_layout=MN_CONTIG, lda=kp, ldb=r8, ldc=r,
@@ -345,7 +362,7 @@ class _ApproxStep(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             # dx = dout + dh Wd: B(kk = j, n' = k) = Wd[j][k], MN-contiguous [r64][D8]
             d8 = _rup(D, 8)
-            wdt = torch.zeros(rk, d8, device=dev, dtype=BF16)
+            wdt = _alloc_pad(rk, d8, r, d8, dev)
             ops.cast_pad_rows(wd.detach().float().contiguous(), r, D, wdt, d8)
             dx = torch.empty(T, D, device=dev, dtype=F32)
             ops.gemm(dhb, wdt, dx, T, D, rk, a_layout=K_CONTIG, b_layout=MN_CONTIG, lda=rk, ldb=d8, ldc=D,
@@ -401,8 +418,8 @@ def _mlp_forward(xb, T, kp, w1, b1, w2, b2, w3, b3):
     acts = []
     a_in, k_in = xb, kp
     for (b, n, npad), wb in zip(((b1, H1, h1p), (b2, H2, h2p)), ws[:2]):
-        g = torch.zeros(rp, npad, device=dev, dtype=BF16)
-        gp = torch.zeros(rp, npad, device=dev, dtype=BF16)
+        g = _alloc_pad(rp, npad, T, n, dev)
+        gp = _alloc_pad(rp, npad, T, n, dev)
         if T:
             ops.gemm(a_in, wb, gp, T, n, k_in, a_layout=K_CONTIG, b_layout=K_CONTIG, lda=k_in, ldb=k_in, ldc=npad,
                      epilogue=EPI_BIAS_GELU_DGELU, bias=b.detach().float().contiguous(), C2=g, ldc2=npad)
@@ -420,7 +437,7 @@ def _dgrad_mul(dyb, w, n_in, T, gp, npad_out):
     rp, dev = dyb.shape[0], dyb.device
     k8 = _rup(n_in, 8)
     wt = _pad_bf16(w.detach().float().contiguous(), dyb.shape[1], k8)
-    du = torch.zeros(rp, npad_out, device=dev, dtype=BF16)
+    du = _alloc_pad(rp, npad_out, T, n_in, dev)
     if T:
         ops.gemm(dyb, wt, du, T, n_in, dyb.shape[1], a_layout=K_CONTIG, b_layout=MN_CONTIG, lda=dyb.shape[1], ldb=k8,
                  ldc=npad_out, epilogue=EPI_MUL_BF16, aux=gp, ldaux=npad_out)
@@ -509,15 +526,15 @@ class _RouterNet(torch.autograd.Function):
         rp, dp, h0p = _rup(max(T, 1), 64), _rup(D, 64), _rup(Hh, 64)
         kp = _rup(K1, 64)
         x2 = x.contiguous().float().view(T, D)
-        lnb = torch.zeros(rp, dp, device=dev, dtype=BF16)
+        lnb = _alloc_pad(rp, dp, T, D, dev)
         mean = torch.empty(T, device=dev, dtype=F32)
         rstd = torch.empty(T, device=dev, dtype=F32)
         if T:
             ops.layernorm_fwd(x2, D, ln_w.detach().float().contiguous(), ln_b.detach().float().contiguous(), lnb, dp,
                               mean, rstd, T, D, eps)
         w0b = _pad_bf16(w0.detach().float().contiguous(), Hh, dp)
-        xcat = torch.zeros(rp, kp, device=dev, dtype=BF16)  # [x_embed | global] operand of out_conv
-        gp0 = torch.zeros(rp, h0p, device=dev, dtype=BF16)
+        xcat = _alloc_pad(rp, kp, T, K1, dev)  # [x_embed | global] operand of out_conv
+        gp0 = _alloc_pad(rp, h0p, T, Hh, dev)
         if T:
             ops.gemm(lnb, w0b, gp0, T, Hh, dp, a_layout=K_CONTIG, b_layout=K_CONTIG, lda=dp, ldb=dp, ldc=h0p,
                      epilogue=EPI_BIAS_GELU_DGELU, bias=b0.detach().float().contiguous(), C2=xcat, ldc2=kp)
