@@ -455,8 +455,9 @@ def _dgrad_f32(dyb, w, n_in, T):
     return dx
 
 
-def _mlp_backward(d2, T, xb, acts, w1, w2, w3, need_dx):
-    """gradients of _mlp_forward: (dX f32 [T][K1] or None, dW1, db1, dW2, db2, dW3, db3)"""
+def _mlp_backward(d2, T, xb, acts, w1, w2, w3, need_dx, out_du1=None):
+    """gradients of _mlp_forward: (dX f32 [T][K1] or None, dW1, db1, dW2, db2, dW3, db3); out_du1: a list that
+    receives the first layer's bf16 dU (its input gradient is then left to the caller)"""
     g1, gp1, g2, gp2 = acts
     rp, kp, h1p, h2p = xb.shape[0], xb.shape[1], g1.shape[1], g2.shape[1]
     H1, H2, O, K1 = w1.shape[0], w2.shape[0], w3.shape[0], w1.shape[1]
@@ -474,6 +475,8 @@ def _mlp_backward(d2, T, xb, acts, w1, w2, w3, need_dx):
     dw1 = torch.empty(H1, K1, device=dev, dtype=F32)
     ops.wgrad(du1, h1p, xb, kp, H1, K1, rp, dw1, K1)
     dx = _dgrad_f32(du1, w1, K1, T) if need_dx else None
+    if out_du1 is not None:
+        out_du1.append(du1)
     return dx, dw1, db1, dw2, db2, dw3, db3
 
 
@@ -553,11 +556,18 @@ class _RouterNet(torch.autograd.Function):
         dev = dout.device
         rp, dp, h0p = xcat.shape[0], lnb.shape[1], gp0.shape[1]
         d2 = dout.contiguous().float().view(T, w3.shape[0])
-        dcat, *mlp_grads = _mlp_backward(d2, T, xcat, (g1, gp1, g2, gp2), w1, w2, w3, True)
-        dc = dcat.view(B, N, K1)
-        dxe = dc[:, :, :Hh].clone()
-        dxe[:, reserve:, :] += (dc[:, :, Hh:].sum(dim=1) / (N - reserve))[:, None, :]
-        du0 = dxe.view(T, Hh) * gp0[:T, :Hh].float()
+        du1l = []
+        _, *mlp_grads = _mlp_backward(d2, T, xcat, (g1, gp1, g2, gp2), w1, w2, w3, False, du1l)
+        du1 = du1l[0]
+        H1 = w1.shape[0]
+        # out_conv's input gradient, by halves: the x_embed half as one GEMM (dU1 W1[:, :h]); the global half
+        # only through its per-image token sum, which by linearity is (sum_t dU1[t]) W1[:, h:] — a [B][h]
+        # product instead of a [T][h] GEMM, a copy and a token reduction of it
+        dxe = _dgrad_f32(du1, w1[:, :Hh], Hh, T).view(B, N, Hh)
+        s1 = du1[:T].view(B, N, du1.shape[1])[:, :, :H1].sum(dim=1, dtype=F32)
+        w1r = w1.detach()[:, Hh:].to(BF16).float()  # the bf16 operand values the per-token GEMM would use
+        dxe[:, reserve:, :] += (torch.matmul(s1, w1r) / (N - reserve))[:, None, :]
+        du0 = dxe.view(T, Hh) * gp0[:T, :Hh]
         du0b = _pad_bf16(du0, rp, h0p)
         db0 = _colsum(du0b, T, Hh, h0p)
         dw0 = torch.empty(Hh, D, device=dev, dtype=F32)
