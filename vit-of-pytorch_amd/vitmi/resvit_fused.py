@@ -319,9 +319,7 @@ class _ApproxStep(torch.autograd.Function):
             ops.zero_(xb[T:])
         wdb = torch.empty(r, kp, device=dev, dtype=BF16)  # B(k, n) = Wd[n][k]: K-contiguous
         ops.cast_pad_rows(wd.detach().float().contiguous(), r, D, wdb, kp)
-        hb = torch.empty(rp, rk, device=dev, dtype=BF16)
-        if rp > T or rk > r:
-            ops.zero_(hb)
+        hb = _alloc_pad(rp, rk, T, r, dev)
         ops.gemm(xb, wdb, hb, T, r, kp, a_layout=K_CONTIG, b_layout=K_CONTIG, lda=kp, ldb=kp, ldc=rk,
                  epilogue=EPI_BF16)
         selb = sel.reshape(T, 1).to(BF16)
@@ -350,13 +348,11 @@ class _ApproxStep(torch.autograd.Function):
         r8 = _rup(r, 8)
         wut = _alloc_pad(kp, r8, D, r8, dev)
         ops.cast_pad_rows(wu.detach().float().contiguous(), D, r, wut, r8)
-        dh = torch.empty(T, r, device=dev, dtype=F32)
-        ops.gemm(db, wut, dh, T, r, kp, a_layout=K_CONTIG, b_layout=MN_CONTIG, lda=kp, ldb=r8, ldc=r,
-                 epilogue=EPI_F32)
-        dhb = torch.empty(rp, rk, device=dev, dtype=BF16)
-        ops.cast_pad_rows(dh, T, r, dhb, rk)
-        if rp > T:
-            ops.zero_(dhb[T:])
+        # dh = dout Wu, rounded to the bf16 operand by the GEMM's epilogue (the same RNE rounding as a cast of the
+        # f32 product: no f32 [T][r] pass)
+        dhb = _alloc_pad(rp, rk, T, r, dev)
+        ops.gemm(db, wut, dhb, T, r, kp, a_layout=K_CONTIG, b_layout=MN_CONTIG, lda=kp, ldb=r8, ldc=rk,
+                 epilogue=EPI_BF16)
         dhb[:T].mul_(selb)
         dx = dwd = dwu = None
         if ctx.needs_input_grad[0]:
