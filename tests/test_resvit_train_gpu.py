@@ -10,8 +10,9 @@ torch.nn.utils.clip_grad_norm_(params, 1.0) and transformers.get_cosine_schedule
 * end to end: the three steps through vitmi.resvit_train.train_step with the reference's Gumbel draws
   and routing decisions replayed: every step's losses (1e-3 relative; bf16 operands), clip norm
   (2e-2) and the parameter trajectory (the accumulated update p3 - p0 of every tensor with a
-  meaningful update within 0.15 relative: Adam's first steps are ~lr * sign(g), so bf16-level gradient
-  noise flips the sign of near-zero gradient elements).
+  meaningful update within 0.10 relative: Adam's first steps are ~lr * sign(g), so bf16-level gradient
+  noise flips the sign of near-zero gradient elements; measured round 4: at most 6.5e-2, layer 1's
+  lora_k and approximator up-projection, both paths).
 """
 import os
 
@@ -144,8 +145,10 @@ def test_three_training_steps_match_reference(gold, fused):
         if float(np.square(d_ref).sum()) < 1e-4 * tot_upd:
             continue
         d_me = named[n].detach().double().cpu() - torch.from_numpy(gold["p0/" + n]).double()
-        if rel(d_me, d_ref) > 0.15:
-            bad.append((n, rel(d_me, d_ref)))
+        e = rel(d_me, d_ref)
+        print(f"update rel {n}: {e:.3e}")
+        if e > 0.10:
+            bad.append((n, e))
     assert not bad, bad
 
 
