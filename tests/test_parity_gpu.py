@@ -180,6 +180,34 @@ def test_b16_full_gradients_match_oracle():
     check_grads(m, ref_grads)
 
 
+def test_b16_bs256_gradients_match_oracle_fp32_on_gpu():
+    """The benchmarked shape itself (ViT-B/16 @224, bs 256, T = 50 432 rows: the wave-split GEMM tiles, the split-K
+    weight gradients over every token, the persistent attention kernels): logits, loss and every gradient
+    tensor against the oracle's step evaluated in fp32 on the GPU (torch fp32 ops as the checker, TF32 off; on
+    the CPU it takes about half a minute). Same tolerances as the bs-2 test above."""
+    from vitmi.model import CrossEntropyLoss
+    params = tame_params(init_params(B16, seed=42))
+    g = torch.Generator().manual_seed(13)
+    x = torch.randn(256, 3, 224, 224, generator=g)
+    y = torch.randint(0, 1000, (256,), generator=g)
+    tf32 = (torch.backends.cuda.matmul.allow_tf32, torch.backends.cudnn.allow_tf32)
+    torch.backends.cuda.matmul.allow_tf32 = torch.backends.cudnn.allow_tf32 = False
+    try:
+        pg = OrderedDict((k, v.cuda()) for k, v in params.items())
+        ref_logits, ref_loss, ref_grads = loss_and_grads(pg, x.cuda(), y.cuda(), B16)
+        ref_grads = OrderedDict((k, v.cpu()) for k, v in ref_grads.items())
+        del pg
+    finally:
+        torch.backends.cuda.matmul.allow_tf32, torch.backends.cudnn.allow_tf32 = tf32
+    m = make_model(B16, params)
+    logits = m(x.cuda())
+    loss = CrossEntropyLoss()(logits, y.cuda())
+    loss.backward()
+    assert rel(logits, ref_logits) < 1e-2
+    assert abs(float(loss.detach()) - float(ref_loss)) <= 1e-3 * abs(float(ref_loss))
+    check_grads(m, ref_grads)
+
+
 # ---- fp32 ("exact") forward: the north-star logits gate (<= 1e-3 relative) -----------------------
 H80 = ViTConfig(image_size=28, patch_size=14, emb_dim=320, mlp_dim=640, num_heads=4, num_layers=2, num_classes=10)
 
