@@ -376,6 +376,11 @@ int vit_adamw_chunk_elems(void);
 int vit_scale_by_coef(float* g, int64_t n, const float* coef, vit_stream_t stream);
 /* bytes of device memory at ptr set to 0 on the stream (hipMemsetAsync) */
 int vit_zero(void* ptr, int64_t bytes, vit_stream_t stream);
+/* rows whose mask byte (mask[r], e.g. a torch.bool [rows] tensor) is 0: dst + r*dld <- src + r*sld, row_bytes bytes
+ * (zeros when src is NULL); other rows untouched. 16-B aligned rows, row_bytes % 16 == 0. Res-ViT's routed-layer
+ * selection `where(active, layer(x), x)` (res-vit/model.py:507-512) and its backward masks, inside the fused layer. */
+int vit_rows_select(void* dst, int64_t dld, const void* src, int64_t sld, const void* mask, int64_t rows,
+                    int64_t row_bytes, vit_stream_t stream);
 /* height rows of width bytes: dst + r*dpitch <- src + r*spitch (hipMemcpy2DAsync, device to device) */
 int vit_copy2d(void* dst, int64_t dpitch, const void* src, int64_t spitch, int64_t width, int64_t height,
                vit_stream_t stream);

@@ -370,6 +370,42 @@ def test_fused_layer_matches_per_op_path(dims):
         assert rel(a, b) < 2e-2
 
 
+def test_fused_layer_row_selection_matches_where():
+    """The routed student's where(active, layer(x), x) (res-vit/model.py:507-512) folded into the fused layer node
+    (vit_rows_select on the output, the output gradient masked in the backward, the where's x-gradient carried on
+    the LN1 backward's residual input) against the same node followed by torch.where: output and the six LoRA
+    gradients bit for bit, the input gradient to one f32 rounding; T = 3 x 197 rows, about half active."""
+    from vitmi import resvit
+    torch.manual_seed(3)
+    args = resvit.ModelArgs(**dict(TINY, dim=128, n_heads=2, n_kv_heads=2, mlp_dim=256, device="cuda"))
+    m = resvit.Transformer(args).cuda()
+    blk = m.layers[0]
+    with torch.no_grad():
+        for p in blk.attention.parameters():
+            if p.requires_grad:
+                p.normal_(0.0, 0.05)
+    g = torch.Generator(device="cuda").manual_seed(9)
+    x = torch.randn(3, 197, args.dim, device="cuda", generator=g)
+    w = torch.randn(3, 197, args.dim, device="cuda", generator=g)
+    active = torch.rand(3, 197, 1, device="cuda", generator=g) < 0.5
+    lora = [p for p in blk.attention.parameters() if p.requires_grad]
+    res = []
+    for folded in (True, False):
+        xi = x.clone().requires_grad_(True)
+        for p in lora:
+            p.grad = None
+        out = blk._full(xi, active=active) if folded else torch.where(active, blk._full(xi), xi)
+        (out * w).sum().backward()
+        res.append((out.detach(), xi.grad.detach(), [p.grad.detach().clone() for p in lora]))
+    (o1, dx1, g1), (o0, dx0, g0) = res
+    assert torch.equal(o1, o0)
+    for a, b in zip(g1, g0):
+        assert torch.equal(a, b)
+    # dx: on the inactive rows the LN1 backward now adds dout inside its fused multiply-add instead of autograd
+    # adding it after the kernel's own rounding: equal up to that one rounding
+    assert bool(((dx1 - dx0).abs() <= 2.0 ** -22 * dx0.abs() + 1e-30).all()) or rel(dx1, dx0) < 1e-6
+
+
 @pytest.mark.parametrize("B,N,r", [(3, 197, 16), (2, 17, 256), (1, 65, 32)])
 def test_fused_approximator_matches_per_op_path(B, N, r):
     """vitmi.resvit_fused.approx_step (one node: down GEMM with a bf16 epilogue, unselected rows zeroed, up GEMM

@@ -213,6 +213,34 @@ extern "C" int vit_zero(void* ptr, int64_t bytes, vit_stream_t stream) {
   return vit::check_hip(hipMemsetAsync(ptr, 0, (size_t)bytes, (hipStream_t)stream), "vit_zero");
 }
 
+// Row selection (Res-ViT's `where(active, layer(x), x)` folded into the layer node): every row r whose mask byte is 0
+// gets dst row r <- src row r (zeros when src is null); rows whose mask byte is non-zero are left alone. 16-B chunks.
+__global__ void rows_select_kernel(char* __restrict__ dst, long dld, const char* __restrict__ src, long sld,
+                                   const unsigned char* __restrict__ mask, long rows, long chunks) {
+  const long n = rows * chunks;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const long r = i / chunks, c = i - r * chunks;
+    if (mask[r]) continue;
+    const uint4 v = src ? *reinterpret_cast<const uint4*>(src + r * sld + c * 16) : make_uint4(0u, 0u, 0u, 0u);
+    *reinterpret_cast<uint4*>(dst + r * dld + c * 16) = v;
+  }
+}
+
+extern "C" int vit_rows_select(void* dst, int64_t dld, const void* src, int64_t sld, const void* mask, int64_t rows,
+                               int64_t row_bytes, vit_stream_t stream) {
+  VIT_CHECK_ARG(dst && mask && rows >= 0 && row_bytes >= 0 && row_bytes % 16 == 0 && dld % 16 == 0 &&
+                    (src == nullptr || sld % 16 == 0) && ((uintptr_t)dst | (uintptr_t)src) % 16 == 0,
+                "vit_rows_select: bad args (16-B aligned rows of a multiple of 16 bytes)");
+  VIT_CHECK_ARG(dld >= row_bytes && (src == nullptr || sld >= row_bytes), "vit_rows_select: row pitch below row_bytes");
+  const long n = (long)rows * (row_bytes / 16);
+  if (n == 0) return VIT_OK;
+  long blocks = (n + 255) / 256;
+  blocks = blocks > 8192 ? 8192 : blocks;
+  hipLaunchKernelGGL(rows_select_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, (char*)dst,
+                     (long)dld, (const char*)src, (long)sld, (const unsigned char*)mask, (long)rows, (long)(row_bytes / 16));
+  VIT_LAUNCH_CHECK("vit_rows_select");
+}
+
 extern "C" int vit_copy2d(void* dst, int64_t dpitch, const void* src, int64_t spitch, int64_t width, int64_t height,
                           vit_stream_t stream) {
   VIT_CHECK_ARG(dst && src && width >= 0 && height >= 0 && dpitch >= width && spitch >= width, "vit_copy2d: bad args");

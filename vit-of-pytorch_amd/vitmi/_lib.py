@@ -114,6 +114,7 @@ _SIGS = {
     "vit_scale_by_coef": (c_i32, [c_vp, c_i64, c_vp, c_vp]),
     "vit_zero": (c_i32, [c_vp, c_i64, c_vp]),
     "vit_copy2d": (c_i32, [c_vp, c_i64, c_vp, c_i64, c_i64, c_i64, c_vp]),
+    "vit_rows_select": (c_i32, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_i64, c_vp]),
     "vit_sgd_step_dev": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_f32, c_vp]),
 }
 

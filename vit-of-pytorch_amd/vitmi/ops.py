@@ -383,6 +383,18 @@ def wgrad(A, lda, B, ldb, M, N, K, out, ldo, accumulate=False, batch=1, a_bs=0, 
     splitk_reduce(ws, batch, s, M, N, out, ldo, out_bs, accumulate)
 
 
+def rows_select(dst, mask, src=None):
+    """rows r of the 2-D tensor dst with mask[r] False <- src's row r (zeros when src is None); mask: bool [rows]"""
+    if mask.dtype != torch.bool or not mask.is_contiguous() or mask.numel() != dst.shape[0]:
+        raise ValueError("rows_select: mask must be a contiguous bool tensor of dst.shape[0] elements")
+    rb = dst.shape[1] * dst.element_size()
+    if src is not None and (src.dtype != dst.dtype or src.shape[1] != dst.shape[1]):
+        raise ValueError("rows_select: src must match dst's dtype and row width")
+    check(lib().vit_rows_select(_p(dst), dst.stride(0) * dst.element_size(), _p(src),
+                                0 if src is None else src.stride(0) * src.element_size(), _p(mask), dst.shape[0], rb,
+                                _stream()), "vit_rows_select")
+
+
 def copy2d(dst, dpitch, src, spitch, width, height):
     """height rows of `width` bytes, dst + r*dpitch <- src + r*spitch (byte pitches; hipMemcpy2DAsync)"""
     check(lib().vit_copy2d(_p(dst), dpitch, _p(src), spitch, width, height, _stream()), "vit_copy2d")

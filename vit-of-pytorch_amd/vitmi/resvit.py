@@ -392,6 +392,10 @@ class BlockPathApproximators(nn.Module):
         return x
 
 
+# the routed student's where(active, layer(x), x) folded into the fused layer node (False: torch.where after it)
+FOLD_SELECT = True
+
+
 def _select_rows(mask, a, b):
     """mask [.., 1] bool: rows of a where set, of b elsewhere (the reference's mask * a + (~mask) * b)."""
     return torch.where(mask, a, b)
@@ -427,11 +431,14 @@ class TransformerBlock(nn.Module):
                                            args.norm_eps, block_size=self.block_size, use_lora=args.use_lora)
                 self.block_path_approximators = BlockPathApproximators(args.dim, args.low_rank_dim, self.block_size)
 
-    def _full(self, x, packed=False):
+    def _full(self, x, packed=False, active=None):
+        """the full layer; with `active` (bool [B, N, 1]) where(active, layer(x), x), the routed student's rows"""
         if self.fused and x.dim() == 3 and x.is_cuda and _fused.supported(self):
-            return _fused.full_layer(self, x, packed)  # one fused node (LoRA configuration, vitmi.resvit_fused)
+            # one fused node (LoRA configuration, vitmi.resvit_fused), the row selection folded in
+            return _fused.full_layer(self, x, packed, active)
         h = HF.add(self.attention(self.attention_norm(x)), x)
-        return HF.add(self.feed_forward(self.ffn_norm(h)), h)
+        out = HF.add(self.feed_forward(self.ffn_norm(h)), h)
+        return out if active is None else _select_rows(active, out, x)
 
     def forward(self, x, teacher_x=None, block_info: Optional[Dict] = None, LRA_mask: Optional[List] = None):
         bsz, seqlen, _ = x.shape
@@ -465,7 +472,10 @@ class TransformerBlock(nn.Module):
             with torch.no_grad():
                 teacher_out = self._full(x if teacher_x is None else teacher_x)
             # same block, same LoRA weights: the teacher pass's operand pack serves the student pass
-            student_out = _select_rows(active, self._full(x, packed=True), x)
+            if FOLD_SELECT:
+                student_out = self._full(x, packed=True, active=active)
+            else:  # A/B (bench.py VITMI_RESVIT_WHERE_OPS=1): the layer node, then torch.where
+                student_out = _select_rows(active, self._full(x, packed=True), x)
             return teacher_out, approximators(student_out, router_indices, lra_lora), w, block_info
 
         # inference: only the active tokens query (ragged), every token is a key / value

@@ -163,7 +163,7 @@ class _Frozen:
 
 class _FusedLayer(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, aq, bq, ak, bk, av, bv, block, packed):
+    def forward(ctx, x, aq, bq, ak, bk, av, bv, block, packed, active):
         a, ff = block.attention, block.feed_forward
         fz = block._vitmi_frozen.get(block)
         B, N, D = x.shape
@@ -214,6 +214,11 @@ class _FusedLayer(torch.autograd.Function):
         out = torch.empty(T, D, device=dev)
         ops.gemm(g, fz.w2, out, T, D, M, a_layout=K_CONTIG, b_layout=K_CONTIG, lda=M, ldb=M, ldc=D,
                  epilogue=EPI_BIAS_RESID_F32, bias=ff.fc2.bias.detach(), aux=h, ldaux=D)
+        am = None
+        if active is not None:  # where(active, layer(x), x): the inactive rows of the output take x's rows
+            am = active.reshape(T)
+            ops.rows_select(out, am, xf)
+        ctx.active = am
         if torch.is_grad_enabled() or any(ctx.needs_input_grad):
             ctx.save_for_backward(xf, a1, mu1, rs1, qkv, o, lse, h, mu2, rs2, gp, a_all, bq, bk, bv)
             ctx.block = block
@@ -232,6 +237,9 @@ class _FusedLayer(torch.autograd.Function):
         dout = dout.contiguous().float().view(T, D)
         dob = torch.empty(T, D, device=dev, dtype=BF16)
         ops.cast_bf16(dout, dob, T * D)
+        am = ctx.active
+        if am is not None:  # the layer's output gradient is dout on the active rows only
+            ops.rows_select(dob, am)
         # fc2 data gradient x GELU'(fc1 pre-activation)
         dg = torch.empty(T, M, device=dev, dtype=BF16)
         ops.gemm(dob, fz.w2_t, dg, T, M, D, a_layout=K_CONTIG, b_layout=K_CONTIG, lda=D, ldb=D, ldc=M,
@@ -243,8 +251,13 @@ class _FusedLayer(torch.autograd.Function):
         part = torch.empty(ops.layernorm_bwd_partial_rows(T), 3 * D, device=dev)
         dh = torch.empty(T, D, device=dev)
         dhb = torch.empty(T, D, device=dev, dtype=BF16)
+        # with a row selection the residual path carries all of dout: on an inactive row the layer's branches
+        # get no gradient (dy2 = 0 there) and dh = dout is exactly the where's gradient to x, carried on to the
+        # LN1 backward's residual input; the attention branch's operand keeps the layer's own (masked) dh
         ops.layernorm_bwd(dy2, D, h, D, mu2, rs2, n2.weight, dh, D, part, T, D, dres=dout, lddres=D, dx_bf16=dhb,
                           lddxb=D)
+        if am is not None:
+            ops.rows_select(dhb, am)
         dO = torch.empty(T, D, device=dev, dtype=BF16)
         ops.gemm(dhb, fz.wo_t, dO, T, D, D, a_layout=K_CONTIG, b_layout=K_CONTIG, lda=D, ldb=D, ldc=D,
                  epilogue=EPI_BF16)
@@ -279,19 +292,21 @@ class _FusedLayer(torch.autograd.Function):
         grads = []
         for z in range(3):
             grads += [dA[z] if need[1 + 2 * z] else None, dB[z] if need[2 + 2 * z] else None]
-        return (dx, *grads, None, None)
+        return (dx, *grads, None, None, None)
 
 
-def full_layer(block, x, packed=False):
+def full_layer(block, x, packed=False, active=None):
     """TransformerBlock._full(x) (res-vit/model.py:471-492: attention + residual, FFN + residual) as one
     fused node; x [B, N, D] f32 -> [B, N, D] f32. packed: a call on the same block earlier in this forward
-    (the teacher pass) packed the LoRA operands from the same weights"""
+    (the teacher pass) packed the LoRA operands from the same weights. active (bool [B, N, 1]): the routed
+    student's where(active, layer(x), x) (res-vit/model.py:507-512) folded into the node"""
     if not hasattr(block, "_vitmi_frozen"):
         block._vitmi_frozen = _Frozen()
     a = block.attention
     return _FusedLayer.apply(x, a.lora_q.lora_A.weight, a.lora_q.lora_B.weight, a.lora_k.lora_A.weight,
                              a.lora_k.lora_B.weight, a.lora_v.lora_A.weight, a.lora_v.lora_B.weight, block,
-                             bool(packed and block._vitmi_frozen.a_all is not None))
+                             bool(packed and block._vitmi_frozen.a_all is not None),
+                             None if active is None else active.contiguous())
 
 
 # ---- routed low-rank approximator step (res-vit/model.py:319-368) ------------------------------------
