@@ -3,7 +3,7 @@
 # Res-ViT-B/16 bs 128 line on the final code
 set -o pipefail
 export TMPDIR=/tmp
-O=gpurun_out/r04_final_v4; mkdir -p $O
+O=gpurun_out/r04_final_v5; mkdir -p $O
 step() { echo "== $1"; shift; "$@" || { echo "FAILED: $*"; exit 1; }; }
 step "pytest -m gpu" timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1
 tail -1 $O/gpu_tests.log
