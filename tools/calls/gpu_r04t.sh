@@ -4,7 +4,7 @@
 set -o pipefail
 export TMPDIR=/tmp
 O=gpurun_out/r04t; rm -rf $O; mkdir -p $O
-for spec in b16:256 l16:64 h14:128 resvit_b16:128; do
+for spec in ${SPECS:-b16:256 l16:64 h14:128 resvit_b16:128}; do
   arch=${spec%%:*}; bs=${spec##*:}; n=${arch}_bs${bs}
   timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $O/kt_$n -o run -- python3 bench.py --arch $arch --batch $bs --steps 6 --warmup 2 --no-cpu-baseline > $O/kt_$n.log 2>&1 || { tail -5 $O/kt_$n.log; exit 1; }
   T=$(find $O/kt_$n -name "*kernel_trace.csv" | head -1)
