@@ -435,6 +435,9 @@ def bench_resvit(args, world, rank, dev, backend, comm):
     if os.environ.get("VITMI_RESVIT_ZERO_FULL", "0") != "0":  # A/B: padded operands cleared whole
         from vitmi import resvit_fused
         resvit_fused.ZERO_FULL = True
+    if os.environ.get("VITMI_RESVIT_NO_SINK", "0") != "0":  # A/B: weight gradients through AccumulateGrad
+        from vitmi import flat as vflat
+        vflat.SINKS = False
     if os.environ.get("VITMI_RESVIT_APPROX_OPS", "0") != "0":  # A/B: the per-op approximator path
         for l in model.layers:
             if hasattr(l, "block_path_approximators"):

@@ -203,6 +203,46 @@ def test_graphed_step_matches_eager_and_reference(gold, fused, warmup):
     assert all(torch.equal(a, b) for a, b in zip(pe, pg))
 
 
+def test_grad_sinks_match_autograd_accumulation(gold, monkeypatch):
+    """vitmi.flat.grad_sink: the fused router-MLP / approximator nodes accumulate their weight gradients in place
+    into the flat .grad views (no AccumulateGrad add) — three reference steps (routing replayed) end with
+    bit-identical losses, parameters and used flags to the same steps through autograd's accumulation, and
+    the sinks were taken."""
+    from vitmi import flat as vflat
+    from vitmi.optim import AdamW, get_cosine_schedule_with_warmup
+    from vitmi.resvit_train import train_step
+    h = hp(gold)
+    taken = []
+    real_sunk = vflat.sunk
+    monkeypatch.setattr(vflat, "sunk", lambda p: (taken.append(id(p)), real_sunk(p)))
+    runs = []
+    for sinks in (False, True):
+        monkeypatch.setattr(vflat, "SINKS", sinks)
+        m = build(gold).train()
+        opt = AdamW(m.parameters(), lr=h["lr"], weight_decay=h["wd"], betas=h["betas"], eps=h["eps"],
+                    max_grad_norm=1.0)
+        sched = get_cosine_schedule_with_warmup(opt, h["warmup"], h["total"])
+        routers = [l.router for l in m.layers if hasattr(l, "router")]
+        losses = []
+        for s in range(3):
+            for j, r in enumerate(routers):
+                hh = torch.from_numpy(gold[f"s{s}/router{j}_hard"]).cuda()
+                gg = torch.from_numpy(gold[f"s{s}/gumbel{j}"]).cuda()
+                r.hard_override = lambda logits, hh=hh: hh
+                r.gumbel_noise = lambda logits, gg=gg: gg
+            x = torch.from_numpy(gold[f"s{s}/x"]).cuda()
+            y = torch.from_numpy(gold[f"s{s}/y"]).cuda()
+            out = train_step(m, x, y, opt, sched, h["la"], h["ld"], h["lc"], clip_grad_norm=True)
+            losses.append(torch.stack([out[0], out[1], out[3]]).detach().clone())
+        runs.append((torch.stack(losses), [p.detach().clone() for p in opt.flat.params], opt.flat.used.clone(),
+                     len(taken)))
+    (l0, p0, u0, n0), (l1, p1, u1, n1) = runs
+    assert n0 == 0 and n1 > 0, (n0, n1)
+    assert torch.equal(l0, l1)
+    assert torch.equal(u0, u1)
+    assert all(torch.equal(a, b) for a, b in zip(p0, p1))
+
+
 def test_flat_params_keep_grad_views_and_skip_unused():
     """FlatParams: parameters become views of one buffer, autograd accumulates into the preset .grad
     views in place, a parameter outside the graph is marked unused, module.zero_grad() (set_to_none)

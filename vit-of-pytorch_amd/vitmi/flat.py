@@ -11,7 +11,9 @@ Gradients: each parameter's `.grad` is preset to its view of the flat gradient b
 accumulates into an existing `.grad` in place, so the backward writes the flat buffer directly. A
 post-accumulate hook marks which parameters received a gradient in this step — torch's AdamW skips a
 parameter whose `.grad` is None (an approximator no token was routed to), and so does the HIP update
-(`used` flags; vit_adamw_prep). A `.grad` replaced behind our back (module.zero_grad() setting it to
+(`used` flags; vit_adamw_prep). The fused Res-ViT nodes (vitmi.resvit_fused) go one step further: their
+weight-gradient reductions accumulate straight into a flat `.grad` view (`grad_sink`) and return None for
+that parameter, so no AccumulateGrad add runs at all; they then run the same marking. A `.grad` replaced behind our back (module.zero_grad() setting it to
 None, then a fresh tensor from autograd) is folded back into the flat buffer by `adopt_grads()`.
 """
 from __future__ import annotations
@@ -47,6 +49,29 @@ def _take_gate(p):
         return None
     del _GATES[id(p)]
     return e[1]
+
+
+# A/B switch (bench.py VITMI_RESVIT_NO_SINK=1): False leaves every gradient to autograd's AccumulateGrad (one add
+# into the flat view per parameter and step)
+SINKS = True
+
+
+def grad_sink(p, need=True):
+    """the gradient view a backward node may accumulate p's gradient into in place (returning None for p), or
+    None: p is not held by a live FlatParams, its .grad is no longer the flat view, or the backward records a
+    graph (create_graph)"""
+    if not (SINKS and need) or torch.is_grad_enabled():
+        return None
+    e = getattr(p, "_vitmi_flat", None)
+    f = e[0]() if e is not None else None
+    return f.sink(p) if f is not None else None
+
+
+def sunk(p):
+    """after a node accumulated p's gradient through grad_sink: what AccumulateGrad's post hook would do"""
+    f = p._vitmi_flat[0]()
+    if f is not None:
+        f._mark(p)
 
 
 def _rup(x, m):
@@ -95,6 +120,9 @@ class FlatParams:
         self._gate_idx = {}
         self._used_k = 0
         self.on_grad = None  # callable(segment index) after each parameter's gradient accumulation
+        me = weakref.ref(self)
+        for i, p in enumerate(ps):
+            p._vitmi_flat = (me, i)  # (grad_sink: fused backward nodes accumulate into the flat view in place)
         self._hooks = [p.register_post_accumulate_grad_hook(self._mark) for p in ps]
         # update chunks: (segment, start, length), <= vit_adamw_chunk_elems() elements, inside one segment
         ch = ops.adamw_chunk_elems()
@@ -111,6 +139,14 @@ class FlatParams:
     def view(self, buf, i):
         p, o = self.params[i], self.offsets[i]
         return buf[o:o + p.numel()].view(p.shape)
+
+    def sink(self, p):
+        """p's flat gradient view when p.grad still is that view (else None: autograd's own accumulation)"""
+        i = self._index.get(id(p))
+        if i is None or p.grad is None:
+            return None
+        o = self.offsets[i]
+        return p.grad if p.grad.data_ptr() == self.grad[o:o + 1].data_ptr() else None
 
     def _mark(self, p):
         i = self._index[id(p)]

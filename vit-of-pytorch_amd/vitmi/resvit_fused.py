@@ -29,6 +29,7 @@ import math
 
 import torch
 
+from . import flat as _flat
 from . import ops
 from ._lib import (EPI_BF16, EPI_BIAS_BF16, EPI_BIAS_GELU_DGELU, EPI_BIAS_RESID_F32, EPI_F32, EPI_MUL_BF16,
                    K_CONTIG, MN_CONTIG)
@@ -345,6 +346,7 @@ class _ApproxStep(torch.autograd.Function):
         ops.gemm(hb, wub, out, T, D, rk, a_layout=K_CONTIG, b_layout=K_CONTIG, lda=rk, ldb=rk, ldc=D,
                  epilogue=EPI_BIAS_RESID_F32, bias=_zero_row(D, dev), aux=x2, ldaux=D)
         ctx.save_for_backward(xb, hb, wd, wu, selb)
+        ctx.params = (wd, wu)
         ctx.dims = (B, N, D, T, r)
         return out.view(B, N, D)
 
@@ -379,12 +381,12 @@ class _ApproxStep(torch.autograd.Function):
             ops.gemm(dhb, wdt, dx, T, D, rk, a_layout=K_CONTIG, b_layout=MN_CONTIG, lda=rk, ldb=d8, ldc=D,
                      epilogue=EPI_BIAS_RESID_F32, bias=_zero_row(D, dev), aux=d2, ldaux=D)
             dx = dx.view(B, N, D)
+        marks = []
         if ctx.needs_input_grad[2]:  # dWu [D][r] = dout^T h
-            dwu = torch.empty(D, r, device=dev, dtype=F32)
-            ops.wgrad(db, kp, hb, rk, D, r, rp, dwu, r)
+            dwu = _wgrad(db, kp, hb, rk, D, r, rp, ctx.params[1], True, marks)
         if ctx.needs_input_grad[1]:  # dWd [r][D] = dh^T x
-            dwd = torch.empty(r, D, device=dev, dtype=F32)
-            ops.wgrad(dhb, rk, xb, kp, r, D, rp, dwd, D)
+            dwd = _wgrad(dhb, rk, xb, kp, r, D, rp, ctx.params[0], True, marks)
+        _sunk(marks)
         return dx, dwd, dwu, None
 
 
@@ -411,11 +413,36 @@ def _pad_bf16(x2, rows_p, cols_p):
     return out
 
 
-def _colsum(x, rows, cols, ld):
-    out = torch.empty(cols, device=x.device, dtype=F32)
+def _colsum(x, rows, cols, ld, p=None, need=True, marks=None):
+    """column sums of x (a bias gradient); with p: accumulated in place into p's flat .grad view when it has
+    one (vitmi.flat.grad_sink: p appended to marks, None returned)"""
     part = torch.empty(ops.colsum_partial_rows(max(rows, 1)), cols, device=x.device, dtype=F32)
+    sk = _flat.grad_sink(p, need) if p is not None else None
+    if sk is not None:
+        ops.colsum(x, rows, cols, ld, part, sk, accumulate=True)
+        marks.append(p)
+        return None
+    out = torch.empty(cols, device=x.device, dtype=F32)
     ops.colsum(x, rows, cols, ld, part, out)
     return out
+
+
+def _wgrad(A, lda, B, ldb, M, N, K, p=None, need=True, marks=None):
+    """weight gradient [M][N] = A^T B (ops.wgrad), accumulated into p's flat .grad view in place when it has one
+    (as _colsum); else a new f32 tensor. With the view, no AccumulateGrad add runs for p."""
+    sk = _flat.grad_sink(p, need) if p is not None else None
+    if sk is not None:
+        ops.wgrad(A, lda, B, ldb, M, N, K, sk, N, accumulate=True)
+        marks.append(p)
+        return None
+    out = torch.empty(M, N, device=A.device, dtype=F32)
+    ops.wgrad(A, lda, B, ldb, M, N, K, out, N)
+    return out
+
+
+def _sunk(marks):
+    for p in marks:
+        _flat.sunk(p)
 
 
 def _mlp_forward(xb, T, kp, w1, b1, w2, b2, w3, b3):
@@ -466,25 +493,26 @@ def _dgrad_f32(dyb, w, n_in, T):
     return dx
 
 
-def _mlp_backward(d2, T, xb, acts, w1, w2, w3, need_dx, out_du1=None):
+def _mlp_backward(d2, T, xb, acts, w1, w2, w3, need_dx, out_du1=None, params=None, need=None, marks=None):
     """gradients of _mlp_forward: (dX f32 [T][K1] or None, dW1, db1, dW2, db2, dW3, db3); out_du1: a list that
-    receives the first layer's bf16 dU (its input gradient is then left to the caller)"""
+    receives the first layer's bf16 dU (its input gradient is then left to the caller); params / need: the six
+    parameters and their needs_input_grad flags, whose gradients go to their flat .grad views where they have
+    them (None returned for those, appended to marks)"""
+    ps = params if params is not None else (None,) * 6
+    nd = need if need is not None else (True,) * 6
     g1, gp1, g2, gp2 = acts
     rp, kp, h1p, h2p = xb.shape[0], xb.shape[1], g1.shape[1], g2.shape[1]
     H1, H2, O, K1 = w1.shape[0], w2.shape[0], w3.shape[0], w1.shape[1]
     dev = d2.device
-    db3 = _colsum(d2, T, O, O)
+    db3 = _colsum(d2, T, O, O, ps[5], nd[5], marks)
     dlb = _pad_bf16(d2, rp, _rup(O, 64))
-    dw3 = torch.empty(O, H2, device=dev, dtype=F32)
-    ops.wgrad(dlb, dlb.shape[1], g2, h2p, O, H2, rp, dw3, H2)
+    dw3 = _wgrad(dlb, dlb.shape[1], g2, h2p, O, H2, rp, ps[4], nd[4], marks)
     du2 = _dgrad_mul(dlb, w3, H2, T, gp2, h2p)
-    db2 = _colsum(du2, T, H2, h2p)
-    dw2 = torch.empty(H2, H1, device=dev, dtype=F32)
-    ops.wgrad(du2, h2p, g1, h1p, H2, H1, rp, dw2, H1)
+    db2 = _colsum(du2, T, H2, h2p, ps[3], nd[3], marks)
+    dw2 = _wgrad(du2, h2p, g1, h1p, H2, H1, rp, ps[2], nd[2], marks)
     du1 = _dgrad_mul(du2, w2, H1, T, gp1, h1p)
-    db1 = _colsum(du1, T, H1, h1p)
-    dw1 = torch.empty(H1, K1, device=dev, dtype=F32)
-    ops.wgrad(du1, h1p, xb, kp, H1, K1, rp, dw1, K1)
+    db1 = _colsum(du1, T, H1, h1p, ps[1], nd[1], marks)
+    dw1 = _wgrad(du1, h1p, xb, kp, H1, K1, rp, ps[0], nd[0], marks)
     dx = _dgrad_f32(du1, w1, K1, T) if need_dx else None
     if out_du1 is not None:
         out_du1.append(du1)
@@ -509,6 +537,7 @@ class _RouterMLP(torch.autograd.Function):
         xb = _pad_bf16(x2, _rup(max(T, 1), 64), _rup(K1, 64))
         out, acts = _mlp_forward(xb, T, xb.shape[1], w1, b1, w2, b2, w3, b3)
         ctx.save_for_backward(xb, *acts, w1, w2, w3)
+        ctx.params = (w1, b1, w2, b2, w3, b3)
         ctx.dims = (lead, T, K1)
         return out.reshape(*lead, w3.shape[0])
 
@@ -517,7 +546,10 @@ class _RouterMLP(torch.autograd.Function):
         xb, g1, gp1, g2, gp2, w1, w2, w3 = ctx.saved_tensors
         lead, T, K1 = ctx.dims
         d2 = dout.contiguous().float().reshape(T, w3.shape[0])
-        dx, *grads = _mlp_backward(d2, T, xb, (g1, gp1, g2, gp2), w1, w2, w3, ctx.needs_input_grad[0])
+        marks = []
+        dx, *grads = _mlp_backward(d2, T, xb, (g1, gp1, g2, gp2), w1, w2, w3, ctx.needs_input_grad[0],
+                                   params=ctx.params, need=ctx.needs_input_grad[1:7], marks=marks)
+        _sunk(marks)
         return (dx.reshape(*lead, K1) if dx is not None else None, *grads)
 
 
@@ -557,6 +589,7 @@ class _RouterNet(torch.autograd.Function):
         xc[:, :, Hh:K1].copy_(glob.to(BF16)[:, None, :])
         out, acts = _mlp_forward(xcat, T, kp, w1, b1, w2, b2, w3, b3)
         ctx.save_for_backward(x2, mean, rstd, ln_w, lnb, gp0, xcat, *acts, w0, w1, w2, w3)
+        ctx.params = (w0, b0, w1, b1, w2, b2, w3, b3)
         ctx.dims = (B, N, D, T, Hh, K1, reserve)
         return out.view(B, N, w3.shape[0])
 
@@ -567,8 +600,9 @@ class _RouterNet(torch.autograd.Function):
         dev = dout.device
         rp, dp, h0p = xcat.shape[0], lnb.shape[1], gp0.shape[1]
         d2 = dout.contiguous().float().view(T, w3.shape[0])
-        du1l = []
-        _, *mlp_grads = _mlp_backward(d2, T, xcat, (g1, gp1, g2, gp2), w1, w2, w3, False, du1l)
+        du1l, marks, need = [], [], ctx.needs_input_grad
+        _, *mlp_grads = _mlp_backward(d2, T, xcat, (g1, gp1, g2, gp2), w1, w2, w3, False, du1l,
+                                      params=ctx.params[2:], need=need[5:11], marks=marks)
         du1 = du1l[0]
         H1 = w1.shape[0]
         # out_conv's input gradient, by halves: the x_embed half as one GEMM (dU1 W1[:, :h]); the global half
@@ -580,9 +614,8 @@ class _RouterNet(torch.autograd.Function):
         dxe[:, reserve:, :] += (torch.matmul(s1, w1r) / (N - reserve))[:, None, :]
         du0 = dxe.view(T, Hh) * gp0[:T, :Hh]
         du0b = _pad_bf16(du0, rp, h0p)
-        db0 = _colsum(du0b, T, Hh, h0p)
-        dw0 = torch.empty(Hh, D, device=dev, dtype=F32)
-        ops.wgrad(du0b, h0p, lnb, dp, Hh, D, rp, dw0, D)
+        db0 = _colsum(du0b, T, Hh, h0p, ctx.params[1], need[4], marks)
+        dw0 = _wgrad(du0b, h0p, lnb, dp, Hh, D, rp, ctx.params[0], need[3], marks)
         dln = _dgrad_f32(du0b, w0, D, T)
         dx = torch.empty(T, D, device=dev, dtype=F32)
         need_ln = ctx.needs_input_grad[1] or ctx.needs_input_grad[2]
@@ -593,6 +626,7 @@ class _RouterNet(torch.autograd.Function):
                               dgamma_dbeta=gb)
         dg = gb[:D].clone() if need_ln else None
         dbt = gb[D:].clone() if need_ln else None
+        _sunk(marks)
         return (dx.view(B, N, D), dg, dbt, dw0, db0, *mlp_grads, None, None)
 
 
