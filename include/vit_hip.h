@@ -37,6 +37,9 @@ enum vit_status {
 
 const char* vit_last_error(void);
 int vit_abi_version(void);
+/* Source fingerprint the library was built from (16 hex digits, vit-of-pytorch_amd/vitmi/buildid.py over
+ * Makefile, csrc/ and this header); the Python binding refuses a library whose id differs from its tree. */
+const char* vit_build_id(void);
 
 /* ------------------------------------------------------------------------------------------
  * bf16 MFMA GEMM with fused epilogues.

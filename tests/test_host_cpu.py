@@ -26,6 +26,46 @@ def test_library_exports_every_header_symbol():
     assert lib.vit_abi_version() == _lib.ABI_VERSION
 
 
+def test_library_build_id_matches_tree():
+    """The library was built from exactly these sources: load() re-derives the fingerprint of csrc/,
+    the Makefile and include/vit_hip.h and compares it with the stamped vit_build_id()."""
+    from vitmi import _lib, buildid
+    if not os.path.exists(_lib.LIB_PATH):
+        pytest.skip("libvit_hip.so not built (run __graft_entry__.build())")
+    lib = ctypes.CDLL(_lib.LIB_PATH)
+    lib.vit_build_id.restype = ctypes.c_char_p
+    assert lib.vit_build_id().decode() == buildid.tree_id()
+    _lib.check_build_id(lib, _lib.LIB_PATH)  # no raise
+    assert _lib.load() is not None
+
+
+def test_library_with_foreign_build_id_is_refused(tmp_path):
+    """A library whose stamp differs from the tree (built from older sources) raises VitHipError: both a
+    wrong expected id and a copy of the tree whose kernel source changed."""
+    import shutil
+
+    from vitmi import _lib, buildid
+    if not os.path.exists(_lib.LIB_PATH):
+        pytest.skip("libvit_hip.so not built (run __graft_entry__.build())")
+    lib = ctypes.CDLL(_lib.LIB_PATH)
+    lib.vit_build_id.restype = ctypes.c_char_p
+    with pytest.raises(_lib.VitHipError, match="built from other sources"):
+        _lib.check_build_id(lib, _lib.LIB_PATH, expected="0123456789abcdef")
+    # a tree that differs by one byte of one kernel source has another id
+    pkg = tmp_path / "vit-of-pytorch_amd"
+    shutil.copytree(os.path.join(buildid.PKG_ROOT, "csrc"), pkg / "csrc")
+    shutil.copy(os.path.join(buildid.PKG_ROOT, "Makefile"), pkg / "Makefile")
+    (tmp_path / "include").mkdir()
+    shutil.copy(HEADER, tmp_path / "include" / "vit_hip.h")
+    assert buildid.tree_id(str(pkg)) == buildid.tree_id()
+    with open(pkg / "csrc" / "gemm.hip", "a") as f:
+        f.write("\n// edited\n")
+    other = buildid.tree_id(str(pkg))
+    assert other != buildid.tree_id()
+    with pytest.raises(_lib.VitHipError):
+        _lib.check_build_id(lib, _lib.LIB_PATH, expected=other)
+
+
 def test_flat_layout_and_buckets():
     from vitmi.engine import ArchConfig, FlatLayout
     cfg = ArchConfig()

@@ -2,6 +2,8 @@
 #include <stdarg.h>
 
 #include "common.h"
+// VIT_BUILD_ID: the source fingerprint the Makefile generates (vitmi/buildid.py)
+#include "build_id.h"
 
 namespace vit {
 static thread_local char g_last_error[512] = "";
@@ -21,4 +23,5 @@ int check_hip(hipError_t e, const char* what) {
 }  // namespace vit
 
 extern "C" const char* vit_last_error(void) { return vit::g_last_error; }
-extern "C" int vit_abi_version(void) { return 8; }
+extern "C" int vit_abi_version(void) { return 9; }
+extern "C" const char* vit_build_id(void) { return VIT_BUILD_ID; }

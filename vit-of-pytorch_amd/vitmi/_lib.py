@@ -17,7 +17,7 @@ c_i32 = ctypes.c_int32
 c_f32 = ctypes.c_float
 c_vp = ctypes.c_void_p
 
-ABI_VERSION = 8  # vit_abi_version() of the library these prototypes describe
+ABI_VERSION = 9  # vit_abi_version() of the library these prototypes describe
 
 # enum vit_layout / vit_epilogue (include/vit_hip.h)
 K_CONTIG, MN_CONTIG = 0, 1
@@ -116,6 +116,7 @@ _SIGS = {
     "vit_copy2d": (c_i32, [c_vp, c_i64, c_vp, c_i64, c_i64, c_i64, c_vp]),
     "vit_rows_select": (c_i32, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_i64, c_vp]),
     "vit_sgd_step_dev": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_f32, c_vp]),
+    "vit_build_id": (ctypes.c_char_p, []),
 }
 
 EXPORTED = tuple(_SIGS)
@@ -143,8 +144,24 @@ def load(path: str | None = None):
     if lib.vit_abi_version() != ABI_VERSION:
         raise VitHipError(f"{p} has ABI {lib.vit_abi_version()}, the bindings expect {ABI_VERSION}: rebuild it "
                           "(make -C vit-of-pytorch_amd)")
+    check_build_id(lib, p)
     _lib = lib
     return lib
+
+
+def check_build_id(lib, path: str, expected: str | None = None):
+    """Refuse a library built from other sources than the tree beside this package (vitmi/buildid.py):
+    the stamped vit_build_id() must equal the fingerprint of csrc/, the Makefile and include/vit_hip.h
+    as they are now. (A package installed without its sources has nothing to compare against.)"""
+    from . import buildid
+    if expected is None:
+        if not buildid.have_sources():
+            return
+        expected = buildid.tree_id()
+    got = lib.vit_build_id().decode()
+    if got != expected:
+        raise VitHipError(f"{path} was built from other sources (build id {got}, this tree {expected}): rebuild it "
+                          "(make -C vit-of-pytorch_amd)")
 
 
 def check(status: int, what: str):
