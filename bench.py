@@ -107,7 +107,7 @@ def cpu_baseline(arch, image_size, num_classes, seconds_budget=20.0):
     cfg = ViTConfig(image_size=image_size, num_classes=num_classes, **arch)
     sched = OneCycle(0.03, 15000, 500 / 15000)
     rates = {}
-    for proto, bs in (("reference", 4), ("tamed", 8)):  # (CPU img/s is nearly batch-independent)
+    for proto, bs in (("reference", 16), ("tamed", 16)):  # the config batch or bs 16-32
         print(f"cpu_baseline: {proto} init, batch {bs}, {cores} threads", file=sys.stderr, flush=True)
         g = torch.Generator().manual_seed(0)
         x = torch.randn(bs, 3, image_size, image_size, generator=g)
@@ -131,7 +131,7 @@ def cpu_baseline(arch, image_size, num_classes, seconds_budget=20.0):
     return dict(value=round(r[0], 3), unit="images/sec", cores=cores, kind="port", cpu_model=_cpu_model(),
                 value_tamed_init=round(t[0], 3),
                 sample=f"oracle fp32 CPU train step (fwd+CE+bwd+SGD/OneCycleLR) on {cores} threads ({_cpu_model()}): "
-                       f"reference std-1 init, batch 4, {r[1]} steps in {r[2]:.1f} s; tamed init, batch 8, {t[1]} "
+                       f"reference std-1 init, batch 16, {r[1]} steps in {r[2]:.1f} s; tamed init, batch 16, {t[1]} "
                        f"steps in {t[2]:.1f} s; each after 1 warm-up step")
 
 
@@ -300,13 +300,35 @@ def main():
     barrier()
     probe, probe_w = probes
     eng.probe = eng.probe_wgrad = None
-    if world > 1:
-        import torch.distributed as dist
-        t = torch.tensor([dt], device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t)
-    fc1_ms = sum(s.elapsed_time(e) for s, e in probe) / max(1, len(probe))
+    # a second eager probe step: HIP events around every forward / data-gradient GEMM call over all T rows
+    # (the gemm_pp2 family and its wave-split remainder launches; kept apart from the probes above, whose
+    # events would otherwise land inside these)
     T = b * cfg.tokens
+    ops.GEMM_PROBE, ops.GEMM_PROBE_MIN_M = [], T
+    ops.copy2d(hyper, 12, hyper_all[total_steps - 1], 12, 12, 1)
+    step_body()
+    barrier()
+    probe_fd, ops.GEMM_PROBE = ops.GEMM_PROBE, None
+    dist_check = None
+    if world > 1:
+        dist_check = replica_check(eng.flat, dt, args.steps, world, backend, dev)
+        dt = dist_check.pop("_dt_max")
+    fc1_ms = sum(s.elapsed_time(e) for s, e in probe) / max(1, len(probe))
+    fd_ms = [s_.elapsed_time(e_) for s_, e_, _, _ in probe_fd]
+    fd_flop = sum(p_[2] for p_ in probe_fd)
+    fd_tflops = fd_flop / (sum(fd_ms) * 1e-3) / 1e12 if fd_ms else 0.0
+    epi_names = {1: "bf16 (dgrads)", 2: "bias bf16 (qkv fwd)", 4: "bias + f32 residual (fc2 / out-proj fwd)",
+                 6: "patch embed", 8: "bias + GELU + GELU' (fc1 fwd)", 9: "x GELU' (fc2 dgrad)"}
+    fd_by_epi = {}
+    for (s_, e_, fl, epi), ms in zip(probe_fd, fd_ms):
+        d_ = fd_by_epi.setdefault(epi_names.get(epi, f"epilogue {epi}"), {"launches": 0, "ms": 0.0, "gflop": 0.0})
+        d_["launches"] += 1
+        d_["ms"] += ms
+        d_["gflop"] += fl / 1e9
+    for d_ in fd_by_epi.values():
+        d_["frac"] = round(d_["gflop"] / d_["ms"] / PEAK_BF16_TFLOPS, 4) if d_["ms"] else None
+        d_["ms"] = round(d_["ms"], 4)
+        d_["gflop"] = round(d_["gflop"], 2)
     fc1_flop = 2.0 * T * cfg.emb_dim * cfg.mlp_dim
     fc1_tflops = fc1_flop / (fc1_ms * 1e-3) / 1e12
     # the step's dominant kernel by time: the split-K weight-gradient GEMM (gemm_pp_kernel; ~22% of the
@@ -375,11 +397,21 @@ def main():
                      "traffic_detail": traffic,
                      "algorithmic_bytes": T * cfg.emb_dim * 2 + cfg.mlp_dim * cfg.emb_dim * 2 + 2 * T * cfg.mlp_dim * 2,
                      "avg_launch_ms": round(fc1_ms, 4), "launches": len(probe)},
+        "roofline_fwd_dgrad": {"bound": "mfma", "kernel": "every forward and data-gradient GEMM call over all "
+                                                      f"{T} token rows of one step (gemm_pp2_kernel family + the "
+                                                      "wave-split 128x128 remainder launches; HIP events around each "
+                                                      "vit_gemm_bf16 call, a separate eager probe step)",
+                               "achieved": round(fd_tflops, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+                               "frac": round(fd_tflops / PEAK_BF16_TFLOPS, 4), "traffic": None,
+                               "calls": len(fd_ms), "total_ms": round(sum(fd_ms), 4),
+                               "gflop_per_step": round(fd_flop / 1e9, 2), "by_epilogue": fd_by_epi},
         "step_mfma_frac": round(value / world * fpe / 1e12 / PEAK_BF16_TFLOPS, 4),
         "step_mfma_frac_algorithmic": round(step_tflops_per_gpu / PEAK_BF16_TFLOPS, 4),
         "train_gflop_per_image": round(fpi / 1e9, 3),
         "executed_gflop_per_image": round(fpe / 1e9, 3),
     }
+    if dist_check is not None:
+        out["dist_check"] = dist_check
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(arch, args.image_size, args.num_classes, args.cpu_seconds)
     if rank == 0:
@@ -387,6 +419,38 @@ def main():
     if world > 1:
         import torch.distributed as dist
         dist.destroy_process_group()
+        if not dist_check["replicas_identical"]:
+            print("error: the data-parallel replicas' parameters differ after the run", file=sys.stderr)
+            sys.exit(3)
+
+
+def replica_hash(flat):
+    """[2] int64 fingerprint of a flat f32 parameter buffer: the wrapped sum of its 32-bit patterns and a
+    position-weighted wrapped sum (equal buffers give equal hashes, bit for bit; a permutation or any
+    changed bit changes them)."""
+    bits = flat.detach().reshape(-1).view(torch.int32).to(torch.int64)
+    w = torch.arange(bits.numel(), device=bits.device, dtype=torch.int64) % 65521 + 1
+    return torch.stack([bits.sum(), (bits * w).sum()])
+
+
+def replica_check(flat, dt, steps, world, backend, dev):
+    """After the timed run of an N-rank job: every rank's wall time (max = the job's), and an all-gather of
+    replica_hash(flat) — data-parallel replicas must stay bit-identical (reference
+    src/train.py:128-129 keeps one model)."""
+    import torch.distributed as dist
+    t = torch.tensor([dt], device=dev, dtype=torch.float64)
+    ts = [torch.zeros_like(t) for _ in range(world)]
+    dist.all_gather(ts, t)
+    h = replica_hash(flat)
+    hs = [torch.zeros_like(h) for _ in range(world)]
+    dist.all_gather(hs, h)
+    per = [float(x) / steps * 1e3 for x in ts]
+    same = all(torch.equal(hs[0], x) for x in hs)
+    return {"ranks_seen": dist.get_world_size(), "backend": backend,
+            "ms_per_step_per_rank": [round(x, 3) for x in per],
+            "ms_per_step_spread_pct": round((max(per) - min(per)) / min(per) * 100, 2),
+            "replicas_identical": same, "param_hash_rank0": [int(x) for x in hs[0].tolist()],
+            "_dt_max": max(float(x) for x in ts)}
 
 
 def resvit_flops_per_image(a, image_size, block_heads, active_ratio):
@@ -479,11 +543,10 @@ def bench_resvit(args, world, rank, dev, backend, comm):
         step()
     barrier()
     dt = time.perf_counter() - t0
-    if world > 1:
-        import torch.distributed as dist
-        t = torch.tensor([dt], device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t)
+    dist_check = None
+    if world > 1:  # the trainable flat buffer (LoRA, routers, approximators, head): the frozen bases never change
+        dist_check = replica_check(opt.flat.data, dt, args.steps, world, backend, dev)
+        dt = dist_check.pop("_dt_max")
     active = float(torch.stack(ratios[-args.steps:]).mean())
     value = args.steps * b * world / dt
     heads = sum(1 for l in model.layers if hasattr(l, "router"))
@@ -507,11 +570,16 @@ def bench_resvit(args, world, rank, dev, backend, comm):
         "executed_gflop_per_image": round(fpi / 1e9, 3),
         "active_ratio": round(active, 4),
     }
+    if dist_check is not None:
+        out["dist_check"] = dist_check
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
         import torch.distributed as dist
         dist.destroy_process_group()
+        if not dist_check["replicas_identical"]:
+            print("error: the data-parallel replicas' parameters differ after the run", file=sys.stderr)
+            sys.exit(3)
 
 
 if __name__ == "__main__":

@@ -81,3 +81,40 @@ def test_grad_allreduce_gloo_world2(average, compress):
     for r in range(world):
         assert torch.allclose(res[r], expect), r
     assert torch.equal(res[0], res[1])  # replicas bit-identical
+
+
+def _replica_worker(rank, world, port, differ, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import bench
+    flat = torch.linspace(-3, 3, 10007)
+    if differ and rank == 1:
+        flat[5000] = torch.nextafter(flat[5000], torch.tensor(10.0))  # one ulp on one element
+    out = bench.replica_check(flat, 1.0 + 0.5 * rank, 10, world, "gloo", torch.device("cpu"))
+    q.put((rank, out))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("differ", [False, True])
+def test_bench_replica_check_gloo(differ):
+    """bench.py's N > 1 self-check (2 gloo ranks on the CPU): every rank's time is gathered (the job's time is
+    the max), and the flat-parameter fingerprints agree iff the replicas are bit-identical — a one-ulp
+    difference on one element of one rank is caught."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_replica_worker, args=(r, 2, port, differ, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in (0, 1):
+        o = res[r]
+        assert o["ranks_seen"] == 2 and o["backend"] == "gloo"
+        assert o["_dt_max"] == 1.5
+        assert o["ms_per_step_per_rank"] == [100.0, 150.0]
+        assert o["replicas_identical"] is (not differ)

@@ -176,13 +176,9 @@ def test_graphed_step_matches_eager_and_reference(gold, fused, warmup):
         x = torch.from_numpy(gold["s0/x"]).cuda()
         y = torch.from_numpy(gold["s0/y"]).cuda()
         # warmup=0: the eager run before it created the device constants (no pageable copy under capture);
-        # warmup=1: one eager step on batch 0 inside the constructor (the eager run takes the same step first)
-        if graphed:
-            g = GraphedTrainStep(m, x, y, opt, sched, h["la"], h["ld"], h["lc"], True, warmup=warmup)
-        else:
-            g = None
-            for _ in range(warmup):
-                train_step(m, x, y, opt, sched, h["la"], h["ld"], h["lc"], clip_grad_norm=True)
+        # warmup=1: one forward + backward on batch 0 inside the constructor, which leaves the parameters, the
+        # optimizer and the schedule untouched (the eager run takes no extra step)
+        g = GraphedTrainStep(m, x, y, opt, sched, h["la"], h["ld"], h["lc"], True, warmup=warmup) if graphed else None
         losses = []
         for s in range(3):
             for j in range(len(routers)):
@@ -193,8 +189,7 @@ def test_graphed_step_matches_eager_and_reference(gold, fused, warmup):
             out = (g.step(x, y) if graphed else
                    train_step(m, x, y, opt, sched, h["la"], h["ld"], h["lc"], clip_grad_norm=True))
             losses.append(torch.stack([out[0], out[1], out[3]]).detach().clone())
-            if warmup == 0:
-                assert abs(float(out[1]) - float(gold[f"s{s}/c_loss"])) <= 1e-3 * float(gold[f"s{s}/c_loss"]), s
+            assert abs(float(out[1]) - float(gold[f"s{s}/c_loss"])) <= 1e-3 * float(gold[f"s{s}/c_loss"]), s
         runs.append((torch.stack(losses), [p.detach().clone() for p in opt.flat.params], opt.flat.used.clone()))
     (le, pe, ue), (lg, pg, ug) = runs
     assert torch.isfinite(le).all() and le[0, 0] != le[2, 0]  # the graph's gradients reach the parameters
@@ -545,3 +540,72 @@ def test_fused_router_net_matches_per_op_path(B, N, hdim, reserve):
         e = rel(a, b)
         print(f"{n}: {e:.2e}")
         assert e < tol.get(n, 6e-2), (n, e)
+
+
+def test_fused_layer_refuses_backward_after_shared_operand_rewrite(gold):
+    """The fused layer's LN1 | u operand and LoRA pack are per-block buffers shared by the block's forwards
+    (SHARE_PACK): a backward whose forward's buffers were rewritten by a later grad-enabled forward of the same
+    block raises instead of computing the LoRA gradients from the wrong activations; forward -> backward
+    alternation (the training steps) is accepted."""
+    from vitmi import resvit_fused
+    m = build(gold).train()
+    blk = m.layers[0]
+    g = torch.Generator(device="cuda").manual_seed(2)
+    x = torch.randn(2, 17, TINY["dim"], device="cuda", generator=g, requires_grad=True)
+    resvit_fused.full_layer(blk, x).square().sum().backward()  # one forward, its backward: fine
+    y1 = resvit_fused.full_layer(blk, x)
+    y2 = resvit_fused.full_layer(blk, x)
+    with pytest.raises(RuntimeError, match="another forward"):
+        (y1.square().sum() + y2.square().sum()).backward()
+
+
+def test_grad_sinks_only_inside_training_backward(gold):
+    """vitmi.flat.grad_sink answers only inside flat.sinks() (train_step / GraphedTrainStep wrap their backward
+    in it): a plain torch.autograd.grad over the router parameters of a FlatParams-managed model returns their
+    gradients (none is None) and leaves .grad untouched."""
+    from vitmi.optim import AdamW
+    m = build(gold).train()
+    opt = AdamW(m.parameters(), lr=1e-4, weight_decay=0.05, max_grad_norm=1.0)
+    opt.zero_grad()
+    routers = [l.router for l in m.layers if hasattr(l, "router")]
+    params = [p for r in routers for p in r.parameters() if p.requires_grad]
+    x = torch.from_numpy(gold["s0/x"]).cuda()
+    y = torch.from_numpy(gold["s0/y"]).cuda()
+    c_loss, a_loss, d_loss, _, _ = m(x, y)
+    grads = torch.autograd.grad(c_loss + a_loss + d_loss, params, allow_unused=True)
+    assert any(gr is not None for gr in grads)
+    assert all(gr is None or torch.isfinite(gr).all() for gr in grads)
+    assert float(opt.flat.grad.abs().sum()) == 0.0  # nothing was sunk into the flat gradient
+
+
+def test_zero_grad_clears_stale_gates():
+    """flat.gate ORs a forward's participation flag into an existing entry; FlatParams.zero_grad drops the
+    entries of its parameters, so a flag left by a forward no step consumed cannot mark the next step used."""
+    from vitmi.flat import FlatParams, _GATES, _take_gate, gate
+    p = torch.nn.Parameter(torch.zeros(4, device="cuda"))
+    f = FlatParams([p])
+    gate([p], torch.tensor(True, device="cuda"))  # a train-mode forward whose step was skipped
+    f.zero_grad()
+    assert id(p) not in _GATES
+    gate([p], torch.tensor(False, device="cuda"))  # the next step's forward routed no rows to p
+    assert not bool(_take_gate(p))
+
+
+def test_graphed_step_construction_leaves_state_untouched(gold):
+    """GraphedTrainStep(warmup=1) runs its warm-up forward + backward without an optimizer or scheduler step
+    (its Gumbel draws are taken from restored RNG states): parameters, the learning rate and the flat gradient are
+    as before."""
+    from vitmi.optim import AdamW, get_cosine_schedule_with_warmup
+    from vitmi.resvit_train import GraphedTrainStep
+    h = hp(gold)
+    m = build(gold).train()
+    opt = AdamW(m.parameters(), lr=h["lr"], weight_decay=h["wd"], betas=h["betas"], eps=h["eps"], max_grad_norm=1.0)
+    sched = get_cosine_schedule_with_warmup(opt, h["warmup"], h["total"])
+    p0 = opt.flat.data.clone()
+    lr0 = opt.param_groups[0]["lr"]
+    x = torch.from_numpy(gold["s0/x"]).cuda()
+    y = torch.from_numpy(gold["s0/y"]).cuda()
+    GraphedTrainStep(m, x, y, opt, sched, h["la"], h["ld"], h["lc"], True, warmup=1)
+    assert torch.equal(opt.flat.data, p0)
+    assert opt.param_groups[0]["lr"] == lr0
+    assert float(opt.flat.grad.abs().sum()) == 0.0

@@ -18,6 +18,7 @@ None, then a fresh tensor from autograd) is folded back into the flat buffer by 
 """
 from __future__ import annotations
 
+import contextlib
 import math
 import weakref
 
@@ -54,13 +55,29 @@ def _take_gate(p):
 # A/B switch (bench.py VITMI_RESVIT_NO_SINK=1): False leaves every gradient to autograd's AccumulateGrad (one add
 # into the flat view per parameter and step)
 SINKS = True
+# grad_sink answers only inside `sinks()`: the training steps (resvit_train.train_step, GraphedTrainStep) wrap their
+# `total.backward()` in it. Elsewhere (torch.autograd.grad(loss, params), backward(inputs=[...]), any plain
+# backward) every fused node returns its parameter gradients to autograd as usual. A module-level count, not a
+# thread-local: autograd runs the CUDA nodes on its device threads while the caller waits in backward().
+_SINK_DEPTH = 0
+
+
+@contextlib.contextmanager
+def sinks():
+    """enable the in-place gradient sinks of the fused Res-ViT nodes for the backward run inside"""
+    global _SINK_DEPTH
+    _SINK_DEPTH += 1
+    try:
+        yield
+    finally:
+        _SINK_DEPTH -= 1
 
 
 def grad_sink(p, need=True):
     """the gradient view a backward node may accumulate p's gradient into in place (returning None for p), or
-    None: p is not held by a live FlatParams, its .grad is no longer the flat view, or the backward records a
-    graph (create_graph)"""
-    if not (SINKS and need) or torch.is_grad_enabled():
+    None: outside a `sinks()` block, p is not held by a live FlatParams, its .grad is no longer the flat view, or
+    the backward records a graph (create_graph)"""
+    if not (SINKS and need and _SINK_DEPTH > 0) or torch.is_grad_enabled():
         return None
     e = getattr(p, "_vitmi_flat", None)
     f = e[0]() if e is not None else None
@@ -174,6 +191,13 @@ class FlatParams:
         ops.zero_(self.grad)
         self.used_host = [False] * self.nseg
         self.used_reduced = False
+        # gate() ORs a forward's flag into an existing entry (several forwards before one step): entries left by a
+        # forward that no step consumed (a skipped step, a metrics-only train-mode forward) must not leak into
+        # the next zero_grad .. step window
+        for p in self.params:
+            e = _GATES.get(id(p))
+            if e is not None and e[0]() is p:
+                del _GATES[id(p)]
 
     def upload_used(self):
         """the host flags -> self.used (device f32), ordered on the current stream (unless a data-parallel

@@ -75,12 +75,27 @@ def dropout_mask(d, row0, rows, cols, out, ld):
     check(lib().vit_dropout_mask(_dp(d), row0, rows, cols, _p(out), ld, _stream()), "vit_dropout_mask")
 
 
+# bench.py's roofline_fwd_dgrad probe: when a list, every vit_gemm_bf16 call with M >= GEMM_PROBE_MIN_M
+# that is not a split-K weight gradient appends (start event, end event, 2 M N K, epilogue), the events recorded
+# on the stream the call runs on (one call = the 256x256 kernel and its wave-split remainder launch)
+GEMM_PROBE = None
+GEMM_PROBE_MIN_M = 0
+
+
 def gemm(A, B, C, M, N, K, **kw):
     """bf16 MFMA GEMM, C[m,n] = sum_k A(m,k) B(k,n) + fused epilogue (see vit_gemm_args)."""
     _chk(A, BF16, "A")
     _chk(B, BF16, "B")
     a = _gemm_args(A, B, C, M, N, K, **kw)
+    probe = GEMM_PROBE is not None and M >= GEMM_PROBE_MIN_M and a.split_k == 1 and a.epilogue != _lib.EPI_SPLITK
+    if probe:
+        ev0 = torch.cuda.Event(enable_timing=True)
+        ev0.record()
     check(lib().vit_gemm_bf16(ctypes.byref(a), _stream()), "vit_gemm_bf16")
+    if probe:
+        ev1 = torch.cuda.Event(enable_timing=True)
+        ev1.record()
+        GEMM_PROBE.append((ev0, ev1, 2.0 * M * N * K * a.batch, int(a.epilogue)))
 
 
 def gemm_tile_rows(A, B, C, M, N, K, **kw):

@@ -103,6 +103,9 @@ class _Frozen:
         self.a_all = None
         self.a1 = None
         self.a1_rows = 0
+        # bumped on every rewrite of the shared a_all / a1 buffers (raw-pointer kernels: torch's version counter
+        # does not see them); a backward checks that its forward's buffers were not rewritten since
+        self.gen = 0
 
     def pack_lora(self, aq, bq, ak, bk, av, bv):
         """A_all [64][D] (row z*r8 + i = A_z[i], other rows zero) and B_z into columns D + z*r8 of wcat"""
@@ -115,6 +118,7 @@ class _Frozen:
             ops.cast_pad_rows(A.detach().float().contiguous(), r, D, self.a_all[z * r8:], D)
         for z, Bz in enumerate((bq, bk, bv)):
             ops.pack_cols(Bz.detach().float().contiguous(), 0, r, D, r, 1, self.wcat[z * D:, D + z * r8:], Kq)
+        self.gen += 1
         return self.a_all
 
     def operand(self, T, Tp, Kq, dev):
@@ -124,6 +128,7 @@ class _Frozen:
         elif T != self.a1_rows and Tp > T:
             ops.zero_(self.a1[T:])  # rows past T (read by the split-K LoRA gradients) back to zero
         self.a1_rows = T
+        self.gen += 1
         return self.a1
 
     def get(self, block):
@@ -224,6 +229,7 @@ class _FusedLayer(torch.autograd.Function):
             ctx.save_for_backward(xf, a1, mu1, rs1, qkv, o, lse, h, mu2, rs2, gp, a_all, bq, bk, bv)
             ctx.block = block
             ctx.dims = (B, N, D, H, hd, M, r, r8, T, Tp, scale)
+            ctx.gen = fz.gen if SHARE_PACK else None
         return out.view(B, N, D)
 
     @staticmethod
@@ -231,6 +237,14 @@ class _FusedLayer(torch.autograd.Function):
         xf, a1, mu1, rs1, qkv, o, lse, h, mu2, rs2, gp, a_all, bq, bk, bv = ctx.saved_tensors
         block = ctx.block
         fz = block._vitmi_frozen.get(block)
+        if ctx.gen is not None and fz.gen != ctx.gen:
+            # a1 (LN1 | u) and a_all are per-block buffers shared by the block's forwards (SHARE_PACK); another
+            # forward of this block rewrote them after the one this backward belongs to, so the LoRA gradients
+            # would silently use its activations
+            raise RuntimeError("Res-ViT fused layer: this block ran another forward after the one being "
+                               "back-propagated (micro-batch accumulation / retain_graph reuse); its shared LN1 | u "
+                               "operand was overwritten. Run backward before the next forward of the block, or set "
+                               "vitmi.resvit_fused.SHARE_PACK = False")
         B, N, D, H, hd, M, r, r8, T, Tp, scale = ctx.dims
         Kq = D + KX
         dev = xf.device

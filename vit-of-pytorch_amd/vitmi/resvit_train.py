@@ -27,6 +27,7 @@ import torch.distributed as dist
 from . import resvit
 from .optim import AdamW, clip_grad_norm_, get_cosine_schedule_with_warmup
 from .config import process_config
+from .flat import sinks as _flat_sinks
 from .train import MetricTracker, StepWriter, SyntheticDataLoader, _rank_mean, rank_batch, set_seed
 
 METRICS = ["loss", "c_loss", "a_loss", "d_loss", "router_entropy", "acc1", "acc5", "active_ratio", "lr",
@@ -55,7 +56,8 @@ def train_step(model, x, y, optimizer, lr_scheduler=None, lambda_active=10.0, la
     optimizer.zero_grad()
     c_loss, a_loss, d_loss, r_entropy, active_metric = model(x, y)
     total = total_loss(model, c_loss, a_loss, d_loss, lambda_active, lambda_distill, lambda_class)
-    total.backward()
+    with _flat_sinks():
+        total.backward()
     if reducer is not None:
         reducer.finish()
     if clip_grad_norm:
@@ -83,7 +85,13 @@ class GraphedTrainStep:
     train_step does; its inputs are the static `x` / `y` buffers (copy a new batch in with `step(x, y)`)
     and its outputs are static tensors overwritten by every replay.
 
-    Single process (no gradient all-reduce hooks: a data-parallel step stays on train_step).
+    Single process (no gradient all-reduce hooks: a data-parallel step stays on train_step); raises when a
+    torch.distributed group of more than one rank is initialised.
+
+    Construction runs `warmup` forward + backward passes on `x` / `y` (no optimizer or scheduler step; the
+    gradients are zeroed after them, and the torch CPU / CUDA RNG states are restored, so the Gumbel draws
+    of the warm-up do not shift the run's random stream): the model's parameters, the optimizer's moments
+    and the learning-rate schedule are exactly as they were before the constructor.
     """
 
     def __init__(self, model, x, y, optimizer, lr_scheduler=None, lambda_active=10.0, lambda_distill=1.0,
@@ -91,6 +99,9 @@ class GraphedTrainStep:
         from . import flat as _flat
         if not isinstance(optimizer, AdamW):
             raise TypeError("GraphedTrainStep: vitmi.optim.AdamW (flat gradients at fixed addresses) expected")
+        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+            raise RuntimeError("GraphedTrainStep is single-process: a data-parallel step (gradient all-reduce "
+                               "hooks in the backward) runs train_step with a FlatGradAllReducer")
         self.model, self.opt, self.sched = model, optimizer, lr_scheduler
         self.lambdas = (lambda_active, lambda_distill, lambda_class)
         self.clip = clip_grad_norm
@@ -102,17 +113,26 @@ class GraphedTrainStep:
         # through `model.logits`; on any other stream the accumulation would escape the capture
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
+        rng = (torch.get_rng_state(), torch.cuda.get_rng_state())
         with torch.cuda.stream(s):
-            for _ in range(warmup):
-                train_step(model, self.x, self.y, optimizer, lr_scheduler, *self.lambdas, clip_grad_norm)
+            for _ in range(warmup):  # forward + backward only: no parameter, moment or schedule changes
+                optimizer.zero_grad()
+                c_loss, a_loss, d_loss, r_entropy, active_metric = model(self.x, self.y)
+                total = total_loss(model, c_loss, a_loss, d_loss, *self.lambdas)
+                with _flat.sinks():
+                    total.backward()
             optimizer.zero_grad()
         torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
+        torch.set_rng_state(rng[0])
+        torch.cuda.set_rng_state(rng[1])
         f = optimizer.flat
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph, stream=s):
             c_loss, a_loss, d_loss, r_entropy, active_metric = model(self.x, self.y)
             total = total_loss(model, c_loss, a_loss, d_loss, *self.lambdas)
-            total.backward()
+            with _flat.sinks():
+                total.backward()
         self.outputs = (total, c_loss, a_loss, d_loss, r_entropy, active_metric)
         # what the captured pass left on the host: the used flags (post-accumulate hooks) and the gated
         # parameters' device flags (graph outputs, refreshed by every replay)
