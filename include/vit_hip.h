@@ -117,7 +117,7 @@ typedef struct vit_gemm_args {
   int64_t tokens;  /* VIT_EPI_PATCH: tokens per image */
   float* col_partial; /* optional (batch 1, split_k 1): col_partial[tile_m * N + n] = sum over the
                          tile's rows of the epilogue's output (bias-gradient partials); reduce the
-                         ceil(M / tile_rows) rows with vit_colsum. tile_rows: vit_gemm_tile_rows() */
+                         vit_gemm_partial_rows() rows with vit_colsum */
   int32_t epilogue;
   int32_t tile;    /* 0 = auto */
   const vit_dropout* dropout; /* optional, on the epilogue's output (row m, col n):
@@ -127,8 +127,11 @@ typedef struct vit_gemm_args {
 } vit_gemm_args;
 
 int vit_gemm_bf16(const vit_gemm_args* args, vit_stream_t stream);
-/* rows of C covered by one workgroup tile for these arguments (sizing of col_partial) */
+/* rows of C covered by one workgroup tile for these arguments */
 int64_t vit_gemm_tile_rows(const vit_gemm_args* args);
+/* rows of col_partial a call with these arguments writes (the rows to reduce with vit_colsum): one per
+ * 256-row tile of the whole-wave part and one per 128-row tile of a wave-split remainder */
+int64_t vit_gemm_partial_rows(const vit_gemm_args* args);
 
 /* out[z*out_batch_stride + m*ldo + n] (+)= sum_s ws[((z*split + s)*M + m)*N + n]  (f32) */
 int vit_splitk_reduce(const float* ws, int64_t batch, int64_t split, int64_t M, int64_t N,

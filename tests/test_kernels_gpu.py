@@ -88,6 +88,28 @@ def test_gemm_col_partial(tile):
     assert rel(C.float(), gref) < 5e-3
 
 
+def test_gemm_col_partial_wave_split():
+    """The production dispatch of a col_partial GEMM whose last wave of 256 x 256 tiles would run nearly empty
+    (20 x 13 = 260 tiles on 256 CUs): the whole-wave rows on the ping-pong kernel, the remaining 256 rows on two
+    128-row tiles, their column partials continuing after the main ones (vit_gemm_partial_rows rows); the
+    fc2-dgrad x GELU' shape family (EPI_MUL_BF16, both operands K-contiguous)."""
+    from vitmi._lib import EPI_MUL_BF16
+    M, N, K = 5120, 3328, 128
+    A, B, Am, Bm, lda, ldb = _mats(M, N, K, K_CONTIG, K_CONTIG)
+    U = torch.randn(M, N, device=DEV).bfloat16()
+    C = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    kw = dict(a_layout=K_CONTIG, b_layout=K_CONTIG, lda=lda, ldb=ldb, ldc=N, epilogue=EPI_MUL_BF16, aux=U, ldaux=N)
+    rows = ops.gemm_partial_rows(Am, Bm, C, M, N, K, **kw)
+    assert rows == 19 + 2  # 19 whole-wave 256-row tiles, then 2 remainder 128-row tiles
+    part = torch.full((rows + 1, N), float("nan"), device=DEV)
+    ops.gemm(Am, Bm, C, M, N, K, col_partial=part, **kw)
+    assert torch.isnan(part[rows]).all()  # nothing past the reported rows
+    ref = (A.float() @ B.float()) * U.float()
+    assert rel(C.float(), ref) < 5e-3
+    assert rel(part[:rows].sum(0), ref.sum(0)) < 1e-4  # the partials sum the f32 values before bf16 rounding
+    assert rel(part[19:rows].sum(0), ref[19 * 256:].sum(0)) < 1e-4
+
+
 @pytest.mark.parametrize("tile", [1, 2, 6, 9])
 def test_gemm_tiles_epilogue_splitk(tile):
     M, N, K = 700, 520, 512

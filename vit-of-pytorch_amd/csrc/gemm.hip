@@ -55,14 +55,58 @@ int pick_tile(const vit_gemm_args* a) {
   return 0;
 }
 
+int tile_rows_of(int cfg) {
+  switch (cfg) {
+    case 1: case 2: case 3: case 5: case 6: case 7: case 8: case 9: return 256;
+    default: return 128;
+  }
+}
+
+// Wave quantisation of the one-workgroup-per-CU 256 x 256 kernels: when the last wave of tiles would run less
+// than half full (M = 50 432, N = 768: 591 tiles = 2.3 waves on 256 CUs), the rows that fill whole waves run
+// on them and the remaining rows on 128 x 128 tiles (several workgroups per CU), ~2.4 instead of 3 wave-times.
+// Row-local epilogues only; per-tile column partials (col_partial) continue after the whole-wave tiles' rows,
+// one row per 128-row tile of the remainder. Returns the rows of the whole-wave part, 0 for one launch.
+long wave_split_rows(const vit_gemm_args* a, int cfg) {
+  if (!((cfg == 5 || cfg == 9) && a->batch == 1 && a->split_k == 1 && a->epilogue != VIT_EPI_PATCH && a->tile == 0))
+    return 0;
+  static const int ncu = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                               hipSuccess)
+      return 0;
+    return n;
+  }();
+  if (ncu <= 0) return 0;
+  const long tiles_n = (a->N + 255) / 256, tiles = ((a->M + 255) / 256) * tiles_n;
+  const long full = tiles / ncu, rem = tiles - full * ncu;
+  const long main_rows = (full * ncu / tiles_n) * 256;
+  return full >= 1 && rem > 0 && 2 * rem <= ncu && main_rows > 0 && main_rows < a->M ? main_rows : 0;
+}
+
+// tile config of the wave-split remainder launch (128 x 128; VIT_GEMM_REM_CFG in diagnostic builds)
+int rem_config() {
+  static const int rem_cfg = vit::knob("VIT_GEMM_REM_CFG", 0);
+  return rem_cfg >= 0 && rem_cfg <= 9 && rem_cfg != 1 ? rem_cfg : 0;
+}
+
 }  // namespace
 
 extern "C" int64_t vit_gemm_tile_rows(const vit_gemm_args* a) {
   if (!a) return 0;
-  switch (pick_tile(a)) {
-    case 1: case 2: case 3: case 5: case 6: case 7: case 8: case 9: return 256;
-    default: return 128;
+  return tile_rows_of(pick_tile(a));
+}
+
+extern "C" int64_t vit_gemm_partial_rows(const vit_gemm_args* a) {
+  if (!a) return 0;
+  const int cfg = pick_tile(a);
+  const long main_rows = wave_split_rows(a, cfg);
+  if (main_rows > 0) {
+    const long rr = tile_rows_of(rem_config());
+    return main_rows / 256 + (a->M - main_rows + rr - 1) / rr;
   }
+  const long tr = tile_rows_of(cfg);
+  return (a->M + tr - 1) / tr;
 }
 
 extern "C" int vit_gemm_bf16(const vit_gemm_args* a, vit_stream_t stream) {
@@ -179,42 +223,24 @@ extern "C" int vit_gemm_bf16(const vit_gemm_args* a, vit_stream_t stream) {
     vit::set_error("vit_gemm_bf16: unknown epilogue %d", a->epilogue);
     return VIT_ERR_INVALID_ARG;
   }
-  // Wave quantisation of the one-workgroup-per-CU 256 x 256 kernels: when the last wave of tiles
-  // would run less than half full (M = 50 432, N = 768: 591 tiles = 2.3 waves on 256 CUs), the
-  // rows that fill whole waves run on them and the remaining rows on 128 x 128 tiles (several
-  // workgroups per CU), ~2.4 instead of 3 wave-times. Row-local epilogues only.
-  if ((cfg == 5 || cfg == 9) && batch == 1 && split == 1 && !a->col_partial && a->epilogue != VIT_EPI_PATCH &&
-      a->tile == 0) {
-    static const int ncu = [] {
-      int dev = 0, n = 0;
-      if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) !=
-                                                 hipSuccess)
-        return 0;
-      return n;
-    }();
-    const long tiles_n = (a->N + 255) / 256, tiles = ((a->M + 255) / 256) * tiles_n;
-    if (ncu > 0) {
-      const long full = tiles / ncu, rem = tiles - full * ncu;
-      const long main_rows = (full * ncu / tiles_n) * 256;
-      if (full >= 1 && rem > 0 && 2 * rem <= ncu && main_rows > 0 && main_rows < a->M) {
-        GemmDev g1 = d, g2 = d;
-        g1.M = (int)main_rows;
-        g2.M = (int)(a->M - main_rows);
-        const long r0 = main_rows;
-        const long a_off = ak ? r0 * a->lda * 2 : r0 * 2;
-        g2.A = d.A + a_off;
-        g2.a_bytes = d.a_bytes > a_off ? (uint32_t)(d.a_bytes - a_off) : 0u;
-        const int csz = (a->epilogue == VIT_EPI_F32 || a->epilogue == VIT_EPI_BIAS_RESID_F32) ? 4 : 2;
-        g2.C = (char*)d.C + r0 * a->ldc * csz;
-        if (d.C2) g2.C2 = (char*)d.C2 + r0 * a->ldc2 * 2;
-        if (d.aux) g2.aux = (const char*)d.aux + r0 * a->ldaux * (a->epilogue == VIT_EPI_BIAS_RESID_F32 ? 4 : 2);
-        g2.drop.row0 = (int)r0;  // dropout masks are indexed by the absolute row
-        hipError_t e = run(cfg, g1);
-        static const int rem_cfg = vit::knob("VIT_GEMM_REM_CFG", 0);
-        if (e == hipSuccess) e = run(rem_cfg >= 0 && rem_cfg <= 9 && rem_cfg != 1 ? rem_cfg : 0, g2);
-        return vit::check_hip(e, "vit_gemm_bf16 launch");
-      }
-    }
+  // wave quantisation: whole-wave rows on the 256 x 256 kernel, the remainder on 128 x 128 tiles
+  if (const long main_rows = wave_split_rows(a, cfg)) {
+    GemmDev g1 = d, g2 = d;
+    g1.M = (int)main_rows;
+    g2.M = (int)(a->M - main_rows);
+    const long r0 = main_rows;
+    const long a_off = ak ? r0 * a->lda * 2 : r0 * 2;
+    g2.A = d.A + a_off;
+    g2.a_bytes = d.a_bytes > a_off ? (uint32_t)(d.a_bytes - a_off) : 0u;
+    const int csz = (a->epilogue == VIT_EPI_F32 || a->epilogue == VIT_EPI_BIAS_RESID_F32) ? 4 : 2;
+    g2.C = (char*)d.C + r0 * a->ldc * csz;
+    if (d.C2) g2.C2 = (char*)d.C2 + r0 * a->ldc2 * 2;
+    if (d.aux) g2.aux = (const char*)d.aux + r0 * a->ldaux * (a->epilogue == VIT_EPI_BIAS_RESID_F32 ? 4 : 2);
+    if (d.col_partial) g2.col_partial = d.col_partial + (main_rows / 256) * a->N;
+    g2.drop.row0 = (int)r0;  // dropout masks are indexed by the absolute row
+    hipError_t e = run(cfg, g1);
+    if (e == hipSuccess) e = run(rem_config(), g2);
+    return vit::check_hip(e, "vit_gemm_bf16 launch");
   }
   return vit::check_hip(run(cfg, d), "vit_gemm_bf16 launch");
 }

@@ -60,6 +60,7 @@ _SIGS = {
     "vit_abi_version": (c_i32, []),
     "vit_gemm_bf16": (c_i32, [ctypes.POINTER(GemmArgs), c_vp]),
     "vit_gemm_tile_rows": (c_i64, [ctypes.POINTER(GemmArgs)]),
+    "vit_gemm_partial_rows": (c_i64, [ctypes.POINTER(GemmArgs)]),
     "vit_splitk_reduce": (c_i32, [c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_i64, c_i64, c_i32, c_vp]),
     "vit_layernorm_fwd": (c_i32, [c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_i32, c_vp, c_vp, c_i64, c_i64, c_f32, c_vp]),
     "vit_layernorm_bwd_partial_rows": (c_i64, [c_i64]),

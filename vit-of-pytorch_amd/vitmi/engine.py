@@ -521,7 +521,7 @@ class ViTEngine:
         kw = dict(a_layout=K_CONTIG, b_layout=K_CONTIG, lda=D, ldb=D, ldc=M, epilogue=EPI_MUL_BF16, aux=a.c_gp,
                   ldaux=M, col_partial=gpart)
         ops.gemm(a.c_dh, self.w2t[i], a.c_dg, b, M, D, **kw)
-        tiles_m = -(-b // ops.gemm_tile_rows(a.c_dh, self.w2t[i], a.c_dg, b, M, D, **kw))
+        tiles_m = ops.gemm_partial_rows(a.c_dh, self.w2t[i], a.c_dg, b, M, D, **kw)
         bias.reduce(gpart, tiles_m, M, M, (gv("mlp.fc1.bias"),))
         on_side(lambda: self._wgrad(a.c_dg, M, a.c_ln2, D, M, D, bp, gv("mlp.fc1.weight"), D))
         ops.gemm(a.c_dg, self.w1t[i], a.c_dyln, b, D, M, a_layout=K_CONTIG, b_layout=K_CONTIG, lda=M, ldb=M, ldc=D,
@@ -687,7 +687,7 @@ class ViTEngine:
                 kw = dict(a_layout=K_CONTIG, b_layout=K_CONTIG, lda=D, ldb=D, ldc=M, epilogue=EPI_MUL_BF16, aux=a.gp[i],
                           ldaux=M, col_partial=gpart)
                 ops.gemm(dhb, self.w2t[i], dg, T, M, D, **kw)
-                tiles_m = -(-T // ops.gemm_tile_rows(dhb, self.w2t[i], dg, T, M, D, **kw))
+                tiles_m = ops.gemm_partial_rows(dhb, self.w2t[i], dg, T, M, D, **kw)
                 bias.reduce(gpart, tiles_m, M, M, (gv(self.lname(i, "mlp.fc1.bias")),))
                 on_side(lambda: self._wgrad(dg, M, a.ln2[i], D, M, D, a.Tp, gv(self.lname(i, "mlp.fc1.weight")), D))
                 release("dg", li)

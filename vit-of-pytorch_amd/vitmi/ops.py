@@ -102,6 +102,11 @@ def gemm_tile_rows(A, B, C, M, N, K, **kw):
     return int(lib().vit_gemm_tile_rows(ctypes.byref(_gemm_args(A, B, C, M, N, K, **kw))))
 
 
+def gemm_partial_rows(A, B, C, M, N, K, **kw):
+    """rows of col_partial a gemm(...) call with these arguments writes (to be reduced)"""
+    return int(lib().vit_gemm_partial_rows(ctypes.byref(_gemm_args(A, B, C, M, N, K, **kw))))
+
+
 def splitk_reduce(ws, batch, split, M, N, out, ldo, out_bs=0, accumulate=False):
     _chk(ws, F32, "ws")
     _chk(out, F32, "out")
