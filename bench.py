@@ -44,7 +44,7 @@ def train_flops_per_image(a, image_size, num_classes):
     return 3 * fwd - patch
 
 
-def pmc_traffic(kernel_tag="gemm_pp2_kernel<true, true, 8>"):
+def pmc_traffic(kernel_tag="gemm_pp2_kernel<true, true, 8,"):
     """HBM bytes per launch of a roofline kernel from the newest committed rocprofv3 PMC passes
     (tools/prof.sh: FETCH_SIZE and WRITE_SIZE in separate passes, FETCH_SIZE doubled per the gfx950
     correction of MI355X_MICROARCH.md). None when no pass of that kernel is committed."""
@@ -331,7 +331,7 @@ def main():
         d_["gflop"] = round(d_["gflop"], 2)
     fc1_flop = 2.0 * T * cfg.emb_dim * cfg.mlp_dim
     fc1_tflops = fc1_flop / (fc1_ms * 1e-3) / 1e12
-    # the step's dominant kernel by time: the split-K weight-gradient GEMM (gemm_pp_kernel; ~22% of the
+    # the step's dominant kernel by time: the split-K weight-gradient GEMM (gemm_pp2_kernel; ~20% of the
     # step), every launch of the timed steps; achieved = its algorithmic FLOPs / its own time
     # headline: the launches over all T tokens (K = T rounded up to 64); the pruned last layer's
     # launches (K = the b cls rows padded to 64) are reported beside it, not averaged in
@@ -354,7 +354,7 @@ def main():
     fpe = fpi - ((3 * 2 * (N_ - 1) * (D_ * D_ + 2 * D_ * M_) + 3 * 4 * (N_ - q_kept) * N_ * D_)
                  if eng.prune_last else 0)
     traffic = pmc_traffic() if args.arch == "b16" and b == 256 else None
-    traffic_w = pmc_traffic("gemm_pp_kernel<256, 64, 2, false, false, 7>") if args.arch == "b16" and b == 256 else None
+    traffic_w = pmc_traffic("gemm_pp2_kernel<false, false, 7,") if args.arch == "b16" and b == 256 else None
     step_tflops_per_gpu = value / world * fpi / 1e12
     out = {
         "metric": "images/sec training step, ViT-B/16 224px bf16, 1/2/4/8 MI355X" if args.arch == "b16" and
@@ -377,7 +377,7 @@ def main():
                    "parallelism": f"dp{world}", "dist_backend": backend,
                    "step_launch": "one HIP graph per step" if use_graph else "eager",
                    **({"grad_allreduce_dtype": "bf16"} if compress and world > 1 else {})},
-        "roofline": {"bound": "mfma", "kernel": "split-K weight-gradient GEMM gemm_pp_kernel (the step's dominant "
+        "roofline": {"bound": "mfma", "kernel": "split-K weight-gradient GEMM gemm_pp2_kernel (the step's dominant "
                                                 f"kernel): the {len(wg_ms)} launches over all tokens of one step "
                                                 f"(HIP events, an eager step after the timed region), K = {T} tokens "
                                                 "padded to 64; fc1 / fc2 / "

@@ -36,8 +36,11 @@ int pick_tile(const vit_gemm_args* a) {
   //    it loses to the plain ping-pong, so those keep config 5 / 3.
   const bool ak = a->a_layout == VIT_K_CONTIG, bk = a->b_layout == VIT_K_CONTIG;
   if (a->epilogue == VIT_EPI_SPLITK && a->M >= 256 && a->N >= 256) {
-    static const int env_sk = vit::knob("VIT_GEMM_SPLITK_CFG", 5);
-    return env_sk == 6 || env_sk == 7 || env_sk == 8 || env_sk == 9 ? env_sk : 5;
+    // round 5: the half-tile ping-pong with inline-asm transposed reads (both operands M/N-contiguous) beats
+    // gemm_pp_kernel on the split-K weight gradients: B/16 step 8178 / 8187 -> 8256 / 8265 img/s, same box
+    // (profiles/r05/splitk_pp2_ab.txt)
+    static const int env_sk = vit::knob("VIT_GEMM_SPLITK_CFG", 9);
+    return env_sk == 5 || env_sk == 6 || env_sk == 7 || env_sk == 8 ? env_sk : 9;
   }
   if (a->M >= 1024 && a->N >= 256) {
     // (short-K f32 residual outputs keep 2 workgroups per CU; the aux-reading epilogues run on the
@@ -46,8 +49,11 @@ int pick_tile(const vit_gemm_args* a) {
     // (short-K f32 residual outputs — the out-projection — also run here: 7418 vs 7385 img/s over
     // the 256x128 two-workgroup kernel, profiles/r02/gemm_epilogue_diag.txt; VIT_GEMM_RESID_PP2=0
     // restores that)
+    // (round 5: with its M/N-contiguous fragments read by inline asm the half-tile kernel runs a B operand in
+    // either layout at the same speed — fc2 dgrad on W2 as it is 269 vs 268 us on the transposed copy,
+    // profiles/r05/gemm_mn_b_pp2.txt — so the forward / data-gradient GEMMs read the weights in place)
     static const int env_rs = vit::knob("VIT_GEMM_RESID_PP2", 1);
-    if (ak && bk && (env_rs || !(a->epilogue == VIT_EPI_BIAS_RESID_F32 && a->K < 2048))) return 9;
+    if (ak && (env_rs || !(a->epilogue == VIT_EPI_BIAS_RESID_F32 && a->K < 2048))) return 9;
     if (a->N >= 2048 && a->epilogue != VIT_EPI_GELU_BWD && a->epilogue != VIT_EPI_MUL_BF16) return 5;
     if (!bk && a->K >= 3072) return 5;
     return 3;
@@ -57,7 +63,7 @@ int pick_tile(const vit_gemm_args* a) {
 
 int tile_rows_of(int cfg) {
   switch (cfg) {
-    case 1: case 2: case 3: case 5: case 6: case 7: case 8: case 9: return 256;
+    case 1: case 2: case 3: case 5: case 6: case 7: case 8: case 9: case 10: case 11: return 256;
     default: return 128;
   }
 }
@@ -169,8 +175,9 @@ extern "C" int vit_gemm_bf16(const vit_gemm_args* a, vit_stream_t stream) {
   VIT_CHECK_ARG(!d.drop.thr || a->epilogue == VIT_EPI_PATCH || a->epilogue == VIT_EPI_BIAS_RESID_F32 ||
                     a->epilogue == VIT_EPI_BIAS_GELU_DGELU,
                 "vit_gemm_bf16: dropout is supported on the PATCH, BIAS_RESID_F32 and BIAS_GELU_DGELU epilogues");
-  VIT_CHECK_ARG(!d.drop.thr || (a->a_layout == VIT_K_CONTIG && a->b_layout == VIT_K_CONTIG),
-                "vit_gemm_bf16: dropout epilogues need K-contiguous A and B");
+  VIT_CHECK_ARG(!d.drop.thr || (a->a_layout == VIT_K_CONTIG &&
+                                  (a->b_layout == VIT_K_CONTIG || a->epilogue == VIT_EPI_BIAS_RESID_F32)),
+                "vit_gemm_bf16: dropout epilogues need a K-contiguous A (and B, except BIAS_RESID_F32)");
   {
     // tile order: groups of 8 tile rows, column-major inside, so the workgroups resident at once
     // share A row panels and B column panels in L2 (fc1 fwd 326 -> 306 us; VIT_GEMM_GROUP_M=1:
@@ -196,7 +203,11 @@ extern "C" int vit_gemm_bf16(const vit_gemm_args* a, vit_stream_t stream) {
   hipStream_t s = (hipStream_t)stream;
   const int batch = (int)a->batch, split = (int)a->split_k;
   const int cfg = pick_tile(a);
+#ifdef VIT_DIAG_KNOBS
+  VIT_CHECK_ARG(cfg >= 0 && cfg <= 11, "vit_gemm_bf16: bad tile config %d", cfg);
+#else
   VIT_CHECK_ARG(cfg >= 0 && cfg <= 9, "vit_gemm_bf16: bad tile config %d", cfg);
+#endif
   VIT_CHECK_ARG(cfg != 1 || a->K % 32 == 0, "vit_gemm_bf16: K");
   auto run = [&](int c, const GemmDev& g) -> hipError_t {
     switch (a->epilogue) {
@@ -205,15 +216,15 @@ extern "C" int vit_gemm_bf16(const vit_gemm_args* a, vit_stream_t stream) {
       case VIT_EPI_BIAS_BF16: return vitg::launch_layout_x<VIT_EPI_BIAS_BF16>(c, g, ak, bk, batch, split, s);
       case VIT_EPI_BIAS_GELU: return vitg::launch_layout_x<VIT_EPI_BIAS_GELU>(c, g, ak, bk, batch, split, s);
       case VIT_EPI_BIAS_RESID_F32:
-        if (g.drop.thr) return vitg::launch_kk_x<VIT_EPI_BIAS_RESID_F32 | EPI_DROP>(c, g, batch, split, s);
+        if (g.drop.thr) return vitg::launch_kk_x<VIT_EPI_BIAS_RESID_F32 | EPI_DROP>(c, g, bk, batch, split, s);
         return vitg::launch_layout_x<VIT_EPI_BIAS_RESID_F32>(c, g, ak, bk, batch, split, s);
       case VIT_EPI_GELU_BWD: return vitg::launch_layout_x<VIT_EPI_GELU_BWD>(c, g, ak, bk, batch, split, s);
       case VIT_EPI_BIAS_GELU_DGELU:
-        if (g.drop.thr) return vitg::launch_kk_x<VIT_EPI_BIAS_GELU_DGELU | EPI_DROP>(c, g, batch, split, s);
+        if (g.drop.thr) return vitg::launch_kk_x<VIT_EPI_BIAS_GELU_DGELU | EPI_DROP>(c, g, bk, batch, split, s);
         return vitg::launch_layout_x<VIT_EPI_BIAS_GELU_DGELU>(c, g, ak, bk, batch, split, s);
       case VIT_EPI_MUL_BF16: return vitg::launch_layout_x<VIT_EPI_MUL_BF16>(c, g, ak, bk, batch, split, s);
       case VIT_EPI_PATCH:
-        if (g.drop.thr) return vitg::launch_kk_x<VIT_EPI_PATCH | EPI_DROP>(c, g, batch, split, s);
+        if (g.drop.thr) return vitg::launch_kk_x<VIT_EPI_PATCH | EPI_DROP>(c, g, bk, batch, split, s);
         return vitg::launch_layout_x<VIT_EPI_PATCH>(c, g, ak, bk, batch, split, s);
       case VIT_EPI_SPLITK: return vitg::launch_layout_x<VIT_EPI_SPLITK>(c, g, ak, bk, batch, split, s);
       default: return hipErrorInvalidValue;

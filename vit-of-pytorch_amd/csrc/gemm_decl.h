@@ -60,8 +60,8 @@ constexpr int EPI_DROP = 16;
 // launchers, one translation unit per epilogue (gemm_e<EPI>.hip) so the build parallelises
 template <int EPI>
 hipError_t launch_layout_x(int cfg, const GemmDev& d, bool ak, bool bk, int batch, int split, hipStream_t s);
-template <int EPI>  // both operands K-contiguous (the dropout variants)
-hipError_t launch_kk_x(int cfg, const GemmDev& d, int batch, int split, hipStream_t s);
+template <int EPI>  // A K-contiguous (the dropout variants); B K-contiguous, or M/N-contiguous when bk is false
+hipError_t launch_kk_x(int cfg, const GemmDev& d, bool bk, int batch, int split, hipStream_t s);
 template <> hipError_t launch_layout_x<0>(int, const GemmDev&, bool, bool, int, int, hipStream_t);
 template <> hipError_t launch_layout_x<1>(int, const GemmDev&, bool, bool, int, int, hipStream_t);
 template <> hipError_t launch_layout_x<2>(int, const GemmDev&, bool, bool, int, int, hipStream_t);
@@ -72,8 +72,8 @@ template <> hipError_t launch_layout_x<6>(int, const GemmDev&, bool, bool, int, 
 template <> hipError_t launch_layout_x<7>(int, const GemmDev&, bool, bool, int, int, hipStream_t);
 template <> hipError_t launch_layout_x<8>(int, const GemmDev&, bool, bool, int, int, hipStream_t);
 template <> hipError_t launch_layout_x<9>(int, const GemmDev&, bool, bool, int, int, hipStream_t);
-template <> hipError_t launch_kk_x<20>(int, const GemmDev&, int, int, hipStream_t);
-template <> hipError_t launch_kk_x<22>(int, const GemmDev&, int, int, hipStream_t);
-template <> hipError_t launch_kk_x<24>(int, const GemmDev&, int, int, hipStream_t);
+template <> hipError_t launch_kk_x<20>(int, const GemmDev&, bool, int, int, hipStream_t);
+template <> hipError_t launch_kk_x<22>(int, const GemmDev&, bool, int, int, hipStream_t);
+template <> hipError_t launch_kk_x<24>(int, const GemmDev&, bool, int, int, hipStream_t);
 }  // namespace vitg
 

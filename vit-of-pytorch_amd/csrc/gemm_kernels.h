@@ -1151,6 +1151,10 @@ hipError_t launch_cfg(int cfg, const GemmDev& d, int batch, int split, hipStream
     case 7: return launch_pp<256, 32, 4, AK, BKC, EPI>(d, batch, split, s);
     case 8: return launch_pp<256, 32, 5, AK, BKC, EPI>(d, batch, split, s);
     case 9: return launch_pp2<AK, BKC, EPI>(d, batch, split, s);
+#ifdef VIT_DIAG_KNOBS
+    case 10: return launch_pp2<AK, BKC, EPI, 32, 2>(d, batch, split, s);  // diagnostic: 32-deep k-tiles
+    case 11: return launch_pp2<AK, BKC, EPI, 32, 4>(d, batch, split, s);  // ... with a 3-k-tile-deep ring
+#endif
     default: return launch_t<128, 128, 64, 2, 2, 2, AK, BKC, EPI>(d, batch, split, s);
   }
 }

@@ -263,14 +263,12 @@ class ViTEngine:
         D, L = cfg.emb_dim, cfg.num_layers
         M = cfg.mlp_dim
         bf = torch.bfloat16
-        self.wqkv = torch.zeros(L, D, 3 * D, device=self.dev, dtype=bf)   # [in][q|k|v out]: qkv dgrad operand
+        # [in][q|k|v out]: the fused q|k|v GEMM's B operand, M/N-contiguous in the forward, K-contiguous in the
+        # data gradient. Every other weight is read in place from the bf16 mirror in whichever layout its GEMM
+        # sees it (the half-tile ping-pong runs an M/N-contiguous B as fast as a K-contiguous one since round 5:
+        # no transposed copies)
+        self.wqkv = torch.zeros(L, D, 3 * D, device=self.dev, dtype=bf)
         self.bqkv = torch.zeros(L, 3 * D, device=self.dev)
-        # K-contiguous (transposed) bf16 copies: with them every forward and dgrad GEMM has both
-        # operands K-contiguous and runs on the half-tile ping-pong kernel (tile config 9)
-        self.wqkvt = torch.zeros(L, 3 * D, D, device=self.dev, dtype=bf)  # qkv forward
-        self.woutt = torch.zeros(L, D, D, device=self.dev, dtype=bf)      # out-proj forward
-        self.w1t = torch.zeros(L, D, M, device=self.dev, dtype=bf)        # fc1 dgrad
-        self.w2t = torch.zeros(L, M, D, device=self.dev, dtype=bf)        # fc2 dgrad
         kp = _rup(cfg.patch_k, 64)
         self.wconv = torch.zeros(D, kp, device=self.dev, dtype=torch.bfloat16) if kp != cfg.patch_k else None
         self._acts = {}
@@ -345,23 +343,14 @@ class ViTEngine:
         D = cfg.emb_dim
         if full:
             ops.cast_bf16(self.flat, self.mirror, self.layout.numel)
-        # q|k|v packing and K-contiguous copies, one launch per weight kind over all layers (layers sit
-        # at a constant stride in the flat buffer, layer L-1 first)
+        # q|k|v packing, one launch over all layers (layers sit at a constant stride in the flat buffer, layer
+        # L-1 first)
         M, L = cfg.mlp_dim, cfg.num_layers
         lst = self.layer_stride
         o0 = lambda s: self.off(self.lname(0, s))
         zs = self.off(self.lname(0, "attn.key.weight")) - o0("attn.query.weight")
         ops.pack_cols_batched(self.flat[o0("attn.query.weight"):], -lst, zs, D, D, D, 3, self.wqkv, D * 3 * D, 3 * D, L)
         ops.pack_cols_batched(self.flat[o0("attn.query.bias"):], -lst, zs, D, 1, D, 3, self.bqkv, 3 * D, 3 * D, L)
-        for z in range(3):
-            ops.transpose_bf16(self.flat[o0("attn.query.weight") + z * zs:], D, D, D, self.wqkvt[0, z * D:], D,
-                               batch=L, in_bs=-lst, out_bs=3 * D * D)
-        ops.transpose_bf16(self.flat[o0("attn.out.weight"):], D, D, D, self.woutt[0], D, batch=L, in_bs=-lst,
-                           out_bs=D * D)
-        ops.transpose_bf16(self.flat[o0("mlp.fc1.weight"):], M, D, D, self.w1t[0], M, batch=L, in_bs=-lst,
-                           out_bs=D * M)
-        ops.transpose_bf16(self.flat[o0("mlp.fc2.weight"):], D, M, M, self.w2t[0], D, batch=L, in_bs=-lst,
-                           out_bs=M * D)
         if self.wconv is not None:
             w = self.off("embedding.weight")
             ops.cast_pad_rows(self.flat[w:], D, cfg.patch_k, self.wconv, self.wconv.shape[1])
@@ -450,15 +439,15 @@ class ViTEngine:
             ln = lambda s: self.off(self.lname(i, s))
             ops.layernorm_fwd(a.h[i], D, f[ln("norm1.weight"):], f[ln("norm1.bias"):], a.ln1[i], D, a.mu1[i],
                               a.rs1[i], T, D)
-            ops.gemm(a.ln1[i], self.wqkvt[i], a.qkv[i], T, 3 * D, D, a_layout=K_CONTIG, b_layout=K_CONTIG, lda=D,
-                     ldb=D, ldc=3 * D, epilogue=EPI_BIAS_BF16, bias=self.bqkv[i])
+            ops.gemm(a.ln1[i], self.wqkv[i], a.qkv[i], T, 3 * D, D, a_layout=K_CONTIG, b_layout=MN_CONTIG, lda=D,
+                     ldb=3 * D, ldc=3 * D, epilogue=EPI_BIAS_BF16, bias=self.bqkv[i])
             last = self._pruned and i == L - 1
             ops.attention_fwd(a.qkv[i], a.o[i], a.lse[i], b, N, H, hd, scale, q_rows=1 if last else None,
                               path=self.attn_fwd_path)
             if last:
                 self._forward_last_cls(a, i, b)
                 break
-            ops.gemm(a.o[i], self.woutt[i], a.hm[i], T, D, D, a_layout=K_CONTIG, b_layout=K_CONTIG,
+            ops.gemm(a.o[i], mv[ln("attn.out.weight"):], a.hm[i], T, D, D, a_layout=K_CONTIG, b_layout=MN_CONTIG,
                      lda=D, ldb=D, ldc=D, epilogue=EPI_BIAS_RESID_F32, bias=f[ln("attn.out.bias"):], aux=a.h[i],
                      ldaux=D, dropout=dd(1 + 3 * i))
             ops.layernorm_fwd(a.hm[i], D, f[ln("norm2.weight"):], f[ln("norm2.bias"):], a.ln2[i], D, a.mu2[i],
@@ -494,8 +483,8 @@ class ViTEngine:
         f, mv = self.flat, self.mirror
         ln = lambda s: self.off(self.lname(i, s))
         S = N * D
-        ops.gemm(a.o[i], self.woutt[i], a.hm[i], b, D, D, a_layout=K_CONTIG, b_layout=K_CONTIG, lda=S, ldb=D,
-                 ldc=S, epilogue=EPI_BIAS_RESID_F32, bias=f[ln("attn.out.bias"):], aux=a.h[i], ldaux=S)
+        ops.gemm(a.o[i], mv[ln("attn.out.weight"):], a.hm[i], b, D, D, a_layout=K_CONTIG, b_layout=MN_CONTIG, lda=S,
+                 ldb=D, ldc=S, epilogue=EPI_BIAS_RESID_F32, bias=f[ln("attn.out.bias"):], aux=a.h[i], ldaux=S)
         ops.copy2d(a.c_o, D * 2, a.o[i], S * 2, D * 2, b)    # cls rows: the out-proj weight-gradient operand
         ops.layernorm_fwd(a.hm[i], S, f[ln("norm2.weight"):], f[ln("norm2.bias"):], a.c_ln2, D, a.c_mu2, a.c_rs2,
                           b, D)
@@ -518,14 +507,15 @@ class ViTEngine:
         bp = a.bp
         on_side(lambda: self._wgrad(a.c_dh, D, a.c_g, M, D, M, bp, gv("mlp.fc2.weight"), M))
         gpart = bias.buf("gelu", a.gelu_parts)
-        kw = dict(a_layout=K_CONTIG, b_layout=K_CONTIG, lda=D, ldb=D, ldc=M, epilogue=EPI_MUL_BF16, aux=a.c_gp,
+        w2 = mv[self.off(self.lname(i, "mlp.fc2.weight")):]
+        kw = dict(a_layout=K_CONTIG, b_layout=MN_CONTIG, lda=D, ldb=M, ldc=M, epilogue=EPI_MUL_BF16, aux=a.c_gp,
                   ldaux=M, col_partial=gpart)
-        ops.gemm(a.c_dh, self.w2t[i], a.c_dg, b, M, D, **kw)
-        tiles_m = ops.gemm_partial_rows(a.c_dh, self.w2t[i], a.c_dg, b, M, D, **kw)
+        ops.gemm(a.c_dh, w2, a.c_dg, b, M, D, **kw)
+        tiles_m = ops.gemm_partial_rows(a.c_dh, w2, a.c_dg, b, M, D, **kw)
         bias.reduce(gpart, tiles_m, M, M, (gv("mlp.fc1.bias"),))
         on_side(lambda: self._wgrad(a.c_dg, M, a.c_ln2, D, M, D, bp, gv("mlp.fc1.weight"), D))
-        ops.gemm(a.c_dg, self.w1t[i], a.c_dyln, b, D, M, a_layout=K_CONTIG, b_layout=K_CONTIG, lda=M, ldb=M, ldc=D,
-                 epilogue=EPI_BF16)
+        ops.gemm(a.c_dg, mv[self.off(self.lname(i, "mlp.fc1.weight")):], a.c_dyln, b, D, M, a_layout=K_CONTIG,
+                 b_layout=MN_CONTIG, lda=M, ldb=D, ldc=D, epilogue=EPI_BF16)
         bias.ln_bwd(a.c_dyln, D, a.hm[i], S, a.c_mu2, a.c_rs2, f[self.off(self.lname(i, "norm2.weight")):], a.dh, S, b,
                     gv("norm2.weight"), gv("attn.out.bias"), dres=a.dh, lddres=S, dx_bf16=a.c_dh2, lddxb=D)
         on_side(lambda: self._wgrad(a.c_o, D, a.c_dh2, D, D, D, bp, gv("attn.out.weight"), D))
@@ -684,15 +674,16 @@ class ViTEngine:
                 dg = a.dg[li]
                 acquire("dg", li)
                 gpart = bias.buf("gelu", a.gelu_parts)
-                kw = dict(a_layout=K_CONTIG, b_layout=K_CONTIG, lda=D, ldb=D, ldc=M, epilogue=EPI_MUL_BF16, aux=a.gp[i],
+                w2 = mv[ln("mlp.fc2.weight"):]
+                kw = dict(a_layout=K_CONTIG, b_layout=MN_CONTIG, lda=D, ldb=M, ldc=M, epilogue=EPI_MUL_BF16, aux=a.gp[i],
                           ldaux=M, col_partial=gpart)
-                ops.gemm(dhb, self.w2t[i], dg, T, M, D, **kw)
-                tiles_m = ops.gemm_partial_rows(dhb, self.w2t[i], dg, T, M, D, **kw)
+                ops.gemm(dhb, w2, dg, T, M, D, **kw)
+                tiles_m = ops.gemm_partial_rows(dhb, w2, dg, T, M, D, **kw)
                 bias.reduce(gpart, tiles_m, M, M, (gv(self.lname(i, "mlp.fc1.bias")),))
                 on_side(lambda: self._wgrad(dg, M, a.ln2[i], D, M, D, a.Tp, gv(self.lname(i, "mlp.fc1.weight")), D))
                 release("dg", li)
-                ops.gemm(dg, self.w1t[i], a.dyln, T, D, M, a_layout=K_CONTIG, b_layout=K_CONTIG, lda=M,
-                         ldb=M, ldc=D, epilogue=EPI_BF16)
+                ops.gemm(dg, mv[ln("mlp.fc1.weight"):], a.dyln, T, D, M, a_layout=K_CONTIG, b_layout=MN_CONTIG, lda=M,
+                         ldb=D, ldc=D, epilogue=EPI_BF16)
                 wb ^= 1
                 acquire("dhb", wb)
                 dhb = a.dhb[wb]
