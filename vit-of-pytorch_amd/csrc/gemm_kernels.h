@@ -697,18 +697,54 @@ __global__ void __launch_bounds__(WM* WN * 64, (gemm_min_waves<BM, BN, BK, STAGE
     asm volatile("" ::: "memory");
     if (t + STAGES - 1 < nk) issue(t + STAGES - 1);
     const int cur = (t % STAGES) * STAGE;
+    if constexpr (AK && BKC) {
 #pragma unroll
-    for (int kk = 0; kk < KK; ++kk) {
-      v8s bfr[FN];
+      for (int kk = 0; kk < KK; ++kk) {
+        v8s bfr[FN];
 #pragma unroll
-      for (int j = 0; j < FN; ++j) bfr[j] = read_frag<BN, BK, BKC>(smem, cur + A_BYTES, wn0 + j * 16, kk, lane);
+        for (int j = 0; j < FN; ++j) bfr[j] = read_frag<BN, BK, BKC>(smem, cur + A_BYTES, wn0 + j * 16, kk, lane);
 #pragma unroll
-      for (int i = 0; i < FM; ++i) {
-        const v8s af = read_frag<BM, BK, AK>(smem, cur, wm0 + i * 16, kk, lane);
+        for (int i = 0; i < FM; ++i) {
+          const v8s af = read_frag<BM, BK, AK>(smem, cur, wm0 + i * 16, kk, lane);
 #pragma unroll
-        for (int j = 0; j < FN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(v8bf, af),
-                                                              __builtin_bit_cast(v8bf, bfr[j]), acc[i][j], 0, 0, 0);
+          for (int j = 0; j < FN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(v8bf, af),
+                                                                __builtin_bit_cast(v8bf, bfr[j]), acc[i][j], 0, 0, 0);
+        }
+      }
+    } else {
+      // an M/N-contiguous operand: its transposed fragment reads by inline asm (hipcc puts a vmcnt(0) in front of
+      // a ds_read_b64_tr_b16 of this array while the DMA just issued into another stage is in flight: the
+      // round-3 gemm_pp_kernel finding; 60 vs 27 us for the fc1 data gradient's wave-split remainder with W1 read
+      // in place), every read of a k-step issued before an explicit lgkmcnt(0), then the MFMAs
+      const uint32_t sb = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)LDS_PTR(char, smem) + cur);
+#pragma unroll
+      for (int kk = 0; kk < KK; ++kk) {
+        v8s bfr[FN], af[FM];
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          if constexpr (BKC)
+            bfr[j] = read_frag<BN, BK, BKC>(smem, cur + A_BYTES, wn0 + j * 16, kk, lane);
+          else
+            bfr[j] = kk == 0 ? read_frag_tr_asm<BN, 0>(sb + A_BYTES + frag_tr_lane_off<BN>(wn0 + j * 16, lane))
+                             : read_frag_tr_asm<BN, 1>(sb + A_BYTES + frag_tr_lane_off<BN>(wn0 + j * 16, lane));
+        }
+#pragma unroll
+        for (int i = 0; i < FM; ++i) {
+          if constexpr (AK)
+            af[i] = read_frag<BM, BK, AK>(smem, cur, wm0 + i * 16, kk, lane);
+          else
+            af[i] = kk == 0 ? read_frag_tr_asm<BM, 0>(sb + frag_tr_lane_off<BM>(wm0 + i * 16, lane))
+                            : read_frag_tr_asm<BM, 1>(sb + frag_tr_lane_off<BM>(wm0 + i * 16, lane));
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(v8bf, af[i]),
+                                                                __builtin_bit_cast(v8bf, bfr[j]), acc[i][j], 0, 0, 0);
       }
     }
     asm volatile("" ::: "memory");
