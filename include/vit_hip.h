@@ -132,6 +132,14 @@ int64_t vit_gemm_tile_rows(const vit_gemm_args* args);
 /* rows of col_partial a call with these arguments writes (the rows to reduce with vit_colsum): one per
  * 256-row tile of the whole-wave part and one per 128-row tile of a wave-split remainder */
 int64_t vit_gemm_partial_rows(const vit_gemm_args* args);
+/* rows of the whole-wave part of a wave-split call (the 256 x 256 tiles that fill whole waves of the CUs; the
+ * remaining rows run on 128 x 128 tiles), 0 when the call runs as one launch */
+int64_t vit_gemm_split_rows(const vit_gemm_args* args);
+/* one part of vit_gemm_bf16: part 1 = the whole-wave rows [0, split_rows) (the whole GEMM when it does not
+ * split), part 2 = the remainder rows [split_rows, M) (nothing when it does not split). Parts 1 and 2 together
+ * are exactly vit_gemm_bf16(args); they may run on different streams (the remainder beside a row-local op of
+ * the whole-wave rows) */
+int vit_gemm_bf16_part(const vit_gemm_args* args, int32_t part, vit_stream_t stream);
 
 /* out[z*out_batch_stride + m*ldo + n] (+)= sum_s ws[((z*split + s)*M + m)*N + n]  (f32) */
 int vit_splitk_reduce(const float* ws, int64_t batch, int64_t split, int64_t M, int64_t N,

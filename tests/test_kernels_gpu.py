@@ -110,6 +110,35 @@ def test_gemm_col_partial_wave_split():
     assert rel(part[19:rows].sum(0), ref[19 * 256:].sum(0)) < 1e-4
 
 
+def test_gemm_parts_equal_whole():
+    """vit_gemm_bf16_part: the whole-wave rows (part 1) and the wave-split remainder (part 2), on two streams,
+    write exactly what one vit_gemm_bf16 call writes (bias + f32 residual epilogue, the out-projection shape
+    family); a GEMM that does not split runs whole as part 1 and not at all as part 2."""
+    M, N, K = 5120, 3328, 128
+    A, B, Am, Bm, lda, ldb = _mats(M, N, K, K_CONTIG, K_CONTIG)
+    bias, res = torch.randn(N, device=DEV), torch.randn(M, N, device=DEV)
+    kw = dict(a_layout=K_CONTIG, b_layout=K_CONTIG, lda=lda, ldb=ldb, ldc=N, epilogue=EPI_BIAS_RESID_F32, bias=bias,
+              aux=res, ldaux=N)
+    whole, parts = torch.empty(M, N, device=DEV), torch.full((M, N), float("nan"), device=DEV)
+    assert ops.gemm_split_rows(Am, Bm, whole, M, N, K, **kw) == 19 * 256
+    ops.gemm(Am, Bm, whole, M, N, K, **kw)
+    ops.gemm(Am, Bm, parts, M, N, K, part=1, **kw)
+    assert torch.isnan(parts[19 * 256:]).all() and not torch.isnan(parts[:19 * 256]).any()
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        ops.gemm(Am, Bm, parts, M, N, K, part=2, **kw)
+    torch.cuda.current_stream().wait_stream(side)
+    assert torch.equal(parts, whole)
+    assert rel(whole, A.float() @ B.float() + bias + res) < 5e-3
+    small = torch.full((256, N), float("nan"), device=DEV)
+    assert ops.gemm_split_rows(Am, Bm, small, 256, N, K, **kw) == 0
+    ops.gemm(Am, Bm, small, 256, N, K, part=2, **kw)
+    assert torch.isnan(small).all()
+    ops.gemm(Am, Bm, small, 256, N, K, part=1, **kw)
+    assert torch.equal(small, whole[:256])
+
+
 @pytest.mark.parametrize("tile", [1, 2, 6, 9])
 def test_gemm_tiles_epilogue_splitk(tile):
     M, N, K = 700, 520, 512

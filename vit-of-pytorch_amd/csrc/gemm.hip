@@ -115,7 +115,15 @@ extern "C" int64_t vit_gemm_partial_rows(const vit_gemm_args* a) {
   return (a->M + tr - 1) / tr;
 }
 
-extern "C" int vit_gemm_bf16(const vit_gemm_args* a, vit_stream_t stream) {
+extern "C" int64_t vit_gemm_split_rows(const vit_gemm_args* a) {
+  if (!a) return 0;
+  return wave_split_rows(a, pick_tile(a));
+}
+
+namespace {
+// part 0: the whole GEMM; 1: its whole-wave rows (all of it when it does not split); 2: the wave-split remainder
+// rows (nothing when it does not split)
+int gemm_bf16_impl(const vit_gemm_args* a, int part, vit_stream_t stream) {
   VIT_CHECK_ARG(a != nullptr, "vit_gemm_bf16: null args");
   VIT_CHECK_ARG(a->M >= 0 && a->N >= 0 && a->K >= 0, "vit_gemm_bf16: negative size");
   VIT_CHECK_ARG(a->K % 64 == 0, "vit_gemm_bf16: K=%lld must be a multiple of 64", (long long)a->K);
@@ -249,11 +257,21 @@ extern "C" int vit_gemm_bf16(const vit_gemm_args* a, vit_stream_t stream) {
     if (d.aux) g2.aux = (const char*)d.aux + r0 * a->ldaux * (a->epilogue == VIT_EPI_BIAS_RESID_F32 ? 4 : 2);
     if (d.col_partial) g2.col_partial = d.col_partial + (main_rows / 256) * a->N;
     g2.drop.row0 = (int)r0;  // dropout masks are indexed by the absolute row
-    hipError_t e = run(cfg, g1);
-    if (e == hipSuccess) e = run(rem_config(), g2);
+    hipError_t e = hipSuccess;
+    if (part != 2) e = run(cfg, g1);
+    if (e == hipSuccess && part != 1) e = run(rem_config(), g2);
     return vit::check_hip(e, "vit_gemm_bf16 launch");
   }
+  if (part == 2) return VIT_OK;
   return vit::check_hip(run(cfg, d), "vit_gemm_bf16 launch");
+}
+}  // namespace
+
+extern "C" int vit_gemm_bf16(const vit_gemm_args* a, vit_stream_t stream) { return gemm_bf16_impl(a, 0, stream); }
+
+extern "C" int vit_gemm_bf16_part(const vit_gemm_args* a, int32_t part, vit_stream_t stream) {
+  VIT_CHECK_ARG(part == 1 || part == 2, "vit_gemm_bf16_part: part %d (1 = whole-wave rows, 2 = remainder)", part);
+  return gemm_bf16_impl(a, part, stream);
 }
 
 // ---- split-K reduction -------------------------------------------------------------------------

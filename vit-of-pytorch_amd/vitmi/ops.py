@@ -82,11 +82,15 @@ GEMM_PROBE = None
 GEMM_PROBE_MIN_M = 0
 
 
-def gemm(A, B, C, M, N, K, **kw):
-    """bf16 MFMA GEMM, C[m,n] = sum_k A(m,k) B(k,n) + fused epilogue (see vit_gemm_args)."""
+def gemm(A, B, C, M, N, K, part=0, **kw):
+    """bf16 MFMA GEMM, C[m,n] = sum_k A(m,k) B(k,n) + fused epilogue (see vit_gemm_args).
+    part 1 / 2: only the whole-wave rows / the wave-split remainder rows (vit_gemm_bf16_part)."""
     _chk(A, BF16, "A")
     _chk(B, BF16, "B")
     a = _gemm_args(A, B, C, M, N, K, **kw)
+    if part:
+        check(lib().vit_gemm_bf16_part(ctypes.byref(a), int(part), _stream()), "vit_gemm_bf16_part")
+        return
     probe = GEMM_PROBE is not None and M >= GEMM_PROBE_MIN_M and a.split_k == 1 and a.epilogue != _lib.EPI_SPLITK
     if probe:
         ev0 = torch.cuda.Event(enable_timing=True)
@@ -100,6 +104,11 @@ def gemm(A, B, C, M, N, K, **kw):
 
 def gemm_tile_rows(A, B, C, M, N, K, **kw):
     return int(lib().vit_gemm_tile_rows(ctypes.byref(_gemm_args(A, B, C, M, N, K, **kw))))
+
+
+def gemm_split_rows(A, B, C, M, N, K, **kw):
+    """rows of the whole-wave part of a wave-split gemm(...) call (0: one launch)"""
+    return int(lib().vit_gemm_split_rows(ctypes.byref(_gemm_args(A, B, C, M, N, K, **kw))))
 
 
 def gemm_partial_rows(A, B, C, M, N, K, **kw):
