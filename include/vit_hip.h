@@ -140,6 +140,11 @@ int64_t vit_gemm_split_rows(const vit_gemm_args* args);
  * are exactly vit_gemm_bf16(args); they may run on different streams (the remainder beside a row-local op of
  * the whole-wave rows) */
 int vit_gemm_bf16_part(const vit_gemm_args* args, int32_t part, vit_stream_t stream);
+/* up to 4 split-K weight-gradient GEMMs in ONE launch (the concatenation of their grids): each member is a
+ * vit_gemm_bf16 call with epilogue VIT_EPI_SPLITK, both operands M/N-contiguous, M, N >= 256, its own split_k /
+ * batch, and writes exactly what that call writes (the same f32 slabs). Fills the CUs where members alone leave a
+ * wave partly empty (the out-projection and q|k|v weight gradients of one layer) */
+int vit_gemm_splitk_group(const vit_gemm_args* args, int32_t n, vit_stream_t stream);
 
 /* out[z*out_batch_stride + m*ldo + n] (+)= sum_s ws[((z*split + s)*M + m)*N + n]  (f32) */
 int vit_splitk_reduce(const float* ws, int64_t batch, int64_t split, int64_t M, int64_t N,

@@ -134,6 +134,10 @@ def test_splitk_factor_one_wave_splits_and_h14_tail():
     assert [f(4096, 1024, 12608), f(3072, 1024, 12608), f(1024, 1024, 12608)] == [4, 5, 16]
     assert [f(5120, 1280, 32896), f(1280, 5120, 32896), f(3840, 1280, 32896)] == [5, 5, 3]
     assert f(768, 768, 256) == 1 and f(768, 768, 64) == 1        # at least 8 k-tiles per split
+    # one grid for a layer's out-projection + q|k|v weight gradients: B/16 one wave at 7, L/16 bs 64 one at 4
+    from vitmi.ops import splitk_factor_group as fg
+    assert fg([(768, 768, 1), (768, 768, 3)], 50432) == 7
+    assert fg([(1024, 1024, 1), (1024, 1024, 3)], 12608) == 4
     for M, N, K in [(768, 768, 50432), (64, 64, 1 << 20), (5120, 1280, 32896)]:
         s = f(M, N, K)
         assert 1 <= s <= 32 and (s == 1 or K // 64 // s >= 8)

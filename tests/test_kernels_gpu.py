@@ -139,6 +139,35 @@ def test_gemm_parts_equal_whole():
     assert torch.equal(small, whole[:256])
 
 
+def test_gemm_splitk_group_equals_members():
+    """vit_gemm_splitk_group: an out-projection-like member (batch 1) and a q|k|v-like one (batch 3, B columns
+    strided) in one launch write bit-identical f32 slabs to their own vit_gemm_bf16 calls at the same split, and the
+    slabs sum to the f32 products; a member that breaks the contract (K-contiguous A) is refused."""
+    from vitmi._lib import EPI_SPLITK, VitHipError
+    g = torch.Generator(device="cpu").manual_seed(7)
+    K, D, S = 1024, 256, 3
+    A1 = torch.randn(K, D, generator=g).bfloat16().to(DEV)       # [tokens][M]: M/N-contiguous
+    B1 = torch.randn(K, D, generator=g).bfloat16().to(DEV)
+    A2 = torch.randn(K, D, generator=g).bfloat16().to(DEV)
+    B2 = torch.randn(K, 3 * D, generator=g).bfloat16().to(DEV)   # three [tokens][D] column blocks
+    kw1 = dict(a_layout=MN_CONTIG, b_layout=MN_CONTIG, lda=D, ldb=D, ldc=D, epilogue=EPI_SPLITK, split_k=S)
+    kw2 = dict(a_layout=MN_CONTIG, b_layout=MN_CONTIG, lda=D, ldb=3 * D, ldc=D, epilogue=EPI_SPLITK, split_k=S,
+               batch=3, b_bs=D)
+    w1, w2 = torch.empty(S, D, D, device=DEV), torch.empty(3, S, D, D, device=DEV)
+    ops.gemm(A1, B1, w1, D, D, K, **kw1)
+    ops.gemm(A2, B2, w2, D, D, K, **kw2)
+    g1, g2 = torch.full_like(w1, float("nan")), torch.full_like(w2, float("nan"))
+    ops.gemm_splitk_group([(A1, B1, g1, D, D, K, kw1), (A2, B2, g2, D, D, K, kw2)])
+    assert torch.equal(g1, w1) and torch.equal(g2, w2)
+    ref1 = A1.float().t() @ B1.float()
+    assert rel(g1.sum(0), ref1) < 1e-5
+    for z in range(3):
+        assert rel(g2[z].sum(0), A2.float().t() @ B2[:, z * D:(z + 1) * D].float()) < 1e-5
+    bad = dict(kw1, a_layout=K_CONTIG, lda=K)
+    with pytest.raises(VitHipError, match="split-K weight gradient"):
+        ops.gemm_splitk_group([(A1.t().contiguous(), B1, g1, D, D, K, bad)])
+
+
 @pytest.mark.parametrize("tile", [1, 2, 6, 9])
 def test_gemm_tiles_epilogue_splitk(tile):
     M, N, K = 700, 520, 512

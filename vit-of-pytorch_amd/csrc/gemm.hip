@@ -121,9 +121,9 @@ extern "C" int64_t vit_gemm_split_rows(const vit_gemm_args* a) {
 }
 
 namespace {
-// part 0: the whole GEMM; 1: its whole-wave rows (all of it when it does not split); 2: the wave-split remainder
-// rows (nothing when it does not split)
-int gemm_bf16_impl(const vit_gemm_args* a, int part, vit_stream_t stream) {
+// validated device descriptor of a call's arguments; `empty`: M or N is 0 (nothing to launch)
+int make_dev(const vit_gemm_args* a, GemmDev& d, bool& empty) {
+  empty = false;
   VIT_CHECK_ARG(a != nullptr, "vit_gemm_bf16: null args");
   VIT_CHECK_ARG(a->M >= 0 && a->N >= 0 && a->K >= 0, "vit_gemm_bf16: negative size");
   VIT_CHECK_ARG(a->K % 64 == 0, "vit_gemm_bf16: K=%lld must be a multiple of 64", (long long)a->K);
@@ -133,7 +133,10 @@ int gemm_bf16_impl(const vit_gemm_args* a, int part, vit_stream_t stream) {
   VIT_CHECK_ARG(a->split_k == 1 || a->epilogue == VIT_EPI_SPLITK, "vit_gemm_bf16: split_k>1 needs VIT_EPI_SPLITK");
   VIT_CHECK_ARG(a->a_layout == VIT_K_CONTIG || a->a_layout == VIT_MN_CONTIG, "vit_gemm_bf16: bad a_layout");
   VIT_CHECK_ARG(a->b_layout == VIT_K_CONTIG || a->b_layout == VIT_MN_CONTIG, "vit_gemm_bf16: bad b_layout");
-  if (a->M == 0 || a->N == 0) return VIT_OK;
+  if (a->M == 0 || a->N == 0) {
+    empty = true;
+    return VIT_OK;
+  }
   const bool ak = a->a_layout == VIT_K_CONTIG, bk = a->b_layout == VIT_K_CONTIG;
   // valid extents (bytes) of one batch of each operand
   const long a_rows = ak ? a->M : a->K, a_cols = ak ? a->K : a->M;
@@ -158,7 +161,7 @@ int gemm_bf16_impl(const vit_gemm_args* a, int part, vit_stream_t stream) {
       break;
     default: break;
   }
-  GemmDev d;
+  d = GemmDev{};
   d.M = (int)a->M; d.N = (int)a->N; d.K = (int)a->K;
   d.A = (const char*)a->A; d.lda = a->lda; d.a_bs = a->a_batch_stride; d.a_bytes = (uint32_t)a_bytes;
   d.B = (const char*)a->B; d.ldb = a->ldb; d.b_bs = a->b_batch_stride; d.b_bytes = (uint32_t)b_bytes;
@@ -201,6 +204,17 @@ int gemm_bf16_impl(const vit_gemm_args* a, int part, vit_stream_t stream) {
     static const int env_prio = vit::knob("VIT_GEMM_PRIO", 1);
     d.prio = env_prio;
   }
+  return VIT_OK;
+}
+
+// part 0: the whole GEMM; 1: its whole-wave rows (all of it when it does not split); 2: the wave-split remainder
+// rows (nothing when it does not split)
+int gemm_bf16_impl(const vit_gemm_args* a, int part, vit_stream_t stream) {
+  GemmDev d;
+  bool empty = false;
+  if (const int rc = make_dev(a, d, empty)) return rc;
+  if (empty) return VIT_OK;
+  const bool ak = a->a_layout == VIT_K_CONTIG, bk = a->b_layout == VIT_K_CONTIG;
   if (a->col_partial) {
     VIT_CHECK_ARG(a->batch == 1 && a->split_k == 1 && d.vec && a->N % 8 == 0 &&
                       (a->epilogue == VIT_EPI_F32 || a->epilogue == VIT_EPI_BF16 || a->epilogue == VIT_EPI_GELU_BWD ||
@@ -272,6 +286,29 @@ extern "C" int vit_gemm_bf16(const vit_gemm_args* a, vit_stream_t stream) { retu
 extern "C" int vit_gemm_bf16_part(const vit_gemm_args* a, int32_t part, vit_stream_t stream) {
   VIT_CHECK_ARG(part == 1 || part == 2, "vit_gemm_bf16_part: part %d (1 = whole-wave rows, 2 = remainder)", part);
   return gemm_bf16_impl(a, part, stream);
+}
+
+extern "C" int vit_gemm_splitk_group(const vit_gemm_args* args, int32_t n, vit_stream_t stream) {
+  VIT_CHECK_ARG(args != nullptr && n >= 1 && n <= vitg::GEMM_GROUP_MAX, "vit_gemm_splitk_group: 1..%d members, got %d",
+                vitg::GEMM_GROUP_MAX, n);
+  vitg::GemmGroup g{};
+  long total = 0;
+  for (int i = 0; i < n; ++i) {
+    const vit_gemm_args* a = args + i;
+    VIT_CHECK_ARG(a->epilogue == VIT_EPI_SPLITK && a->a_layout == VIT_MN_CONTIG && a->b_layout == VIT_MN_CONTIG &&
+                      a->M >= 256 && a->N >= 256 && a->tile == 0 && !a->col_partial && !a->dropout,
+                  "vit_gemm_splitk_group: member %d must be a split-K weight gradient (VIT_EPI_SPLITK, both operands "
+                  "M/N-contiguous, M and N >= 256, no tile / col_partial / dropout)", i);
+    bool empty = false;
+    if (const int rc = make_dev(a, g.g[i], empty)) return rc;
+    VIT_CHECK_ARG(!empty, "vit_gemm_splitk_group: member %d is empty", i);
+    g.start[i] = (int)total;
+    total += ((a->M + 255) / 256) * ((a->N + 255) / 256) * a->split_k * a->batch;
+    VIT_CHECK_ARG(total < (1L << 30), "vit_gemm_splitk_group: grid too large");
+  }
+  g.start[n] = (int)total;
+  g.n = n;
+  return vit::check_hip(vitg::launch_splitk_group(g, (hipStream_t)stream), "vit_gemm_splitk_group launch");
 }
 
 // ---- split-K reduction -------------------------------------------------------------------------

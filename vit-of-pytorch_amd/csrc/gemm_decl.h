@@ -53,6 +53,16 @@ struct GemmDev {
   int prio;            // s_setprio(1) around the ping-pong kernels' MFMA clusters (VIT_GEMM_PRIO)
 };
 
+// a group of split-K GEMMs launched as one grid (vit_gemm_splitk_group): member i owns workgroup positions
+// [start[i], start[i + 1])
+constexpr int GEMM_GROUP_MAX = 4;
+struct GemmGroup {
+  GemmDev g[GEMM_GROUP_MAX];
+  int start[GEMM_GROUP_MAX + 1];
+  int n;
+};
+hipError_t launch_splitk_group(const GemmGroup& g, hipStream_t s);
+
 // Internal epilogue flag: the dropout variant of PATCH / BIAS_RESID_F32 / BIAS_GELU_DGELU (its own
 // instantiation, so the dropout-free kernels carry none of the Philox code)
 constexpr int EPI_DROP = 16;

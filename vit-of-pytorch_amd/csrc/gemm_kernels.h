@@ -4,6 +4,8 @@
 
 namespace {
 using vitg::GemmDev;
+using vitg::GemmGroup;
+using vitg::GEMM_GROUP_MAX;
 
 // blockIdx (after the XCD remap) -> output tile. Grouping tile rows keeps the weight panels a
 // group's concurrent workgroups share hot in the XCD's L2.

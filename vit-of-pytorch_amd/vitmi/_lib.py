@@ -17,7 +17,7 @@ c_i32 = ctypes.c_int32
 c_f32 = ctypes.c_float
 c_vp = ctypes.c_void_p
 
-ABI_VERSION = 10  # vit_abi_version() of the library these prototypes describe
+ABI_VERSION = 11  # vit_abi_version() of the library these prototypes describe
 
 # enum vit_layout / vit_epilogue (include/vit_hip.h)
 K_CONTIG, MN_CONTIG = 0, 1
@@ -63,6 +63,7 @@ _SIGS = {
     "vit_gemm_partial_rows": (c_i64, [ctypes.POINTER(GemmArgs)]),
     "vit_gemm_split_rows": (c_i64, [ctypes.POINTER(GemmArgs)]),
     "vit_gemm_bf16_part": (c_i32, [ctypes.POINTER(GemmArgs), c_i32, c_vp]),
+    "vit_gemm_splitk_group": (c_i32, [ctypes.POINTER(GemmArgs), c_i32, c_vp]),
     "vit_splitk_reduce": (c_i32, [c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_i64, c_i64, c_i32, c_vp]),
     "vit_layernorm_fwd": (c_i32, [c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_i32, c_vp, c_vp, c_i64, c_i64, c_f32, c_vp]),
     "vit_layernorm_bwd_partial_rows": (c_i64, [c_i64]),

@@ -289,6 +289,9 @@ class ViTEngine:
         # alone, so the serial order is faster on one MI355X (B/16 bs256: 6778 vs 6588 img/s,
         # tools/sweep_env.sh). The DP all-reduce keeps its own stream either way (vitmi/dist.py).
         self.overlap_wgrad = os.environ.get("VITMI_OVERLAP", "0") == "1"
+        # each layer's out-projection and q|k|v weight gradients in one split-K launch (ops.gemm_splitk_group);
+        # VITMI_GROUP_WGRAD=0: two launches
+        self.group_wgrad = os.environ.get("VITMI_GROUP_WGRAD", "1") != "0"
         # Only the cls token of the last layer's output reaches the classifier (src/model.py:210),
         # so that layer's out-projection, LayerNorm 2 and MLP (forward and backward) run on the b cls
         # rows and its attention on the first 32-query pair of each (image, head) (q_rows = 1); the
@@ -394,6 +397,36 @@ class ViTEngine:
             ev1.record()
             self.probe_wgrad.append((ev0, ev1, 2.0 * M * N * K * batch, K))
         ops.splitk_reduce(ws, batch, s, M, N, out, ldo, out_bs)
+
+    def _wgrad_group(self, specs):
+        """Several _wgrad calls over the same K (token rows) as ONE split-K launch (ops.gemm_splitk_group) at a
+        common split (ops.splitk_factor_group), then each member's fixed-order reduction. specs: [(A, lda, B, ldb,
+        M, N, K, out, ldo, batch, b_bs, out_bs)]. Each output equals its _wgrad's up to the split (same slabs
+        summed in the same order when the splits agree)."""
+        K = specs[0][6]
+        assert all(sp[6] == K for sp in specs)
+        s = ops.splitk_factor_group([(sp[4], sp[5], sp[9]) for sp in specs], K, _WGRAD_TARGET)
+        sizes = [sp[9] * s * sp[4] * sp[5] for sp in specs]
+        ws = self._workspace(sum(sizes))
+        members, views, o = [], [], 0
+        for sp, n in zip(specs, sizes):
+            A, lda, B, ldb, M, N, _, _, _, batch, b_bs, _ = sp
+            w = ws[o:o + n]
+            o += n
+            views.append(w)
+            members.append((A, B, w, M, N, K, dict(a_layout=MN_CONTIG, b_layout=MN_CONTIG, lda=lda, ldb=ldb, ldc=N,
+                                                    epilogue=EPI_SPLITK, batch=batch, b_bs=b_bs, split_k=s)))
+        if self.probe_wgrad is not None:
+            ev0 = torch.cuda.Event(enable_timing=True)
+            ev0.record()
+        ops.gemm_splitk_group(members)
+        if self.probe_wgrad is not None:
+            ev1 = torch.cuda.Event(enable_timing=True)
+            ev1.record()
+            self.probe_wgrad.append((ev0, ev1, sum(2.0 * sp[4] * sp[5] * K * sp[9] for sp in specs), K))
+        for sp, w in zip(specs, views):
+            _, _, _, _, M, N, _, out, ldo, batch, _, out_bs = sp
+            ops.splitk_reduce(w, batch, s, M, N, out, ldo, out_bs)
 
     # ---- forward -------------------------------------------------------------------------------
     def _dd(self, site, row_stride=1):
@@ -640,6 +673,8 @@ class ViTEngine:
             hook(g, *bucket, evs)
 
         self._ev_next = 0  # the event pool is reused from the start by every backward
+        group = self.group_wgrad and D >= 256  # (the grouped kernel takes M, N >= 256)
+        out_wb = None  # dhb buffer of a deferred out-projection weight gradient (group)
         bias = _BiasReducer(self, a)
         # classifier head (f32): dWc = dl^T lncls, dbc = colsum(dl), dlncls = dl Wc
         ops.gemm_f32(C, D, b, dl, C, True, a.lncls, D, False, gv("classifier.weight"), D)
@@ -691,8 +726,12 @@ class ViTEngine:
                             gv(self.lname(i, "norm2.weight")), gv(self.lname(i, "attn.out.bias")),
                             dres=a.dh, lddres=D, dx_bf16=dhb, lddxb=D, dx_dropout=dd(1 + 3 * i))
                 # ---- attention: hm = h + out(attn(ln1(h))) ----
-                on_side(lambda: self._wgrad(a.o[i], D, dhb, D, D, D, a.Tp, gv(self.lname(i, "attn.out.weight")), D))
-                release("dhb", wb)
+                out_spec = (a.o[i], D, dhb, D, D, D, a.Tp, gv(self.lname(i, "attn.out.weight")), D, 1, 0, 0)
+                if group:  # launched with the q|k|v weight gradient below (dhb stays intact until then)
+                    out_wb = wb
+                else:
+                    on_side(lambda: self._wgrad(*out_spec[:9]))
+                    release("dhb", wb)
                 ops.gemm(dhb, mv[ln("attn.out.weight"):], a.dO, T, D, D, a_layout=K_CONTIG, b_layout=K_CONTIG, lda=D,
                          ldb=D, ldc=D, epilogue=EPI_BF16)
             dqkv = a.dqkv[li]
@@ -704,9 +743,17 @@ class ViTEngine:
             zs = ln("attn.key.weight") - qo
             qb = ln("attn.query.bias")
             bias.reduce(qpart, b * a.attn_bias_rows, 3 * D, 3 * D, (g[qb:], g[qb + zs:], g[qb + 2 * zs:]), seg=D)
-            on_side(lambda: self._wgrad(a.ln1[i], D, dqkv, 3 * D, D, D, a.Tp, g[qo:], D, batch=3, b_bs=D,
-                                        out_bs=zs))
-            release("dqkv", li)
+            qkv_spec = (a.ln1[i], D, dqkv, 3 * D, D, D, a.Tp, g[qo:], D, 3, D, zs)
+            if out_wb is not None:
+                # the out-projection (9 tiles at B/16) and q|k|v (27) weight gradients as one grid: one wave of
+                # 252 workgroups at split 7 instead of 252 short ones (split 28) and 243 (split 9)
+                on_side(lambda: self._wgrad_group([out_spec, qkv_spec]))
+                release("dqkv", li)
+                release("dhb", out_wb)
+                out_wb = None
+            else:
+                on_side(lambda: self._wgrad(*qkv_spec[:9], batch=3, b_bs=D, out_bs=zs))
+                release("dqkv", li)
             ops.gemm(dqkv, self.wqkv[i], a.dyln, T, D, 3 * D, a_layout=K_CONTIG, b_layout=K_CONTIG, lda=3 * D,
                      ldb=3 * D, ldc=D, epilogue=EPI_BF16)
             wb ^= 1

@@ -378,6 +378,35 @@ def zero_(t):
     check(lib().vit_zero(_p(t), t.numel() * t.element_size(), _stream()), "vit_zero")
 
 
+def splitk_factor_group(shapes, K, cus=256):
+    """common split-K factor of weight-gradient GEMMs [(M, N, batch), ...] over the same K launched as one grid
+    (vit_gemm_splitk_group; M, N >= 256): splitk_factor's model over their summed tiles and slabs"""
+    tiles = sum(-(-M // 256) * -(-N // 256) * b for M, N, b in shapes)
+    smax = max(1, min((K // 64) // 8, 32))
+    t_tile = 2.0 * 256 * 256 * K / 4.0e12
+    slab = sum(2.0 * M * N * 4 * b for M, N, b in shapes) / 5.0e12
+    best, best_t = 1, None
+    for s in range(1, smax + 1):
+        t = -(-tiles * s // cus) * t_tile / s + s * slab
+        if best_t is None or t < best_t * (1 - 1e-9):
+            best, best_t = s, t
+    return best
+
+
+def gemm_splitk_group(members):
+    """Up to 4 split-K weight-gradient GEMMs in one launch (vit_gemm_splitk_group). members: [(A, B, C, M, N, K,
+    kwargs)], each exactly a gemm(A, B, C, M, N, K, **kwargs) call with epilogue EPI_SPLITK and both operands
+    M/N-contiguous; the grid is the concatenation of theirs."""
+    if not 1 <= len(members) <= 4:
+        raise ValueError("gemm_splitk_group: 1 to 4 members")
+    arr = (GemmArgs * len(members))()
+    for i, (A, B, C, M, N, K, kw) in enumerate(members):
+        _chk(A, BF16, "A")
+        _chk(B, BF16, "B")
+        arr[i] = _gemm_args(A, B, C, M, N, K, **kw)
+    check(lib().vit_gemm_splitk_group(arr, len(members), _stream()), "vit_gemm_splitk_group")
+
+
 def splitk_factor(M, N, K, batch=1, cus=256):
     """split-K factor of a weight-gradient GEMM (K = tokens) on `cus` compute units: the split with the
     least modelled time, ceil(tiles*s / slots) waves of 1/s of a tile's k-range each plus the f32 slab
