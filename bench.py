@@ -331,8 +331,9 @@ def main():
         d_["gflop"] = round(d_["gflop"], 2)
     fc1_flop = 2.0 * T * cfg.emb_dim * cfg.mlp_dim
     fc1_tflops = fc1_flop / (fc1_ms * 1e-3) / 1e12
-    # the step's dominant kernel by time: the split-K weight-gradient GEMM (gemm_pp2_kernel; ~20% of the
-    # step), every launch of the timed steps; achieved = its algorithmic FLOPs / its own time
+    # the step's dominant kernel by time: the split-K weight-gradient GEMMs (gemm_pp2_kernel<false, false, 7> and
+    # the grouped gemm_pp2_group_kernel; ~20% of the step), every launch of the probe step; achieved = their
+    # algorithmic FLOPs / their own time
     # headline: the launches over all T tokens (K = T rounded up to 64); the pruned last layer's
     # launches (K = the b cls rows padded to 64) are reported beside it, not averaged in
     full_w = [p_ for p_ in probe_w if p_[3] >= T]
@@ -377,11 +378,11 @@ def main():
                    "parallelism": f"dp{world}", "dist_backend": backend,
                    "step_launch": "one HIP graph per step" if use_graph else "eager",
                    **({"grad_allreduce_dtype": "bf16"} if compress and world > 1 else {})},
-        "roofline": {"bound": "mfma", "kernel": "split-K weight-gradient GEMM gemm_pp2_kernel (the step's dominant "
-                                                f"kernel): the {len(wg_ms)} launches over all tokens of one step "
-                                                f"(HIP events, an eager step after the timed region), K = {T} tokens "
-                                                "padded to 64; fc1 / fc2 / "
-                                                "out-proj weights one GEMM each, q|k|v three GEMMs in one batched launch",
+        "roofline": {"bound": "mfma", "kernel": "split-K weight-gradient GEMMs (the step's dominant kernel family): "
+                                                f"the {len(wg_ms)} launches over all tokens of one step (HIP events, an "
+                                                f"eager step after the timed region), K = {T} tokens padded to 64; fc1 "
+                                                "and fc2 one gemm_pp2_kernel<false, false, 7> launch each, each layer's "
+                                                "out-proj + q|k|v (three batched GEMMs) one gemm_pp2_group_kernel launch",
                      "achieved": round(wg_tflops, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                      "frac": round(wg_tflops / PEAK_BF16_TFLOPS, 4), "traffic": (traffic_w or {}).get("bytes"),
                      "traffic_detail": traffic_w,

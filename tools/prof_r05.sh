@@ -24,7 +24,7 @@ python3 tools/prof_summary.py $S 13 > $O/kernel_summary.txt
 python3 tools/trace_step.py $T 3 $O/step_launches.txt > $O/step_timeline.txt
 cp $S $O/kernel_stats.csv
 rm -rf $O/ktrace
-RX='gemm_pp2_kernel<false, false, 7|gemm_\w+_kernel<.*true, true, 8|attn_bwd_pers_kernel'
+RX='gemm_pp2_kernel<false, false, 7|gemm_pp2_group_kernel|gemm_\w+_kernel<.*true, true, 8|attn_bwd_pers_kernel'
 step "pmc fetch" timeout -k 10 -s KILL 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$RX" --output-format csv -d $O/fetch -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > $O/fetch.log 2>&1
 step "pmc write" timeout -k 10 -s KILL 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$RX" --output-format csv -d $O/write -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > $O/write.log 2>&1
 step "pmc mfma" timeout -k 10 -s KILL 300 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_BUSY_CYCLES --kernel-include-regex "$RX" --output-format csv -d $O/mfma -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > $O/mfma.log 2>&1
@@ -34,11 +34,12 @@ M=$(find $O/mfma -name "*counter_collection.csv" | head -1)
 python3 tools/pmc_traffic.py 'gemm_pp2_kernel<false, false, 7' $F $W $O/wgrad_traffic.json > /dev/null
 python3 tools/pmc_traffic.py 'gemm_\w+_kernel<.*true, true, 8' $F $W $O/fc1_traffic.json > /dev/null
 python3 tools/pmc_traffic.py 'attn_bwd_pers_kernel' $F $W $O/attn_bwd_traffic.json > /dev/null
+python3 tools/pmc_traffic.py 'gemm_pp2_group_kernel' $F $W $O/wgrad_group_traffic.json > /dev/null
 python3 tools/kernel_pmc.py $O/kernel_pmc.txt $F $W $M
 cp $F $O/fetch.csv; cp $W $O/write.csv; cp $M $O/mfma.csv
 rm -rf $O/fetch $O/write $O/mfma
 head -30 $O/kernel_summary.txt; head -4 $O/step_timeline.txt
-python3 -c "import json;[print(k, round(json.load(open('$O/'+k))['traffic_bytes']/1e6,1),'MB') for k in ['wgrad_traffic.json','fc1_traffic.json','attn_bwd_traffic.json']]"
+python3 -c "import json;[print(k, round(json.load(open('$O/'+k))['traffic_bytes']/1e6,1),'MB') for k in ['wgrad_traffic.json','wgrad_group_traffic.json','fc1_traffic.json','attn_bwd_traffic.json']]"
 head -30 $O/kernel_pmc.txt
 # same-box A/B: the whole B/16 step replayed from one HIP graph (VITMI_BENCH_GRAPH=1) vs eager launches
 [ "$3" == "graph" ] || exit 0
