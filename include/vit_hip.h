@@ -141,9 +141,10 @@ int64_t vit_gemm_split_rows(const vit_gemm_args* args);
  * the whole-wave rows) */
 int vit_gemm_bf16_part(const vit_gemm_args* args, int32_t part, vit_stream_t stream);
 /* up to 4 split-K weight-gradient GEMMs in ONE launch (the concatenation of their grids): each member is a
- * vit_gemm_bf16 call with epilogue VIT_EPI_SPLITK, both operands M/N-contiguous, M, N >= 256, its own split_k /
- * batch, and writes exactly what that call writes (the same f32 slabs). Fills the CUs where members alone leave a
- * wave partly empty (the out-projection and q|k|v weight gradients of one layer) */
+ * vit_gemm_bf16 call with epilogue VIT_EPI_SPLITK and both operands M/N-contiguous, its own split_k / batch, and
+ * writes exactly what that call writes (the same f32 slabs; every member on 256 x 256 tiles, M or N below 256 as
+ * partial tiles). Fills the CUs where members alone leave a wave partly empty (the out-projection and q|k|v weight
+ * gradients of one layer; the Res-ViT router's four weight gradients) */
 int vit_gemm_splitk_group(const vit_gemm_args* args, int32_t n, vit_stream_t stream);
 
 /* out[z*out_batch_stride + m*ldo + n] (+)= sum_s ws[((z*split + s)*M + m)*N + n]  (f32) */
@@ -363,6 +364,19 @@ int vit_dropout_apply_f32(const vit_dropout* d, const float* in, float* out, int
                           vit_stream_t stream);
 /* out[o*inner + i] = x[o*inner + i] + y[i]  (PositionEmbs: x + pos_embedding, src/model.py:17) */
 int vit_add_bcast_f32(const float* x, const float* y, float* out, int64_t outer, int64_t inner, vit_stream_t stream);
+/* Res-ViT router backward (res-vit/model.py:186-190, the global half of out_conv's input):
+ * vit_segment_colsum: out[s*ldo + c] = sum_{r < seg_rows} in[(s*seg_rows + r)*ld + c] (per-image token sums; f32
+ *   or bf16 in, rows in order);
+ * vit_router_dx_gate: out (bf16 [rows_pad][cols_pad], ld ldo) = bf16((dx[t][c] + [t % N >= reserve] g_scale
+ *   g[t / N][c]) * gp[t][c]) for t < T, c < cols, zero elsewhere (in_conv's input-gradient times its saved GELU');
+ *   optional col_partial[b*ldp + c] = column sums of the rounded values over row block b
+ *   (vit_router_dx_gate_partial_rows(rows_pad) blocks; reduce with vit_colsum_batch) */
+int vit_segment_colsum(const void* in, int32_t in_bf16, int64_t ld, int64_t segs, int64_t seg_rows, int64_t cols,
+                       float* out, int64_t ldo, vit_stream_t stream);
+int64_t vit_router_dx_gate_partial_rows(int64_t rows_pad);
+int vit_router_dx_gate(const float* dx, int64_t ldx, const float* g, int64_t ldg, float g_scale, const void* gp,
+                       int64_t ldgp, int64_t T, int64_t N, int64_t reserve, int64_t cols, void* out, int64_t ldo,
+                       int64_t rows_pad, int64_t cols_pad, float* col_partial, int64_t ldp, vit_stream_t stream);
 /* out[r*ldo + c] = f32(in[r*ldi + c]) for bf16 `in` (attention outputs / gradients back to f32 modules) */
 int vit_unpack_bf16_f32(const void* in, int64_t ldi, int64_t rows, int64_t cols, float* out, int64_t ldo,
                         vit_stream_t stream);

@@ -168,6 +168,59 @@ def test_gemm_splitk_group_equals_members():
         ops.gemm_splitk_group([(A1.t().contiguous(), B1, g1, D, D, K, bad)])
 
 
+def test_gemm_splitk_group_small_members():
+    """the Res-ViT router's weight gradients as one group: members narrower than a tile (M = 2: the 2-logit layer;
+    N = 512) run as partial 256 x 256 tiles and match their own calls bit for bit"""
+    from vitmi._lib import EPI_SPLITK
+    g = torch.Generator(device="cpu").manual_seed(11)
+    K, S = 640, 2
+    shapes = [(2, 256, 64, 256), (256, 512, 256, 512), (512, 768, 512, 768)]  # (M, N, lda, ldb)
+    members, refs = [], []
+    for M, N, lda, ldb in shapes:
+        A = torch.randn(K, lda, generator=g).bfloat16().to(DEV)
+        B = torch.randn(K, ldb, generator=g).bfloat16().to(DEV)
+        kw = dict(a_layout=MN_CONTIG, b_layout=MN_CONTIG, lda=lda, ldb=ldb, ldc=N, epilogue=EPI_SPLITK, split_k=S)
+        w = torch.empty(S, M, N, device=DEV)
+        ops.gemm(A, B, w, M, N, K, **kw)
+        refs.append((w, A[:, :M].float().t() @ B[:, :N].float()))
+        members.append((A, B, torch.full_like(w, float("nan")), M, N, K, kw))
+    ops.gemm_splitk_group(members)
+    for (_, _, out, *_), (w, ref) in zip(members, refs):
+        assert torch.equal(out, w)
+        assert rel(out.sum(0), ref) < 1e-5
+
+
+def test_segment_colsum_and_router_dx_gate():
+    """the Res-ViT router backward helpers against torch: per-image token sums (bf16 and f32 inputs), and
+    bf16((dx + [t % N >= reserve] s g[t // N]) * gp) with zero padding and per-64-row column partials of the
+    rounded values"""
+    g = torch.Generator(device="cpu").manual_seed(5)
+    Bn, N, C, ld = 3, 50, 200, 264
+    x = torch.randn(Bn * N, ld, generator=g).to(DEV)
+    for inp in (x, x.bfloat16()):
+        out = torch.full((Bn, C + 8), float("nan"), device=DEV)
+        ops.segment_colsum(inp, ld, Bn, N, C, out, C + 8)
+        ref = inp[:, :C].float().view(Bn, N, C).sum(1)
+        assert torch.allclose(out[:, :C], ref, rtol=1e-5, atol=1e-4)
+        assert torch.isnan(out[:, C:]).all()
+    T, reserve, scale = Bn * N, 2, 1.0 / 48
+    rows_pad, cols_pad = 192, 256
+    dx = torch.randn(T, C, generator=g).to(DEV)
+    gs = torch.randn(Bn, C, generator=g).to(DEV)
+    gp = torch.randn(rows_pad, cols_pad, generator=g).bfloat16().to(DEV)
+    out = torch.full((rows_pad, cols_pad), float("nan"), device=DEV).bfloat16()
+    nb = ops.router_dx_gate_partial_rows(rows_pad)
+    part = torch.full((nb, C), float("nan"), device=DEV)
+    ops.router_dx_gate(dx, C, gs, C, scale, gp, cols_pad, T, N, reserve, C, out, cols_pad, part, C)
+    keep = (torch.arange(T, device=DEV) % N >= reserve).float()[:, None]
+    ref = ((dx + keep * scale * gs.repeat_interleave(N, 0)) * gp[:T, :C].float()).bfloat16()
+    assert torch.equal(out[:T, :C], ref)
+    assert (out[T:].float() == 0).all() and (out[:, C:].float() == 0).all()
+    full = torch.zeros(rows_pad, C, device=DEV)
+    full[:T] = ref.float()
+    assert torch.allclose(part, full.view(nb, 64, C).sum(1), rtol=1e-5, atol=1e-4)
+
+
 @pytest.mark.parametrize("tile", [1, 2, 6, 9])
 def test_gemm_tiles_epilogue_splitk(tile):
     M, N, K = 700, 520, 512

@@ -120,7 +120,7 @@ def test_train_step_matches_reference(golden):
     c, a, d, ent, metric = m(x, y)
     (10.0 * c + 10.0 * a + 1.0 * d).backward()
     assert rel(m.logits, golden["train/logits"]) < 1e-2
-    assert abs(float(c) - float(golden["train/c_loss"])) <= 1e-3 * float(golden["train/c_loss"])
+    assert abs(float(c.detach()) - float(golden["train/c_loss"])) <= 1e-3 * float(golden["train/c_loss"])
     assert abs(float(d) - float(golden["train/d_loss"])) <= 1e-2 * float(golden["train/d_loss"])
     assert abs(float(a) - float(golden["train/a_loss"])) <= 1e-2 * float(golden["train/a_loss"]) + 1e-6
     assert abs(float(ent) - float(golden["train/r_entropy"])) <= 1e-2 * abs(float(golden["train/r_entropy"])) + 1e-6

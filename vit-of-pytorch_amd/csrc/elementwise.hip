@@ -954,6 +954,87 @@ extern "C" int vit_add_bcast_f32(const float* x, const float* y, float* out, int
   VIT_LAUNCH_CHECK("vit_add_bcast_f32");
 }
 
+// ---- Res-ViT router backward helpers (res-vit/model.py:186-190 RouterModule: the global half of out_conv's
+// input and in_conv's GELU) ------------------------------------------------------------------------------------
+namespace {
+// out[s][c] = sum over the seg_rows rows of segment s of in[row][c], rows in order (deterministic)
+template <bool BF16>
+__global__ void __launch_bounds__(256) segment_colsum_kernel(const void* __restrict__ in, long ld, long seg_rows,
+                                                             int cols, float* __restrict__ out, long ldo) {
+  const int c = blockIdx.y * 256 + threadIdx.x;
+  if (c >= cols) return;
+  const long r0 = (long)blockIdx.x * seg_rows;
+  float acc = 0.f;
+  for (long r = 0; r < seg_rows; ++r) {
+    const long i = (r0 + r) * ld + c;
+    acc += BF16 ? bf2f(((const bf16_t*)in)[i]) : ((const float*)in)[i];
+  }
+  out[(long)blockIdx.x * ldo + c] = acc;
+}
+
+// out (bf16 [rows_pad][cols_pad]) = (dx[t][c] + [t % N >= reserve] * g_scale * g[t / N][c]) * gp[t][c] on the T x cols
+// block, rounded once to bf16, zero elsewhere; col_partial[blockIdx.y][c] = the column sums of the rounded values of
+// the block's RB rows (column c: thread c of the 256-column group)
+constexpr int RDG_RB = 64;
+__global__ void __launch_bounds__(256) router_dx_gate_kernel(const float* __restrict__ dx, long ldx,
+                                                             const float* __restrict__ g, long ldg, float g_scale,
+                                                             const bf16_t* __restrict__ gp, long ldgp, long T, long N,
+                                                             long reserve, int cols, bf16_t* __restrict__ out,
+                                                             long ldo, long rows_pad, int cols_pad,
+                                                             float* __restrict__ col_partial, long ldp) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= cols_pad) return;
+  const long r0 = (long)blockIdx.y * RDG_RB;
+  const long r1 = r0 + RDG_RB < rows_pad ? r0 + RDG_RB : rows_pad;
+  float acc = 0.f;
+  for (long t = r0; t < r1; ++t) {
+    bf16_t o = 0;
+    if (t < T && c < cols) {
+      float v = dx[t * ldx + c];
+      if (t % N >= reserve) v += g_scale * g[(t / N) * ldg + c];
+      o = f2bf(v * bf2f(gp[t * ldgp + c]));
+      acc += bf2f(o);
+    }
+    out[t * ldo + c] = o;
+  }
+  if (col_partial && c < cols) col_partial[blockIdx.y * ldp + c] = acc;
+}
+}  // namespace
+
+extern "C" int vit_segment_colsum(const void* in, int32_t in_bf16, int64_t ld, int64_t segs, int64_t seg_rows,
+                                  int64_t cols, float* out, int64_t ldo, vit_stream_t stream) {
+  VIT_CHECK_ARG(in && out && segs >= 0 && seg_rows >= 0 && cols > 0 && ld >= cols && ldo >= cols &&
+                    cols < (1L << 30),
+                "vit_segment_colsum: bad args");
+  if (segs == 0) return VIT_OK;
+  const dim3 grid((unsigned)segs, (unsigned)((cols + 255) / 256));
+  if (in_bf16)
+    hipLaunchKernelGGL(segment_colsum_kernel<true>, grid, dim3(256), 0, (hipStream_t)stream, in, (long)ld,
+                       (long)seg_rows, (int)cols, out, (long)ldo);
+  else
+    hipLaunchKernelGGL(segment_colsum_kernel<false>, grid, dim3(256), 0, (hipStream_t)stream, in, (long)ld,
+                       (long)seg_rows, (int)cols, out, (long)ldo);
+  VIT_LAUNCH_CHECK("vit_segment_colsum");
+}
+
+extern "C" int64_t vit_router_dx_gate_partial_rows(int64_t rows_pad) { return (rows_pad + RDG_RB - 1) / RDG_RB; }
+
+extern "C" int vit_router_dx_gate(const float* dx, int64_t ldx, const float* g, int64_t ldg, float g_scale,
+                                  const void* gp, int64_t ldgp, int64_t T, int64_t N, int64_t reserve, int64_t cols,
+                                  void* out, int64_t ldo, int64_t rows_pad, int64_t cols_pad, float* col_partial,
+                                  int64_t ldp, vit_stream_t stream) {
+  VIT_CHECK_ARG(dx && g && gp && out && T >= 0 && N > 0 && reserve >= 0 && cols > 0 && cols_pad >= cols &&
+                    rows_pad >= T && ldx >= cols && ldg >= cols && ldgp >= cols && ldo >= cols_pad &&
+                    (!col_partial || ldp >= cols) && cols_pad < (1L << 30),
+                "vit_router_dx_gate: bad args");
+  if (rows_pad == 0) return VIT_OK;
+  const dim3 grid((unsigned)((cols_pad + 255) / 256), (unsigned)vit_router_dx_gate_partial_rows(rows_pad));
+  hipLaunchKernelGGL(router_dx_gate_kernel, grid, dim3(256), 0, (hipStream_t)stream, dx, (long)ldx, g, (long)ldg,
+                     g_scale, (const bf16_t*)gp, (long)ldgp, (long)T, (long)N, (long)reserve, (int)cols, (bf16_t*)out,
+                     (long)ldo, (long)rows_pad, (int)cols_pad, col_partial, (long)ldp);
+  VIT_LAUNCH_CHECK("vit_router_dx_gate");
+}
+
 namespace {
 __global__ void unpack_bf16_f32_kernel(const bf16_t* __restrict__ in, long ldi, long rows, int cols,
                                        float* __restrict__ out, long ldo) {

@@ -296,9 +296,9 @@ extern "C" int vit_gemm_splitk_group(const vit_gemm_args* args, int32_t n, vit_s
   for (int i = 0; i < n; ++i) {
     const vit_gemm_args* a = args + i;
     VIT_CHECK_ARG(a->epilogue == VIT_EPI_SPLITK && a->a_layout == VIT_MN_CONTIG && a->b_layout == VIT_MN_CONTIG &&
-                      a->M >= 256 && a->N >= 256 && a->tile == 0 && !a->col_partial && !a->dropout,
+                      a->tile == 0 && !a->col_partial && !a->dropout,
                   "vit_gemm_splitk_group: member %d must be a split-K weight gradient (VIT_EPI_SPLITK, both operands "
-                  "M/N-contiguous, M and N >= 256, no tile / col_partial / dropout)", i);
+                  "M/N-contiguous, no tile / col_partial / dropout)", i);
     bool empty = false;
     if (const int rc = make_dev(a, g.g[i], empty)) return rc;
     VIT_CHECK_ARG(!empty, "vit_gemm_splitk_group: member %d is empty", i);

@@ -326,6 +326,29 @@ def add_bcast_f32(x, y, out, outer, inner):
     check(lib().vit_add_bcast_f32(_p(x), _p(y), _p(out), outer, inner, _stream()), "vit_add_bcast_f32")
 
 
+def segment_colsum(inp, ld, segs, seg_rows, cols, out, ldo):
+    """out[s][c] = sum of rows [s*seg_rows, (s+1)*seg_rows) of inp's column c (f32 or bf16 inp; rows in order)"""
+    _chk(out, F32, "out")
+    check(lib().vit_segment_colsum(_p(inp), int(inp.dtype == BF16), ld, segs, seg_rows, cols, _p(out), ldo, _stream()),
+          "vit_segment_colsum")
+
+
+def router_dx_gate_partial_rows(rows_pad):
+    return int(lib().vit_router_dx_gate_partial_rows(rows_pad))
+
+
+def router_dx_gate(dx, ldx, g, ldg, g_scale, gp, ldgp, T, N, reserve, cols, out, ldo, col_partial=None, ldp=0):
+    """out (bf16 [rows_pad][cols_pad]) = bf16((dx + [t % N >= reserve] g_scale g[t // N]) * gp) on [T][cols], zeros
+    in the padding; col_partial: per 64-row block column sums of the rounded values (vit_router_dx_gate)"""
+    _chk(dx, F32, "dx")
+    _chk(g, F32, "g")
+    _chk(gp, BF16, "gp")
+    _chk(out, BF16, "out")
+    check(lib().vit_router_dx_gate(_p(dx), ldx, _p(g), ldg, float(g_scale), _p(gp), ldgp, T, N, reserve, cols, _p(out),
+                                   ldo, out.shape[0], out.shape[1], _p(col_partial), ldp, _stream()),
+          "vit_router_dx_gate")
+
+
 def unpack_bf16_f32(inp, ldi, rows, cols, out, ldo):
     """out[r*ldo + c] = f32(inp[r*ldi + c])"""
     _chk(inp, BF16, "inp")
@@ -380,7 +403,7 @@ def zero_(t):
 
 def splitk_factor_group(shapes, K, cus=256):
     """common split-K factor of weight-gradient GEMMs [(M, N, batch), ...] over the same K launched as one grid
-    (vit_gemm_splitk_group; M, N >= 256): splitk_factor's model over their summed tiles and slabs"""
+    (vit_gemm_splitk_group, 256 x 256 tiles): splitk_factor's model over their summed tiles and slabs"""
     tiles = sum(-(-M // 256) * -(-N // 256) * b for M, N, b in shapes)
     smax = max(1, min((K // 64) // 8, 32))
     t_tile = 2.0 * 256 * 256 * K / 4.0e12

@@ -32,7 +32,7 @@ import torch
 from . import flat as _flat
 from . import ops
 from ._lib import (EPI_BF16, EPI_BIAS_BF16, EPI_BIAS_GELU_DGELU, EPI_BIAS_RESID_F32, EPI_F32, EPI_MUL_BF16,
-                   K_CONTIG, MN_CONTIG)
+                   EPI_SPLITK, K_CONTIG, MN_CONTIG)
 
 BF16, F32 = torch.bfloat16, torch.float32
 KX = 64  # extra K columns of the q|k|v operand (LoRA down-projections, zero padded)
@@ -459,14 +459,23 @@ def _sunk(marks):
         _flat.sunk(p)
 
 
+def _weight_pads(w1, w2, w3, kp, h1p, h2p):
+    """bf16 [rows rounded to 64][cols] copies of the out_conv weights (zero padding): the forward GEMMs' K-contiguous
+    B operands and, unchanged, the backward's M/N-contiguous B operands of the data gradients (K = the padded output
+    rows)"""
+    H1, H2, O = w1.shape[0], w2.shape[0], w3.shape[0]
+    return [_pad_bf16(w.detach().float().contiguous(), _rup(n, 64), k)
+            for w, n, k in ((w1, H1, kp), (w2, H2, h1p), (w3, O, h2p))]
+
+
 def _mlp_forward(xb, T, kp, w1, b1, w2, b2, w3, b3):
     """the router's out_conv on a bf16 operand xb [rp][kp] (T valid rows): hidden layers as one GEMM each whose
     epilogue writes GELU(u) (the next operand) and GELU'(u) (kept for the backward); returns (logits f32 [T][O],
-    saved activations)"""
+    saved activations, padded bf16 weights)"""
     rp, dev = xb.shape[0], xb.device
     H1, H2, O = w1.shape[0], w2.shape[0], w3.shape[0]
     h1p, h2p = _rup(H1, 64), _rup(H2, 64)
-    ws = [_pad_bf16(w.detach().float().contiguous(), n, k) for w, n, k in ((w1, H1, kp), (w2, H2, h1p), (w3, O, h2p))]
+    ws = _weight_pads(w1, w2, w3, kp, h1p, h2p)
     acts = []
     a_in, k_in = xb, kp
     for (b, n, npad), wb in zip(((b1, H1, h1p), (b2, H2, h2p)), ws[:2]):
@@ -481,66 +490,104 @@ def _mlp_forward(xb, T, kp, w1, b1, w2, b2, w3, b3):
     if T:
         ops.gemm(a_in, ws[2], out, T, O, k_in, a_layout=K_CONTIG, b_layout=K_CONTIG, lda=k_in, ldb=k_in, ldc=O,
                  epilogue=EPI_BIAS_RESID_F32, bias=b3.detach().float().contiguous(), aux=_zero_row(O, dev), ldaux=0)
-    return out, acts
+    return out, acts, ws
 
 
-def _dgrad_mul(dyb, w, n_in, T, gp, npad_out):
-    """dU = (dY W) * GELU'(u): B(kk = j, n' = k) = W[j][k], MN-contiguous; bf16 out [rp][npad_out]"""
+def _dgrad_mul(dyb, wpad, ldw, n_in, T, gp, npad_out):
+    """dU = (dY W) * GELU'(u) for W [n_out][n_in] given as its padded bf16 copy wpad ([>= dY width rows][ldw]: B(kk = j,
+    n' = k) = W[j][k], M/N-contiguous); bf16 out [rp][npad_out] and its per-tile column partials (the bias gradient:
+    (partials f32 [rows][n_in], rows))"""
     rp, dev = dyb.shape[0], dyb.device
-    k8 = _rup(n_in, 8)
-    wt = _pad_bf16(w.detach().float().contiguous(), dyb.shape[1], k8)
     du = _alloc_pad(rp, npad_out, T, n_in, dev)
+    kw = dict(a_layout=K_CONTIG, b_layout=MN_CONTIG, lda=dyb.shape[1], ldb=ldw, ldc=npad_out, epilogue=EPI_MUL_BF16,
+              aux=gp, ldaux=npad_out)
+    rows = ops.gemm_partial_rows(dyb, wpad, du, T, n_in, dyb.shape[1], **kw) if T else 0
+    part = torch.empty(max(rows, 1), n_in, device=dev, dtype=F32)
     if T:
-        ops.gemm(dyb, wt, du, T, n_in, dyb.shape[1], a_layout=K_CONTIG, b_layout=MN_CONTIG, lda=dyb.shape[1], ldb=k8,
-                 ldc=npad_out, epilogue=EPI_MUL_BF16, aux=gp, ldaux=npad_out)
-    return du
+        ops.gemm(dyb, wpad, du, T, n_in, dyb.shape[1], col_partial=part, **kw)
+    return du, (part, rows)
 
 
-def _dgrad_f32(dyb, w, n_in, T):
-    """dX = dY W (f32 [T][n_in]) for W [n_out][n_in]"""
-    k8 = _rup(n_in, 8)
-    wt = _pad_bf16(w.detach().float().contiguous(), dyb.shape[1], k8)
+def _dgrad_f32(dyb, wpad, ldw, n_in, T):
+    """dX = dY W (f32 [T][n_in]) for W [n_out][n_in] given as its padded bf16 copy (as _dgrad_mul)"""
     dx = torch.empty(T, n_in, device=dyb.device, dtype=F32)
     if T:
-        ops.gemm(dyb, wt, dx, T, n_in, dyb.shape[1], a_layout=K_CONTIG, b_layout=MN_CONTIG, lda=dyb.shape[1], ldb=k8,
+        ops.gemm(dyb, wpad, dx, T, n_in, dyb.shape[1], a_layout=K_CONTIG, b_layout=MN_CONTIG, lda=dyb.shape[1], ldb=ldw,
                  ldc=n_in, epilogue=EPI_F32)
     return dx
 
 
-def _mlp_backward(d2, T, xb, acts, w1, w2, w3, need_dx, out_du1=None, params=None, need=None, marks=None):
-    """gradients of _mlp_forward: (dX f32 [T][K1] or None, dW1, db1, dW2, db2, dW3, db3); out_du1: a list that
-    receives the first layer's bf16 dU (its input gradient is then left to the caller); params / need: the six
-    parameters and their needs_input_grad flags, whose gradients go to their flat .grad views where they have
-    them (None returned for those, appended to marks)"""
-    ps = params if params is not None else (None,) * 6
-    nd = need if need is not None else (True,) * 6
+def _finish_grads(K, wgrads, biases, params, need, marks, dev):
+    """The weight and bias gradients of a router backward, all at once: wgrads [(A, lda, B, ldb, M, N, i)] are
+    [M][N] = A^T B over the same K (padded token) rows, as ONE split-K launch (ops.gemm_splitk_group) at a common
+    split and each member's fixed-order reduction; biases [(partials f32 [rows][cols], rows, cols, i)] are column
+    sums of GEMM / gate partials, ONE vit_colsum_batch launch. i indexes params / need; a gradient goes to the
+    parameter's flat .grad view in place when it has one (vitmi.flat.grad_sink: parameter appended to marks, None
+    returned), else to a new f32 tensor. Returns {i: gradient or None}."""
+    out = {}
+
+    def dst(i, shape):
+        p = params[i]
+        sk = _flat.grad_sink(p, need[i]) if p is not None else None
+        if sk is not None:
+            marks.append(p)
+            out[i] = None
+            return sk, True
+        t = torch.empty(*shape, device=dev, dtype=F32)
+        out[i] = t
+        return t, False
+
+    if wgrads:
+        s = ops.splitk_factor_group([(M, N, 1) for (_, _, _, _, M, N, _) in wgrads], K)
+        ws = torch.empty(sum(s * M * N for (_, _, _, _, M, N, _) in wgrads), device=dev, dtype=F32)
+        members, views, o = [], [], 0
+        for A, lda, B, ldb, M, N, _ in wgrads:
+            w = ws[o:o + s * M * N]
+            o += s * M * N
+            views.append(w)
+            members.append((A, B, w, M, N, K, dict(a_layout=MN_CONTIG, b_layout=MN_CONTIG, lda=lda, ldb=ldb, ldc=N,
+                                                    epilogue=EPI_SPLITK, split_k=s)))
+        ops.gemm_splitk_group(members)
+        for (_, _, _, _, M, N, i), w in zip(wgrads, views):
+            d, acc = dst(i, (M, N))
+            ops.splitk_reduce(w, 1, s, M, N, d, N, 0, acc)
+    jobs = []
+    for part, rows, cols, i in biases:
+        d, acc = dst(i, (cols,))
+        if rows:
+            jobs.append((part, rows, cols, cols, 0, (d,), acc))
+        elif not acc:
+            d.zero_()
+    for k in range(0, len(jobs), ops.COLSUM_BATCH_MAX):
+        ops.colsum_batch(jobs[k:k + ops.COLSUM_BATCH_MAX])
+    return out
+
+
+def _mlp_backward(d2, T, xb, acts, ws, w1, w2, w3, need_dx, params, need, marks):
+    """data gradients of _mlp_forward and the work list of its parameter gradients: returns (dX f32 [T][K1] or None,
+    dU1 bf16 (the first layer's input-side gradient), wgrads, biases) in _finish_grads' form, indices 0..5 = (W1, b1,
+    W2, b2, W3, b3); b3's gradient (column sums of the f32 dY) is taken here, through params / need / marks"""
     g1, gp1, g2, gp2 = acts
     rp, kp, h1p, h2p = xb.shape[0], xb.shape[1], g1.shape[1], g2.shape[1]
     H1, H2, O, K1 = w1.shape[0], w2.shape[0], w3.shape[0], w1.shape[1]
-    dev = d2.device
-    db3 = _colsum(d2, T, O, O, ps[5], nd[5], marks)
+    db3 = _colsum(d2, T, O, O, params[5], need[5], marks)
     dlb = _pad_bf16(d2, rp, _rup(O, 64))
-    dw3 = _wgrad(dlb, dlb.shape[1], g2, h2p, O, H2, rp, ps[4], nd[4], marks)
-    du2 = _dgrad_mul(dlb, w3, H2, T, gp2, h2p)
-    db2 = _colsum(du2, T, H2, h2p, ps[3], nd[3], marks)
-    dw2 = _wgrad(du2, h2p, g1, h1p, H2, H1, rp, ps[2], nd[2], marks)
-    du1 = _dgrad_mul(du2, w2, H1, T, gp1, h1p)
-    db1 = _colsum(du1, T, H1, h1p, ps[1], nd[1], marks)
-    dw1 = _wgrad(du1, h1p, xb, kp, H1, K1, rp, ps[0], nd[0], marks)
-    dx = _dgrad_f32(du1, w1, K1, T) if need_dx else None
-    if out_du1 is not None:
-        out_du1.append(du1)
-    return dx, dw1, db1, dw2, db2, dw3, db3
+    du2, (p2, r2) = _dgrad_mul(dlb, ws[2], h2p, H2, T, gp2, h2p)
+    du1, (p1, r1) = _dgrad_mul(du2, ws[1], h1p, H1, T, gp1, h1p)
+    dx = _dgrad_f32(du1, ws[0], kp, K1, T) if need_dx else None
+    wgrads = [(dlb, dlb.shape[1], g2, h2p, O, H2, 4), (du2, h2p, g1, h1p, H2, H1, 2), (du1, h1p, xb, kp, H1, K1, 0)]
+    biases = [(p2, r2, H2, 3), (p1, r1, H1, 1)]
+    return dx, du1, wgrads, biases, db3
 
 
 class _RouterMLP(torch.autograd.Function):
     """Linear -> GELU -> Linear -> GELU -> Linear (the router's out_conv) as one node: each hidden layer is one
     GEMM whose epilogue writes GELU(u) (the next GEMM's bf16 operand) and GELU'(u) (kept for the backward),
     the way the ViT engine runs fc1; the backward's data gradients multiply GELU' in their epilogue
-    (EPI_MUL_BF16). Replaces, per hidden layer, the f32 GEMM output, the f32 GELU pass and the cast to the
-    next operand (forward) and the f32 GELU backward and its cast (backward). Rounding differs from the
-    per-op path only in GELU' being bf16 (as in the engine's MLP) and the hidden-bias gradients summing
-    the bf16 dU."""
+    (EPI_MUL_BF16) and sum the hidden-bias gradients in it (column partials), and the three weight gradients run
+    as one grouped split-K launch. Replaces, per hidden layer, the f32 GEMM output, the f32 GELU pass and the cast
+    to the next operand (forward) and the f32 GELU backward and its cast (backward). Rounding differs from the
+    per-op path only in GELU' being bf16 (as in the engine's MLP)."""
 
     @staticmethod
     def forward(ctx, x, w1, b1, w2, b2, w3, b3):
@@ -549,22 +596,23 @@ class _RouterMLP(torch.autograd.Function):
         x2 = x.contiguous().float().reshape(-1, K1)
         T = x2.shape[0]
         xb = _pad_bf16(x2, _rup(max(T, 1), 64), _rup(K1, 64))
-        out, acts = _mlp_forward(xb, T, xb.shape[1], w1, b1, w2, b2, w3, b3)
-        ctx.save_for_backward(xb, *acts, w1, w2, w3)
+        out, acts, ws = _mlp_forward(xb, T, xb.shape[1], w1, b1, w2, b2, w3, b3)
+        ctx.save_for_backward(xb, *acts, *ws, w1, w2, w3)
         ctx.params = (w1, b1, w2, b2, w3, b3)
         ctx.dims = (lead, T, K1)
         return out.reshape(*lead, w3.shape[0])
 
     @staticmethod
     def backward(ctx, dout):
-        xb, g1, gp1, g2, gp2, w1, w2, w3 = ctx.saved_tensors
+        xb, g1, gp1, g2, gp2, wp1, wp2, wp3, w1, w2, w3 = ctx.saved_tensors
         lead, T, K1 = ctx.dims
         d2 = dout.contiguous().float().reshape(T, w3.shape[0])
-        marks = []
-        dx, *grads = _mlp_backward(d2, T, xb, (g1, gp1, g2, gp2), w1, w2, w3, ctx.needs_input_grad[0],
-                                   params=ctx.params, need=ctx.needs_input_grad[1:7], marks=marks)
+        marks, need = [], ctx.needs_input_grad[1:7]
+        dx, _, wgrads, biases, db3 = _mlp_backward(d2, T, xb, (g1, gp1, g2, gp2), (wp1, wp2, wp3), w1, w2, w3,
+                                                   ctx.needs_input_grad[0], ctx.params, need, marks)
+        g = _finish_grads(xb.shape[0], wgrads, biases, ctx.params, need, marks, d2.device)
         _sunk(marks)
-        return (dx.reshape(*lead, K1) if dx is not None else None, *grads)
+        return (dx.reshape(*lead, K1) if dx is not None else None, g[0], g[1], g[2], g[3], g[4], db3)
 
 
 class _RouterNet(torch.autograd.Function):
@@ -573,9 +621,11 @@ class _RouterNet(torch.autograd.Function):
     LN writes its bf16 output as the in_conv GEMM's operand, that GEMM's epilogue writes GELU(u) straight into
     the left half of the out_conv operand [T][2h] (and GELU'(u) aside), the per-image mean (of those bf16
     values) is broadcast into the right half, and out_conv runs as in _RouterMLP: no f32 x_embed, GELU pass,
-    concatenation or cast. Backward: out_conv's input gradient splits into the x_embed part and the per-image
-    sum of the global part (spread back over the non-reserved tokens), times GELU', then in_conv and the LN
-    backward."""
+    concatenation or cast. Backward: out_conv's input gradient splits into the x_embed part (one GEMM) and the
+    per-image token sum of the global part, (sum_t dU1[t]) W1[:, h:] (vit_segment_colsum + a [B][h] f32 product),
+    spread over the non-reserved tokens and times GELU' in one pass (vit_router_dx_gate, which also sums in_conv's
+    bias gradient), then in_conv's data gradient and the LN backward; the four weight gradients are one grouped
+    split-K launch and the three hidden-bias gradients one column-sum launch (_finish_grads)."""
 
     @staticmethod
     def forward(ctx, x, ln_w, ln_b, w0, b0, w1, b1, w2, b2, w3, b3, reserve, eps):
@@ -592,7 +642,7 @@ class _RouterNet(torch.autograd.Function):
         if T:
             ops.layernorm_fwd(x2, D, ln_w.detach().float().contiguous(), ln_b.detach().float().contiguous(), lnb, dp,
                               mean, rstd, T, D, eps)
-        w0b = _pad_bf16(w0.detach().float().contiguous(), Hh, dp)
+        w0b = _pad_bf16(w0.detach().float().contiguous(), h0p, dp)
         xcat = _alloc_pad(rp, kp, T, K1, dev)  # [x_embed | global] operand of out_conv
         gp0 = _alloc_pad(rp, h0p, T, Hh, dev)
         if T:
@@ -601,36 +651,45 @@ class _RouterNet(torch.autograd.Function):
         xc = xcat[:T].view(B, N, kp)
         glob = xc[:, reserve:, :Hh].float().mean(dim=1)  # [B][h] (mean of the bf16 x_embed values)
         xc[:, :, Hh:K1].copy_(glob.to(BF16)[:, None, :])
-        out, acts = _mlp_forward(xcat, T, kp, w1, b1, w2, b2, w3, b3)
-        ctx.save_for_backward(x2, mean, rstd, ln_w, lnb, gp0, xcat, *acts, w0, w1, w2, w3)
+        out, acts, ws = _mlp_forward(xcat, T, kp, w1, b1, w2, b2, w3, b3)
+        ctx.save_for_backward(x2, mean, rstd, ln_w, lnb, gp0, xcat, *acts, w0b, *ws, w1)
         ctx.params = (w0, b0, w1, b1, w2, b2, w3, b3)
         ctx.dims = (B, N, D, T, Hh, K1, reserve)
         return out.view(B, N, w3.shape[0])
 
     @staticmethod
     def backward(ctx, dout):
-        x2, mean, rstd, ln_w, lnb, gp0, xcat, g1, gp1, g2, gp2, w0, w1, w2, w3 = ctx.saved_tensors
+        x2, mean, rstd, ln_w, lnb, gp0, xcat, g1, gp1, g2, gp2, w0b, wp1, wp2, wp3, w1 = ctx.saved_tensors
         B, N, D, T, Hh, K1, reserve = ctx.dims
+        w0, w2, w3 = ctx.params[0], ctx.params[4], ctx.params[6]
         dev = dout.device
-        rp, dp, h0p = xcat.shape[0], lnb.shape[1], gp0.shape[1]
+        rp, dp, h0p, kp = xcat.shape[0], lnb.shape[1], gp0.shape[1], xcat.shape[1]
         d2 = dout.contiguous().float().view(T, w3.shape[0])
-        du1l, marks, need = [], [], ctx.needs_input_grad
-        _, *mlp_grads = _mlp_backward(d2, T, xcat, (g1, gp1, g2, gp2), w1, w2, w3, False, du1l,
-                                      params=ctx.params[2:], need=need[5:11], marks=marks)
-        du1 = du1l[0]
+        marks, need = [], ctx.needs_input_grad[3:11]  # w0, b0, w1, b1, w2, b2, w3, b3
+        mp, mn = ctx.params[2:], need[2:]
+        _, du1, wg, bs, db3 = _mlp_backward(d2, T, xcat, (g1, gp1, g2, gp2), (wp1, wp2, wp3), w1, w2, w3, False, mp, mn,
+                                            marks)
         H1 = w1.shape[0]
-        # out_conv's input gradient, by halves: the x_embed half as one GEMM (dU1 W1[:, :h]); the global half
-        # only through its per-image token sum, which by linearity is (sum_t dU1[t]) W1[:, h:] — a [B][h]
-        # product instead of a [T][h] GEMM, a copy and a token reduction of it
-        dxe = _dgrad_f32(du1, w1[:, :Hh], Hh, T).view(B, N, Hh)
-        s1 = du1[:T].view(B, N, du1.shape[1])[:, :, :H1].sum(dim=1, dtype=F32)
-        w1r = w1.detach()[:, Hh:].to(BF16).float()  # the bf16 operand values the per-token GEMM would use
-        dxe[:, reserve:, :] += (torch.matmul(s1, w1r) / (N - reserve))[:, None, :]
-        du0 = dxe.view(T, Hh) * gp0[:T, :Hh]
-        du0b = _pad_bf16(du0, rp, h0p)
-        db0 = _colsum(du0b, T, Hh, h0p, ctx.params[1], need[4], marks)
-        dw0 = _wgrad(du0b, h0p, lnb, dp, Hh, D, rp, ctx.params[0], need[3], marks)
-        dln = _dgrad_f32(du0b, w0, D, T)
+        # out_conv's input gradient, by halves: the x_embed half as one GEMM (dU1 W1[:, :h], B = the padded W1's
+        # first h columns); the global half only through its per-image token sum, which by linearity is
+        # (sum_t dU1[t]) W1[:, h:] — a [B][h] product instead of a [T][h] GEMM, a copy and a token reduction of it
+        dxe = _dgrad_f32(du1, wp1, kp, Hh, T)
+        s1 = torch.empty(B, H1, device=dev, dtype=F32)
+        ops.segment_colsum(du1, du1.shape[1], B, N, H1, s1, H1)
+        gsum = torch.empty(B, Hh, device=dev, dtype=F32)
+        w1f = w1.detach().float().contiguous()
+        ops.gemm_f32(B, Hh, H1, s1, H1, False, w1f[:, Hh:], K1, False, gsum, Hh)
+        # du0 = (dxe + [t non-reserved] gsum[image] / (N - reserve)) * GELU'(u0), bf16 [rp][h0p], and the column
+        # partials of in_conv's bias gradient
+        du0b = torch.empty(rp, h0p, device=dev, dtype=BF16)
+        r0 = ops.router_dx_gate_partial_rows(rp)
+        p0 = torch.empty(r0, Hh, device=dev, dtype=F32)
+        ops.router_dx_gate(dxe, Hh, gsum, Hh, 1.0 / (N - reserve), gp0, h0p, T, N, reserve, Hh, du0b, h0p, p0, Hh)
+        dln = _dgrad_f32(du0b, w0b, dp, D, T)
+        # the mlp's members are indexed from 2 (w1 ..); in_conv's weight / bias are 0 / 1
+        wg = [(a, la, b_, lb, m, n, i + 2) for a, la, b_, lb, m, n, i in wg] + [(du0b, h0p, lnb, dp, Hh, D, 0)]
+        bs = [(p_, r_, c_, i + 2) for p_, r_, c_, i in bs] + [(p0, r0, Hh, 1)]
+        g = _finish_grads(rp, wg, bs, ctx.params, need, marks, dev)
         dx = torch.empty(T, D, device=dev, dtype=F32)
         need_ln = ctx.needs_input_grad[1] or ctx.needs_input_grad[2]
         gb = torch.zeros(2 * D, device=dev, dtype=F32) if need_ln else None
@@ -638,10 +697,10 @@ class _RouterNet(torch.autograd.Function):
             part = torch.empty(ops.layernorm_bwd_partial_rows(T), 3 * D, device=dev, dtype=F32)
             ops.layernorm_bwd(dln, D, x2, D, mean, rstd, ln_w.detach().float().contiguous(), dx, D, part, T, D,
                               dgamma_dbeta=gb)
-        dg = gb[:D].clone() if need_ln else None
-        dbt = gb[D:].clone() if need_ln else None
+        dg = gb[:D] if need_ln else None
+        dbt = gb[D:] if need_ln else None
         _sunk(marks)
-        return (dx.view(B, N, D), dg, dbt, dw0, db0, *mlp_grads, None, None)
+        return (dx.view(B, N, D), dg, dbt, g[0], g[1], g[2], g[3], g[4], g[5], g[6], db3, None, None)
 
 
 def router_mlp_supported(seq, x):
