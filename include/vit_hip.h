@@ -365,14 +365,14 @@ int vit_dropout_apply_f32(const vit_dropout* d, const float* in, float* out, int
 /* out[o*inner + i] = x[o*inner + i] + y[i]  (PositionEmbs: x + pos_embedding, src/model.py:17) */
 int vit_add_bcast_f32(const float* x, const float* y, float* out, int64_t outer, int64_t inner, vit_stream_t stream);
 /* Res-ViT router backward (res-vit/model.py:186-190, the global half of out_conv's input):
- * vit_segment_colsum: out[s*ldo + c] = sum_{r < seg_rows} in[(s*seg_rows + r)*ld + c] (per-image token sums; f32
- *   or bf16 in, rows in order);
+ * vit_segment_colsum: out[s*ldo + c] = scale * sum_{r < seg_rows} in[(s*seg_stride + row0 + r)*ld + c] (per-image
+ *   token sums / means; f32 or bf16 in, even ld, fixed order);
  * vit_router_dx_gate: out (bf16 [rows_pad][cols_pad], ld ldo) = bf16((dx[t][c] + [t % N >= reserve] g_scale
  *   g[t / N][c]) * gp[t][c]) for t < T, c < cols, zero elsewhere (in_conv's input-gradient times its saved GELU');
  *   optional col_partial[b*ldp + c] = column sums of the rounded values over row block b
  *   (vit_router_dx_gate_partial_rows(rows_pad) blocks; reduce with vit_colsum_batch) */
-int vit_segment_colsum(const void* in, int32_t in_bf16, int64_t ld, int64_t segs, int64_t seg_rows, int64_t cols,
-                       float* out, int64_t ldo, vit_stream_t stream);
+int vit_segment_colsum(const void* in, int32_t in_bf16, int64_t ld, int64_t segs, int64_t seg_stride, int64_t row0,
+                       int64_t seg_rows, int64_t cols, float scale, float* out, int64_t ldo, vit_stream_t stream);
 int64_t vit_router_dx_gate_partial_rows(int64_t rows_pad);
 int vit_router_dx_gate(const float* dx, int64_t ldx, const float* g, int64_t ldg, float g_scale, const void* gp,
                        int64_t ldgp, int64_t T, int64_t N, int64_t reserve, int64_t cols, void* out, int64_t ldo,

@@ -192,7 +192,7 @@ def test_gemm_splitk_group_small_members():
 
 def test_segment_colsum_and_router_dx_gate():
     """the Res-ViT router backward helpers against torch: per-image token sums (bf16 and f32 inputs), and
-    bf16((dx + [t % N >= reserve] s g[t // N]) * gp) with zero padding and per-64-row column partials of the
+    bf16((dx + [t % N >= reserve] s g[t // N]) * gp) with zero padding and per-row-block column partials of the
     rounded values"""
     g = torch.Generator(device="cpu").manual_seed(5)
     Bn, N, C, ld = 3, 50, 200, 264
@@ -203,6 +203,10 @@ def test_segment_colsum_and_router_dx_gate():
         ref = inp[:, :C].float().view(Bn, N, C).sum(1)
         assert torch.allclose(out[:, :C], ref, rtol=1e-5, atol=1e-4)
         assert torch.isnan(out[:, C:]).all()
+        # the router forward's mean over the non-reserved tokens (odd column count: the last pair half empty)
+        mean = torch.empty(Bn, C - 1, device=DEV)
+        ops.segment_colsum(inp, ld, Bn, N - 2, C - 1, mean, C - 1, seg_stride=N, row0=2, scale=1.0 / (N - 2))
+        assert torch.allclose(mean, inp[:, :C - 1].float().view(Bn, N, C - 1)[:, 2:].mean(1), rtol=1e-5, atol=1e-5)
     T, reserve, scale = Bn * N, 2, 1.0 / 48
     rows_pad, cols_pad = 192, 256
     dx = torch.randn(T, C, generator=g).to(DEV)
@@ -218,7 +222,9 @@ def test_segment_colsum_and_router_dx_gate():
     assert (out[T:].float() == 0).all() and (out[:, C:].float() == 0).all()
     full = torch.zeros(rows_pad, C, device=DEV)
     full[:T] = ref.float()
-    assert torch.allclose(part, full.view(nb, 64, C).sum(1), rtol=1e-5, atol=1e-4)
+    rb = -(-rows_pad // nb)  # rows per partial block
+    assert rb * nb == rows_pad
+    assert torch.allclose(part, full.view(nb, rb, C).sum(1), rtol=1e-5, atol=1e-4)
 
 
 @pytest.mark.parametrize("tile", [1, 2, 6, 9])

@@ -31,10 +31,13 @@ with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], with_stac
     for _ in range(2):
         train_step(model, x, y, opt, sched, 1e-4, 1e-2, 1.0, True, None)
     torch.cuda.synchronize()
+print(prof.key_averages().table(sort_by="self_device_time_total", row_limit=40, max_name_column_width=60), flush=True)
 rows = [e for e in prof.key_averages(group_by_stack_n=8) if e.key in ("aten::add_", "aten::fill_", "aten::copy_",
-                                                                     "aten::where", "aten::add", "aten::mul")]
+                                                                     "aten::where", "aten::add", "aten::mul",
+                                                                     "aten::zero_", "aten::sum", "aten::mean",
+                                                                     "aten::_to_copy", "aten::div", "aten::sub")]
 rows.sort(key=lambda e: -e.self_device_time_total)
-for e in rows[:30]:
+for e in rows[:45]:
     frames = [f for f in e.stack if "vitmi" in f or "bench" in f][:4]
     print(f"{e.key:12s} n={e.count:4d} dev={e.self_device_time_total / 1e3:7.3f} ms  " + " <- ".join(
         f.split("/")[-1] for f in frames), flush=True)

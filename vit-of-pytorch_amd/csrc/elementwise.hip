@@ -957,63 +957,140 @@ extern "C" int vit_add_bcast_f32(const float* x, const float* y, float* out, int
 // ---- Res-ViT router backward helpers (res-vit/model.py:186-190 RouterModule: the global half of out_conv's
 // input and in_conv's GELU) ------------------------------------------------------------------------------------
 namespace {
-// out[s][c] = sum over the seg_rows rows of segment s of in[row][c], rows in order (deterministic)
+// out[s][c] = scale * sum over rows [s * seg_stride + row0, + seg_rows) of in[row][c]. Workgroup = (segment, 128
+// columns): 4 row lanes x 64 column pairs, each lane sums every 4th row (four rows in flight), the lanes are added
+// in order through LDS (deterministic)
 template <bool BF16>
-__global__ void __launch_bounds__(256) segment_colsum_kernel(const void* __restrict__ in, long ld, long seg_rows,
-                                                             int cols, float* __restrict__ out, long ldo) {
-  const int c = blockIdx.y * 256 + threadIdx.x;
-  if (c >= cols) return;
-  const long r0 = (long)blockIdx.x * seg_rows;
-  float acc = 0.f;
-  for (long r = 0; r < seg_rows; ++r) {
-    const long i = (r0 + r) * ld + c;
-    acc += BF16 ? bf2f(((const bf16_t*)in)[i]) : ((const float*)in)[i];
+__global__ void __launch_bounds__(256) segment_colsum_kernel(const void* __restrict__ in, long ld, long seg_stride,
+                                                             long row0, long seg_rows, int cols, float scale,
+                                                             float* __restrict__ out, long ldo) {
+  __shared__ float2 red[4][64];
+  const int cp = threadIdx.x & 63, lane_r = threadIdx.x >> 6;
+  const int c = blockIdx.y * 128 + cp * 2;
+  const long base = (long)blockIdx.x * seg_stride + row0;
+  float2 acc = {0.f, 0.f};
+  auto ld2 = [&](long r) -> float2 {
+    const long i = (base + r) * ld + c;
+    if constexpr (BF16) {
+      if (c + 1 < cols) {
+        const unsigned u = *reinterpret_cast<const unsigned*>((const bf16_t*)in + i);
+        return float2{bf2f((bf16_t)(u & 0xffff)), bf2f((bf16_t)(u >> 16))};
+      }
+      return float2{bf2f(((const bf16_t*)in)[i]), 0.f};
+    } else {
+      if (c + 1 < cols) return *reinterpret_cast<const float2*>((const float*)in + i);
+      return float2{((const float*)in)[i], 0.f};
+    }
+  };
+  if (c < cols) {
+    long r = lane_r;
+    for (; r + 12 < seg_rows; r += 16) {
+      const float2 a = ld2(r), b = ld2(r + 4), d = ld2(r + 8), e = ld2(r + 12);
+      acc.x += a.x; acc.y += a.y; acc.x += b.x; acc.y += b.y;
+      acc.x += d.x; acc.y += d.y; acc.x += e.x; acc.y += e.y;
+    }
+    for (; r < seg_rows; r += 4) {
+      const float2 a = ld2(r);
+      acc.x += a.x; acc.y += a.y;
+    }
   }
-  out[(long)blockIdx.x * ldo + c] = acc;
+  red[lane_r][cp] = acc;
+  __syncthreads();
+  if (lane_r == 0 && c < cols) {
+    float2 t = red[0][cp];
+#pragma unroll
+    for (int q = 1; q < 4; ++q) { t.x += red[q][cp].x; t.y += red[q][cp].y; }
+    float* o = out + (long)blockIdx.x * ldo + c;
+    o[0] = scale * t.x;
+    if (c + 1 < cols) o[1] = scale * t.y;
+  }
 }
 
 // out (bf16 [rows_pad][cols_pad]) = (dx[t][c] + [t % N >= reserve] * g_scale * g[t / N][c]) * gp[t][c] on the T x cols
 // block, rounded once to bf16, zero elsewhere; col_partial[blockIdx.y][c] = the column sums of the rounded values of
-// the block's RB rows (column c: thread c of the 256-column group)
-constexpr int RDG_RB = 64;
+// the block's RB rows. A thread owns a column pair (cols_pad, ldx, ldgp, ldo even) and walks the block's rows four at
+// a time, every load of the four issued before any use (one row at a time left the kernel waiting on HBM latency:
+// 72 us for 25 216 x 512), with the image / position counters stepped, not divided, per row
+constexpr int RDG_RB = 32;
 __global__ void __launch_bounds__(256) router_dx_gate_kernel(const float* __restrict__ dx, long ldx,
                                                              const float* __restrict__ g, long ldg, float g_scale,
                                                              const bf16_t* __restrict__ gp, long ldgp, long T, long N,
                                                              long reserve, int cols, bf16_t* __restrict__ out,
                                                              long ldo, long rows_pad, int cols_pad,
                                                              float* __restrict__ col_partial, long ldp) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
+  const int c = (blockIdx.x * 256 + threadIdx.x) * 2;
   if (c >= cols_pad) return;
   const long r0 = (long)blockIdx.y * RDG_RB;
   const long r1 = r0 + RDG_RB < rows_pad ? r0 + RDG_RB : rows_pad;
-  float acc = 0.f;
-  for (long t = r0; t < r1; ++t) {
-    bf16_t o = 0;
-    if (t < T && c < cols) {
-      float v = dx[t * ldx + c];
-      if (t % N >= reserve) v += g_scale * g[(t / N) * ldg + c];
-      o = f2bf(v * bf2f(gp[t * ldgp + c]));
-      acc += bf2f(o);
+  const long tv = r1 < T ? r1 : T;  // rows [r0, tv) hold data
+  const bool c0v = c < cols, c1v = c + 1 < cols;
+  long img = r0 / N, pos = r0 - img * N;
+  float a0 = 0.f, a1 = 0.f;
+  for (long t = r0; t < r1; t += 4) {
+    float2 dv[4], gv[4];
+    unsigned gu[4];
+    bool ok[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      ok[k] = c0v && t + k < tv;
+      dv[k] = float2{0.f, 0.f};
+      gv[k] = float2{0.f, 0.f};
+      gu[k] = 0u;
+      if (ok[k]) {
+        const float* d = dx + (t + k) * ldx + c;
+        const float* gr = g + img * ldg + c;
+        if (c1v) {  // (dx and g rows 8-B aligned: checked by the launcher)
+          dv[k] = *reinterpret_cast<const float2*>(d);
+          if (pos >= reserve) {
+            const float2 gg = *reinterpret_cast<const float2*>(gr);
+            gv[k] = float2{g_scale * gg.x, g_scale * gg.y};
+          }
+        } else {
+          dv[k].x = d[0];
+          if (pos >= reserve) gv[k].x = g_scale * gr[0];
+        }
+        gu[k] = *reinterpret_cast<const unsigned*>(gp + (t + k) * ldgp + c);
+      }
+      if (++pos == N) {
+        pos = 0;
+        ++img;
+      }
     }
-    out[t * ldo + c] = o;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if (t + k >= r1) break;
+      unsigned o = 0u;
+      if (ok[k]) {
+        const bf16_t o0 = f2bf((dv[k].x + gv[k].x) * bf2f((bf16_t)(gu[k] & 0xffff)));
+        const bf16_t o1 = c1v ? f2bf((dv[k].y + gv[k].y) * bf2f((bf16_t)(gu[k] >> 16))) : (bf16_t)0;
+        a0 += bf2f(o0);
+        a1 += bf2f(o1);
+        o = (unsigned)o0 | ((unsigned)o1 << 16);
+      }
+      *reinterpret_cast<unsigned*>(out + (t + k) * ldo + c) = o;
+    }
   }
-  if (col_partial && c < cols) col_partial[blockIdx.y * ldp + c] = acc;
+  if (col_partial) {
+    if (c0v) col_partial[blockIdx.y * ldp + c] = a0;
+    if (c1v) col_partial[blockIdx.y * ldp + c + 1] = a1;
+  }
 }
 }  // namespace
 
-extern "C" int vit_segment_colsum(const void* in, int32_t in_bf16, int64_t ld, int64_t segs, int64_t seg_rows,
-                                  int64_t cols, float* out, int64_t ldo, vit_stream_t stream) {
-  VIT_CHECK_ARG(in && out && segs >= 0 && seg_rows >= 0 && cols > 0 && ld >= cols && ldo >= cols &&
-                    cols < (1L << 30),
-                "vit_segment_colsum: bad args");
+extern "C" int vit_segment_colsum(const void* in, int32_t in_bf16, int64_t ld, int64_t segs, int64_t seg_stride,
+                                  int64_t row0, int64_t seg_rows, int64_t cols, float scale, float* out, int64_t ldo,
+                                  vit_stream_t stream) {
+  VIT_CHECK_ARG(in && out && segs >= 0 && seg_rows >= 0 && row0 >= 0 && seg_stride >= 0 && cols > 0 && ld >= cols &&
+                    ldo >= cols && cols < (1L << 30) && ld % 2 == 0 && ((uintptr_t)in % (in_bf16 ? 4 : 8)) == 0,
+                "vit_segment_colsum: bad args (even ld, 2-element aligned rows)");
   if (segs == 0) return VIT_OK;
-  const dim3 grid((unsigned)segs, (unsigned)((cols + 255) / 256));
+  const dim3 grid((unsigned)segs, (unsigned)((cols + 127) / 128));
   if (in_bf16)
     hipLaunchKernelGGL(segment_colsum_kernel<true>, grid, dim3(256), 0, (hipStream_t)stream, in, (long)ld,
-                       (long)seg_rows, (int)cols, out, (long)ldo);
+                       (long)seg_stride, (long)row0, (long)seg_rows, (int)cols, scale, out, (long)ldo);
   else
     hipLaunchKernelGGL(segment_colsum_kernel<false>, grid, dim3(256), 0, (hipStream_t)stream, in, (long)ld,
-                       (long)seg_rows, (int)cols, out, (long)ldo);
+                       (long)seg_stride, (long)row0, (long)seg_rows, (int)cols, scale, out, (long)ldo);
   VIT_LAUNCH_CHECK("vit_segment_colsum");
 }
 
@@ -1024,11 +1101,14 @@ extern "C" int vit_router_dx_gate(const float* dx, int64_t ldx, const float* g, 
                                   void* out, int64_t ldo, int64_t rows_pad, int64_t cols_pad, float* col_partial,
                                   int64_t ldp, vit_stream_t stream) {
   VIT_CHECK_ARG(dx && g && gp && out && T >= 0 && N > 0 && reserve >= 0 && cols > 0 && cols_pad >= cols &&
-                    rows_pad >= T && ldx >= cols && ldg >= cols && ldgp >= cols && ldo >= cols_pad &&
-                    (!col_partial || ldp >= cols) && cols_pad < (1L << 30),
-                "vit_router_dx_gate: bad args");
+                    rows_pad >= T && ldx >= cols && ldg >= cols && ldgp >= cols_pad && ldo >= cols_pad &&
+                    (!col_partial || ldp >= cols) && cols_pad < (1L << 30) && cols_pad % 2 == 0 && ldgp % 2 == 0 &&
+                    ldo % 2 == 0 && ((uintptr_t)gp % 4) == 0 && ((uintptr_t)out % 4) == 0 && ldx % 2 == 0 &&
+                    ldg % 2 == 0 && ((uintptr_t)dx % 8) == 0 && ((uintptr_t)g % 8) == 0,
+                "vit_router_dx_gate: bad args (even leading dimensions, 8-B aligned f32 / 4-B aligned bf16 rows; gp as "
+                "wide as the padded output)");
   if (rows_pad == 0) return VIT_OK;
-  const dim3 grid((unsigned)((cols_pad + 255) / 256), (unsigned)vit_router_dx_gate_partial_rows(rows_pad));
+  const dim3 grid((unsigned)((cols_pad / 2 + 255) / 256), (unsigned)vit_router_dx_gate_partial_rows(rows_pad));
   hipLaunchKernelGGL(router_dx_gate_kernel, grid, dim3(256), 0, (hipStream_t)stream, dx, (long)ldx, g, (long)ldg,
                      g_scale, (const bf16_t*)gp, (long)ldgp, (long)T, (long)N, (long)reserve, (int)cols, (bf16_t*)out,
                      (long)ldo, (long)rows_pad, (int)cols_pad, col_partial, (long)ldp);

@@ -64,7 +64,7 @@ _SIGS = {
     "vit_gemm_split_rows": (c_i64, [ctypes.POINTER(GemmArgs)]),
     "vit_gemm_bf16_part": (c_i32, [ctypes.POINTER(GemmArgs), c_i32, c_vp]),
     "vit_gemm_splitk_group": (c_i32, [ctypes.POINTER(GemmArgs), c_i32, c_vp]),
-    "vit_segment_colsum": (c_i32, [c_vp, c_i32, c_i64, c_i64, c_i64, c_i64, c_vp, c_i64, c_vp]),
+    "vit_segment_colsum": (c_i32, [c_vp, c_i32, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_f32, c_vp, c_i64, c_vp]),
     "vit_router_dx_gate_partial_rows": (c_i64, [c_i64]),
     "vit_router_dx_gate": (c_i32, [c_vp, c_i64, c_vp, c_i64, c_f32, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp,
                                    c_i64, c_i64, c_i64, c_vp, c_i64, c_vp]),

@@ -326,11 +326,13 @@ def add_bcast_f32(x, y, out, outer, inner):
     check(lib().vit_add_bcast_f32(_p(x), _p(y), _p(out), outer, inner, _stream()), "vit_add_bcast_f32")
 
 
-def segment_colsum(inp, ld, segs, seg_rows, cols, out, ldo):
-    """out[s][c] = sum of rows [s*seg_rows, (s+1)*seg_rows) of inp's column c (f32 or bf16 inp; rows in order)"""
+def segment_colsum(inp, ld, segs, seg_rows, cols, out, ldo, seg_stride=None, row0=0, scale=1.0):
+    """out[s][c] = scale * sum of rows [s*seg_stride + row0, + seg_rows) of inp's column c (f32 or bf16 inp, even ld;
+    fixed order); seg_stride defaults to seg_rows"""
     _chk(out, F32, "out")
-    check(lib().vit_segment_colsum(_p(inp), int(inp.dtype == BF16), ld, segs, seg_rows, cols, _p(out), ldo, _stream()),
-          "vit_segment_colsum")
+    st = seg_rows if seg_stride is None else seg_stride
+    check(lib().vit_segment_colsum(_p(inp), int(inp.dtype == BF16), ld, segs, st, row0, seg_rows, cols, float(scale),
+                                   _p(out), ldo, _stream()), "vit_segment_colsum")
 
 
 def router_dx_gate_partial_rows(rows_pad):

@@ -347,26 +347,26 @@ class _ApproxStep(torch.autograd.Function):
         ops.cast_pad_rows(x2, T, D, xb, kp)
         if rp > T:
             ops.zero_(xb[T:])
-        wdb = torch.empty(r, kp, device=dev, dtype=BF16)  # B(k, n) = Wd[n][k]: K-contiguous
-        ops.cast_pad_rows(wd.detach().float().contiguous(), r, D, wdb, kp)
+        # Wd [r][D] and Wu [D][r] as bf16, rows and columns padded to 64 with zeros: the forward's K-contiguous B
+        # operands, and unchanged the backward's M/N-contiguous ones (cast once per step)
+        wdb = _pad_bf16(wd.detach().float().contiguous(), rk, kp)  # B(k, n) = Wd[n][k]: K-contiguous
         hb = _alloc_pad(rp, rk, T, r, dev)
         ops.gemm(xb, wdb, hb, T, r, kp, a_layout=K_CONTIG, b_layout=K_CONTIG, lda=kp, ldb=kp, ldc=rk,
                  epilogue=EPI_BF16)
         selb = sel.reshape(T, 1).to(BF16)
         hb[:T].mul_(selb)  # unselected rows: h = 0 (exact)
-        wub = torch.empty(D, rk, device=dev, dtype=BF16)  # B(k, n) = Wu[n][k]: K-contiguous over r
-        ops.cast_pad_rows(wu.detach().float().contiguous(), D, r, wub, rk)
+        wub = _pad_bf16(wu.detach().float().contiguous(), kp, rk)  # B(k, n) = Wu[n][k]: K-contiguous over r
         out = torch.empty(T, D, device=dev, dtype=F32)
         ops.gemm(hb, wub, out, T, D, rk, a_layout=K_CONTIG, b_layout=K_CONTIG, lda=rk, ldb=rk, ldc=D,
                  epilogue=EPI_BIAS_RESID_F32, bias=_zero_row(D, dev), aux=x2, ldaux=D)
-        ctx.save_for_backward(xb, hb, wd, wu, selb)
+        ctx.save_for_backward(xb, hb, wdb, wub, selb)
         ctx.params = (wd, wu)
         ctx.dims = (B, N, D, T, r)
         return out.view(B, N, D)
 
     @staticmethod
     def backward(ctx, dout):
-        xb, hb, wd, wu, selb = ctx.saved_tensors
+        xb, hb, wdb, wub, selb = ctx.saved_tensors
         B, N, D, T, r = ctx.dims
         kp, rp, rk = xb.shape[1], xb.shape[0], hb.shape[1]
         dev = dout.device
@@ -375,33 +375,26 @@ class _ApproxStep(torch.autograd.Function):
         ops.cast_pad_rows(d2, T, D, db, kp)
         if rp > T:
             ops.zero_(db[T:])
-        # dh = dout Wu: B(kk = n, n' = j) = Wu[n][j], MN-contiguous [D][r8]
-        r8 = _rup(r, 8)
-        wut = _alloc_pad(kp, r8, D, r8, dev)
-        ops.cast_pad_rows(wu.detach().float().contiguous(), D, r, wut, r8)
-        # dh = dout Wu, rounded to the bf16 operand by the GEMM's epilogue (the same RNE rounding as a cast of the
-        # f32 product: no f32 [T][r] pass)
+        # dh = dout Wu: B(kk = n, n' = j) = Wu[n][j], M/N-contiguous (the forward's padded [kp][rk] copy), rounded to
+        # the bf16 operand by the GEMM's epilogue (the same RNE rounding as a cast of the f32 product)
         dhb = _alloc_pad(rp, rk, T, r, dev)
-        ops.gemm(db, wut, dhb, T, r, kp, a_layout=K_CONTIG, b_layout=MN_CONTIG, lda=kp, ldb=r8, ldc=rk,
+        ops.gemm(db, wub, dhb, T, r, kp, a_layout=K_CONTIG, b_layout=MN_CONTIG, lda=kp, ldb=rk, ldc=rk,
                  epilogue=EPI_BF16)
         dhb[:T].mul_(selb)
-        dx = dwd = dwu = None
+        dx = None
         if ctx.needs_input_grad[0]:
-            # dx = dout + dh Wd: B(kk = j, n' = k) = Wd[j][k], MN-contiguous [r64][D8]
-            d8 = _rup(D, 8)
-            wdt = _alloc_pad(rk, d8, r, d8, dev)
-            ops.cast_pad_rows(wd.detach().float().contiguous(), r, D, wdt, d8)
+            # dx = dout + dh Wd: B(kk = j, n' = k) = Wd[j][k], M/N-contiguous (the forward's padded [rk][kp] copy)
             dx = torch.empty(T, D, device=dev, dtype=F32)
-            ops.gemm(dhb, wdt, dx, T, D, rk, a_layout=K_CONTIG, b_layout=MN_CONTIG, lda=rk, ldb=d8, ldc=D,
+            ops.gemm(dhb, wdb, dx, T, D, rk, a_layout=K_CONTIG, b_layout=MN_CONTIG, lda=rk, ldb=kp, ldc=D,
                      epilogue=EPI_BIAS_RESID_F32, bias=_zero_row(D, dev), aux=d2, ldaux=D)
             dx = dx.view(B, N, D)
-        marks = []
-        if ctx.needs_input_grad[2]:  # dWu [D][r] = dout^T h
-            dwu = _wgrad(db, kp, hb, rk, D, r, rp, ctx.params[1], True, marks)
-        if ctx.needs_input_grad[1]:  # dWd [r][D] = dh^T x
-            dwd = _wgrad(dhb, rk, xb, kp, r, D, rp, ctx.params[0], True, marks)
+        # dWd [r][D] = dh^T x and dWu [D][r] = dout^T h: one grouped split-K launch (each alone is 3 tiles, under a
+        # wave at any split)
+        marks, need = [], (ctx.needs_input_grad[1], ctx.needs_input_grad[2])
+        wg = [m for m, nd in zip(((dhb, rk, xb, kp, r, D, 0), (db, kp, hb, rk, D, r, 1)), need) if nd]
+        g = _finish_grads(rp, wg, [], ctx.params, (True, True), marks, dev, own_split=True)
         _sunk(marks)
-        return dx, dwd, dwu, None
+        return dx, g.get(0), g.get(1), None
 
 
 def approx_supported(m, x):
@@ -517,13 +510,14 @@ def _dgrad_f32(dyb, wpad, ldw, n_in, T):
     return dx
 
 
-def _finish_grads(K, wgrads, biases, params, need, marks, dev):
+def _finish_grads(K, wgrads, biases, params, need, marks, dev, own_split=False):
     """The weight and bias gradients of a router backward, all at once: wgrads [(A, lda, B, ldb, M, N, i)] are
     [M][N] = A^T B over the same K (padded token) rows, as ONE split-K launch (ops.gemm_splitk_group) at a common
-    split and each member's fixed-order reduction; biases [(partials f32 [rows][cols], rows, cols, i)] are column
-    sums of GEMM / gate partials, ONE vit_colsum_batch launch. i indexes params / need; a gradient goes to the
-    parameter's flat .grad view in place when it has one (vitmi.flat.grad_sink: parameter appended to marks, None
-    returned), else to a new f32 tensor. Returns {i: gradient or None}."""
+    split (own_split: each member at the split ops.wgrad would give it alone, so its sums are bit-identical to
+    ops.wgrad's) and each member's fixed-order reduction; biases [(partials f32 [rows][cols], rows, cols, i)] are
+    column sums of GEMM / gate partials, ONE vit_colsum_batch launch. i indexes params / need; a gradient goes to
+    the parameter's flat .grad view in place when it has one (vitmi.flat.grad_sink: parameter appended to marks,
+    None returned), else to a new f32 tensor. Returns {i: gradient or None}."""
     out = {}
 
     def dst(i, shape):
@@ -538,17 +532,20 @@ def _finish_grads(K, wgrads, biases, params, need, marks, dev):
         return t, False
 
     if wgrads:
-        s = ops.splitk_factor_group([(M, N, 1) for (_, _, _, _, M, N, _) in wgrads], K)
-        ws = torch.empty(sum(s * M * N for (_, _, _, _, M, N, _) in wgrads), device=dev, dtype=F32)
+        if own_split:
+            ss = [ops.splitk_factor(M, N, K) for (_, _, _, _, M, N, _) in wgrads]
+        else:
+            ss = [ops.splitk_factor_group([(M, N, 1) for (_, _, _, _, M, N, _) in wgrads], K)] * len(wgrads)
+        ws = torch.empty(sum(s * M * N for s, (_, _, _, _, M, N, _) in zip(ss, wgrads)), device=dev, dtype=F32)
         members, views, o = [], [], 0
-        for A, lda, B, ldb, M, N, _ in wgrads:
+        for s, (A, lda, B, ldb, M, N, _) in zip(ss, wgrads):
             w = ws[o:o + s * M * N]
             o += s * M * N
             views.append(w)
             members.append((A, B, w, M, N, K, dict(a_layout=MN_CONTIG, b_layout=MN_CONTIG, lda=lda, ldb=ldb, ldc=N,
                                                     epilogue=EPI_SPLITK, split_k=s)))
         ops.gemm_splitk_group(members)
-        for (_, _, _, _, M, N, i), w in zip(wgrads, views):
+        for s, (_, _, _, _, M, N, i), w in zip(ss, wgrads, views):
             d, acc = dst(i, (M, N))
             ops.splitk_reduce(w, 1, s, M, N, d, N, 0, acc)
     jobs = []
@@ -649,7 +646,8 @@ class _RouterNet(torch.autograd.Function):
             ops.gemm(lnb, w0b, gp0, T, Hh, dp, a_layout=K_CONTIG, b_layout=K_CONTIG, lda=dp, ldb=dp, ldc=h0p,
                      epilogue=EPI_BIAS_GELU_DGELU, bias=b0.detach().float().contiguous(), C2=xcat, ldc2=kp)
         xc = xcat[:T].view(B, N, kp)
-        glob = xc[:, reserve:, :Hh].float().mean(dim=1)  # [B][h] (mean of the bf16 x_embed values)
+        glob = torch.empty(B, Hh, device=dev, dtype=F32)  # [B][h]: mean of the bf16 x_embed values, reserved tokens out
+        ops.segment_colsum(xcat, kp, B, N - reserve, Hh, glob, Hh, seg_stride=N, row0=reserve, scale=1.0 / (N - reserve))
         xc[:, :, Hh:K1].copy_(glob.to(BF16)[:, None, :])
         out, acts, ws = _mlp_forward(xcat, T, kp, w1, b1, w2, b2, w3, b3)
         ctx.save_for_backward(x2, mean, rstd, ln_w, lnb, gp0, xcat, *acts, w0b, *ws, w1)
