@@ -151,6 +151,18 @@ int vit_gemm_splitk_group(const vit_gemm_args* args, int32_t n, vit_stream_t str
 int vit_splitk_reduce(const float* ws, int64_t batch, int64_t split, int64_t M, int64_t N,
                       float* out, int64_t ldo, int64_t out_batch_stride, int32_t accumulate,
                       vit_stream_t stream);
+/* up to VIT_SPLITK_GROUP_MAX vit_splitk_reduce calls in ONE launch (each job's output bit-identical to its own call;
+ * jobs outside the 16-B vector form fall back to one launch each) */
+#define VIT_SPLITK_GROUP_MAX 8
+typedef struct vit_splitk_job {
+  const float* ws;
+  int64_t batch, split, M, N;
+  float* out;
+  int64_t ldo, out_batch_stride;
+  int32_t accumulate;
+  int32_t reserved;
+} vit_splitk_job;
+int vit_splitk_reduce_group(const vit_splitk_job* jobs, int32_t njobs, vit_stream_t stream);
 
 /* ------------------------------------------------------------------------------------------
  * LayerNorm over the last dim (eps, biased variance, affine).  nn.LayerNorm src/model.py:108,114,146

@@ -190,6 +190,27 @@ def test_gemm_splitk_group_small_members():
         assert rel(out.sum(0), ref) < 1e-5
 
 
+def test_splitk_reduce_group_equals_single_reductions():
+    """vit_splitk_reduce_group: jobs of different shapes, splits, batches, strides and accumulate flags in one launch
+    write what their own vit_splitk_reduce calls write, bit for bit (a scalar-form job falls back per job)"""
+    g = torch.Generator(device="cpu").manual_seed(3)
+    specs = [(1, 7, 768, 256, 256, 0, False), (3, 5, 64, 96, 104, 64 * 104, True), (1, 3, 10, 6, 6, 0, False)]
+    jobs, refs = [], []
+    for batch, split, M, N, ldo, obs, acc in specs:
+        ws = torch.randn(batch * split * M * N, generator=g).to(DEV)
+        init = torch.randn(max(1, batch) * max(M * ldo, obs or 0) + 8, generator=g).to(DEV)
+        a, b = init.clone(), init.clone()
+        ops.splitk_reduce(ws, batch, split, M, N, a, ldo, obs, acc)
+        refs.append(a)
+        jobs.append((ws, batch, split, M, N, b, ldo, obs, acc))
+    ops.splitk_reduce_group(jobs)
+    for (_, _, _, _, _, b, _, _, _), a in zip(jobs, refs):
+        assert torch.equal(a, b)
+    ops.splitk_reduce_group(jobs[:2])  # all vector form: one launch
+    for (_, _, _, _, _, b, _, _, acc), a in zip(jobs[:2], refs[:2]):
+        assert acc or torch.equal(a, b)
+
+
 def test_segment_colsum_and_router_dx_gate():
     """the Res-ViT router backward helpers against torch: per-image token sums (bf16 and f32 inputs), and
     bf16((dx + [t % N >= reserve] s g[t // N]) * gp) with zero padding and per-row-block column partials of the

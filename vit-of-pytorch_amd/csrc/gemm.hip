@@ -359,7 +359,92 @@ __global__ void splitk_reduce4_kernel(const float* __restrict__ ws, int split, l
     *dst = s;
   }
 }
+
+// several vit_splitk_reduce jobs (vector form) in one launch: workgroups [blk0_j, blk0_{j+1}) are job j's, batch-major;
+// the same 4-at-a-time slab order as splitk_reduce4_kernel, so each output equals its own launch's bit for bit
+struct SplitkJobDev {
+  const float* ws;
+  float* out;
+  long M, N, ldo, obs;
+  int split, batch, nb, blk0, acc;
+};
+struct SplitkGroupDev {
+  SplitkJobDev j[VIT_SPLITK_GROUP_MAX];
+  int n;
+};
+__global__ void splitk_reduce4_group_kernel(const SplitkGroupDev G) {
+  int jx = 0;
+#pragma unroll
+  for (int k = 1; k < VIT_SPLITK_GROUP_MAX; ++k)
+    if (k < G.n && (int)blockIdx.x >= G.j[k].blk0) jx = k;
+  const SplitkJobDev& J = G.j[jx];
+  const int local = blockIdx.x - J.blk0;
+  const int z = local / J.nb, bx = local - z * J.nb;
+  const long total = J.M * J.N, total4 = total / 4;
+  const float4* w = reinterpret_cast<const float4*>(J.ws + (long)z * J.split * total);
+  float* o = J.out + z * J.obs;
+  for (long i = (long)bx * blockDim.x + threadIdx.x; i < total4; i += (long)J.nb * blockDim.x) {
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+    int k = 0;
+    for (; k + 4 <= J.split; k += 4) {
+      const float4 a = w[(long)k * total4 + i], b = w[(long)(k + 1) * total4 + i];
+      const float4 c = w[(long)(k + 2) * total4 + i], d = w[(long)(k + 3) * total4 + i];
+      s.x += (a.x + b.x) + (c.x + d.x);
+      s.y += (a.y + b.y) + (c.y + d.y);
+      s.z += (a.z + b.z) + (c.z + d.z);
+      s.w += (a.w + b.w) + (c.w + d.w);
+    }
+    for (; k < J.split; ++k) {
+      const float4 a = w[(long)k * total4 + i];
+      s.x += a.x; s.y += a.y; s.z += a.z; s.w += a.w;
+    }
+    const long e = i * 4, m = e / J.N, n = e - m * J.N;
+    float4* dst = reinterpret_cast<float4*>(o + m * J.ldo + n);
+    if (J.acc) {
+      const float4 p = *dst;
+      s.x += p.x; s.y += p.y; s.z += p.z; s.w += p.w;
+    }
+    *dst = s;
+  }
+}
 }  // namespace
+
+extern "C" int vit_splitk_reduce_group(const vit_splitk_job* jobs, int32_t n, vit_stream_t stream) {
+  VIT_CHECK_ARG(jobs && n >= 1 && n <= VIT_SPLITK_GROUP_MAX, "vit_splitk_reduce_group: 1..%d jobs, got %d",
+                VIT_SPLITK_GROUP_MAX, (int)n);
+  bool vec = true;
+  for (int k = 0; k < n; ++k) {
+    const vit_splitk_job& j = jobs[k];
+    VIT_CHECK_ARG(j.ws && j.out && j.batch >= 1 && j.split >= 1 && j.M >= 1 && j.N >= 1 && j.ldo >= j.N,
+                  "vit_splitk_reduce_group: job %d: bad args", k);
+    vec = vec && j.N % 4 == 0 && j.ldo % 4 == 0 && j.out_batch_stride % 4 == 0 && ((uintptr_t)j.ws % 16) == 0 &&
+          ((uintptr_t)j.out % 16) == 0;
+  }
+  if (!vec) {  // any job outside the vector form: one launch each
+    for (int k = 0; k < n; ++k) {
+      const vit_splitk_job& j = jobs[k];
+      if (const int rc = vit_splitk_reduce(j.ws, j.batch, j.split, j.M, j.N, j.out, j.ldo, j.out_batch_stride,
+                                           j.accumulate, stream))
+        return rc;
+    }
+    return VIT_OK;
+  }
+  SplitkGroupDev g{};
+  long blk = 0;
+  for (int k = 0; k < n; ++k) {
+    const vit_splitk_job& j = jobs[k];
+    long nb = (j.M * j.N / 4 + 255) / 256;
+    if (nb > 4096) nb = 4096;
+    SplitkJobDev& d = g.j[k];
+    d.ws = j.ws; d.out = j.out; d.M = j.M; d.N = j.N; d.ldo = j.ldo; d.obs = j.out_batch_stride;
+    d.split = (int)j.split; d.batch = (int)j.batch; d.nb = (int)nb; d.blk0 = (int)blk; d.acc = j.accumulate ? 1 : 0;
+    blk += nb * j.batch;
+  }
+  g.n = n;
+  VIT_CHECK_ARG(blk < (1L << 31), "vit_splitk_reduce_group: grid too large");
+  hipLaunchKernelGGL(splitk_reduce4_group_kernel, dim3((unsigned)blk), dim3(256), 0, (hipStream_t)stream, g);
+  VIT_LAUNCH_CHECK("vit_splitk_reduce_group");
+}
 
 extern "C" int vit_splitk_reduce(const float* ws, int64_t batch, int64_t split, int64_t M, int64_t N, float* out,
                                  int64_t ldo, int64_t out_batch_stride, int32_t accumulate, vit_stream_t stream) {

@@ -17,7 +17,7 @@ c_i32 = ctypes.c_int32
 c_f32 = ctypes.c_float
 c_vp = ctypes.c_void_p
 
-ABI_VERSION = 12  # vit_abi_version() of the library these prototypes describe
+ABI_VERSION = 13  # vit_abi_version() of the library these prototypes describe
 
 # enum vit_layout / vit_epilogue (include/vit_hip.h)
 K_CONTIG, MN_CONTIG = 0, 1
@@ -54,6 +54,15 @@ class ColsumJob(ctypes.Structure):
 
 COLSUM_BATCH_MAX = 8  # VIT_COLSUM_BATCH_MAX
 
+
+class SplitkJob(ctypes.Structure):
+    """struct vit_splitk_job (include/vit_hip.h)"""
+    _fields_ = [("ws", c_vp), ("batch", c_i64), ("split", c_i64), ("M", c_i64), ("N", c_i64), ("out", c_vp),
+                ("ldo", c_i64), ("out_batch_stride", c_i64), ("accumulate", c_i32), ("reserved", c_i32)]
+
+
+SPLITK_GROUP_MAX = 8  # VIT_SPLITK_GROUP_MAX
+
 # name -> (restype, argtypes)
 _SIGS = {
     "vit_last_error": (ctypes.c_char_p, []),
@@ -68,6 +77,7 @@ _SIGS = {
     "vit_router_dx_gate_partial_rows": (c_i64, [c_i64]),
     "vit_router_dx_gate": (c_i32, [c_vp, c_i64, c_vp, c_i64, c_f32, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp,
                                    c_i64, c_i64, c_i64, c_vp, c_i64, c_vp]),
+    "vit_splitk_reduce_group": (c_i32, [ctypes.POINTER(SplitkJob), c_i32, c_vp]),
     "vit_splitk_reduce": (c_i32, [c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_i64, c_i64, c_i32, c_vp]),
     "vit_layernorm_fwd": (c_i32, [c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_i32, c_vp, c_vp, c_i64, c_i64, c_f32, c_vp]),
     "vit_layernorm_bwd_partial_rows": (c_i64, [c_i64]),

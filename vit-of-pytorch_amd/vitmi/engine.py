@@ -424,9 +424,7 @@ class ViTEngine:
             ev1 = torch.cuda.Event(enable_timing=True)
             ev1.record()
             self.probe_wgrad.append((ev0, ev1, sum(2.0 * sp[4] * sp[5] * K * sp[9] for sp in specs), K))
-        for sp, w in zip(specs, views):
-            _, _, _, _, M, N, _, out, ldo, batch, _, out_bs = sp
-            ops.splitk_reduce(w, batch, s, M, N, out, ldo, out_bs)
+        ops.splitk_reduce_group([(w, sp[9], s, sp[4], sp[5], sp[7], sp[8], sp[11], False) for sp, w in zip(specs, views)])
 
     # ---- forward -------------------------------------------------------------------------------
     def _dd(self, site, row_stride=1):

@@ -123,6 +123,19 @@ def splitk_reduce(ws, batch, split, M, N, out, ldo, out_bs=0, accumulate=False):
           "vit_splitk_reduce")
 
 
+def splitk_reduce_group(jobs):
+    """several splitk_reduce calls in one launch (vit_splitk_reduce_group); jobs: [(ws, batch, split, M, N, out, ldo,
+    out_bs, accumulate)], each output bit-identical to its own splitk_reduce"""
+    for k in range(0, len(jobs), _lib.SPLITK_GROUP_MAX):
+        part = jobs[k:k + _lib.SPLITK_GROUP_MAX]
+        arr = (_lib.SplitkJob * len(part))()
+        for i, (ws, batch, split, M, N, out, ldo, out_bs, acc) in enumerate(part):
+            _chk(ws, F32, "ws")
+            _chk(out, F32, "out")
+            arr[i] = _lib.SplitkJob(_p(ws), batch, split, M, N, _p(out), ldo, out_bs, int(acc), 0)
+        check(lib().vit_splitk_reduce_group(arr, len(part), _stream()), "vit_splitk_reduce_group")
+
+
 def layernorm_fwd(x, ldx, gamma, beta, y, ldy, mean, rstd, rows, D, eps=1e-5):
     _chk(x, F32, "x")
     check(lib().vit_layernorm_fwd(_p(x), ldx, _p(gamma), _p(beta), _p(y), ldy, int(y.dtype == F32), _p(mean),

@@ -289,10 +289,18 @@ class _FusedLayer(torch.autograd.Function):
         ops.gemm(dqkv, b_all, v_all, T, r, D, a_layout=K_CONTIG, b_layout=MN_CONTIG, lda=3 * D, ldb=r8, ldc=KX,
                  epilogue=EPI_BF16, batch=3, a_bs=D, b_bs=D * r8, c_bs=r8)
         need = ctx.needs_input_grad
+        # dB_z and dA_z (batched over z): one grouped split-K launch and one grouped reduction, each at the split
+        # ops.wgrad would give it alone (bit-identical sums)
         dB = torch.empty(3, D, r, device=dev)
-        ops.wgrad(dqkv, 3 * D, a1[:, D:], Kq, D, r, Tp, dB, r, batch=3, a_bs=D, b_bs=r8, out_bs=D * r)
         dA = torch.empty(3, r, D, device=dev)
-        ops.wgrad(v_all, KX, a1, Kq, r, D, Tp, dA, D, batch=3, a_bs=r8, out_bs=r * D)
+        sB, sA = ops.splitk_factor(D, r, Tp, 3), ops.splitk_factor(r, D, Tp, 3)
+        wsB = torch.empty(3 * sB * D * r, device=dev)
+        wsA = torch.empty(3 * sA * r * D, device=dev)
+        kw = dict(a_layout=MN_CONTIG, b_layout=MN_CONTIG, epilogue=EPI_SPLITK, batch=3)
+        ops.gemm_splitk_group([(dqkv, a1[:, D:], wsB, D, r, Tp, dict(kw, lda=3 * D, ldb=Kq, ldc=r, a_bs=D, b_bs=r8,
+                                                                      split_k=sB)),
+                               (v_all, a1, wsA, r, D, Tp, dict(kw, lda=KX, ldb=Kq, ldc=D, a_bs=r8, split_k=sA))])
+        ops.splitk_reduce_group([(wsB, 3, sB, D, r, dB, r, D * r, False), (wsA, 3, sA, r, D, dA, D, r * D, False)])
         # q|k|v data gradient: dqkv W_qkv + v A (f32), then LN1 backward with the residual gradient
         dy1 = torch.empty(T, D, device=dev)
         ops.gemm(v_all, a_all, dy1, T, D, KX, a_layout=K_CONTIG, b_layout=MN_CONTIG, lda=KX, ldb=D, ldc=D,
@@ -545,9 +553,11 @@ def _finish_grads(K, wgrads, biases, params, need, marks, dev, own_split=False):
             members.append((A, B, w, M, N, K, dict(a_layout=MN_CONTIG, b_layout=MN_CONTIG, lda=lda, ldb=ldb, ldc=N,
                                                     epilogue=EPI_SPLITK, split_k=s)))
         ops.gemm_splitk_group(members)
+        jobs = []
         for s, (_, _, _, _, M, N, i), w in zip(ss, wgrads, views):
             d, acc = dst(i, (M, N))
-            ops.splitk_reduce(w, 1, s, M, N, d, N, 0, acc)
+            jobs.append((w, 1, s, M, N, d, N, 0, acc))
+        ops.splitk_reduce_group(jobs)
     jobs = []
     for part, rows, cols, i in biases:
         d, acc = dst(i, (cols,))
