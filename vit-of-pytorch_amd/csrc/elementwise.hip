@@ -1008,10 +1008,11 @@ __global__ void __launch_bounds__(256) segment_colsum_kernel(const void* __restr
 
 // out (bf16 [rows_pad][cols_pad]) = (dx[t][c] + [t % N >= reserve] * g_scale * g[t / N][c]) * gp[t][c] on the T x cols
 // block, rounded once to bf16, zero elsewhere; col_partial[blockIdx.y][c] = the column sums of the rounded values of
-// the block's RB rows. A thread owns a column pair (cols_pad, ldx, ldgp, ldo even) and walks the block's rows four at
-// a time, every load of the four issued before any use (one row at a time left the kernel waiting on HBM latency:
+// the block's RB rows. A thread owns a column pair (cols_pad, ldx, ldgp, ldo even) and walks the block's rows RDG_U at
+// a time, every load of the group issued before any use (one row at a time left the kernel waiting on HBM latency:
 // 72 us for 25 216 x 512), with the image / position counters stepped, not divided, per row
 constexpr int RDG_RB = 32;
+constexpr int RDG_U = 8;  // rows whose loads are in flight together
 __global__ void __launch_bounds__(256) router_dx_gate_kernel(const float* __restrict__ dx, long ldx,
                                                              const float* __restrict__ g, long ldg, float g_scale,
                                                              const bf16_t* __restrict__ gp, long ldgp, long T, long N,
@@ -1026,12 +1027,12 @@ __global__ void __launch_bounds__(256) router_dx_gate_kernel(const float* __rest
   const bool c0v = c < cols, c1v = c + 1 < cols;
   long img = r0 / N, pos = r0 - img * N;
   float a0 = 0.f, a1 = 0.f;
-  for (long t = r0; t < r1; t += 4) {
-    float2 dv[4], gv[4];
-    unsigned gu[4];
-    bool ok[4];
+  for (long t = r0; t < r1; t += RDG_U) {
+    float2 dv[RDG_U], gv[RDG_U];
+    unsigned gu[RDG_U];
+    bool ok[RDG_U];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < RDG_U; ++k) {
       ok[k] = c0v && t + k < tv;
       dv[k] = float2{0.f, 0.f};
       gv[k] = float2{0.f, 0.f};
@@ -1057,7 +1058,7 @@ __global__ void __launch_bounds__(256) router_dx_gate_kernel(const float* __rest
       }
     }
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < RDG_U; ++k) {
       if (t + k >= r1) break;
       unsigned o = 0u;
       if (ok[k]) {

@@ -85,10 +85,15 @@ def grad_sink(p, need=True):
 
 
 def sunk(p):
-    """after a node accumulated p's gradient through grad_sink: what AccumulateGrad's post hook would do"""
+    """after a node accumulated p's gradient through grad_sink: p's used flag (what AccumulateGrad's post hook
+    records). The gradient-exchange count (on_grad) is left to that hook, which autograd still runs for the None the
+    node returns, once per parameter and after every node that sinks into it (a parameter two nodes sink into — an
+    approximator applied at both layers of a block — then counts once, when its gradient is complete; counting here
+    as well made the data-parallel reducer launch buckets before the last contribution landed). Were the hook not
+    to run, the bucket would wait for the reducer's finish()."""
     f = p._vitmi_flat[0]()
     if f is not None:
-        f._mark(p)
+        f.used_host[f._index[id(p)]] = True
 
 
 def _rup(x, m):

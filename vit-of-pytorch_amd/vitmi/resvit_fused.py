@@ -26,6 +26,7 @@ weights trainable; grouped-query attention; shapes the kernels do not cover).
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 
@@ -91,6 +92,9 @@ ZERO_FULL = False
 # A/B switch (bench.py VITMI_RESVIT_PACK_EACH=1): False packs the LoRA factors and clears the q|k|v operand on
 # every call, as before round 4's shared pack
 SHARE_PACK = True
+# the fused layer's LoRA gradients accumulated straight into their flat .grad views (vitmi.flat.grad_sink); False:
+# returned to autograd (AccumulateGrad adds)
+LORA_SINK = os.environ.get("VITMI_RESVIT_LORA_SINK", "1") != "0"
 
 
 class _Frozen:
@@ -228,6 +232,7 @@ class _FusedLayer(torch.autograd.Function):
         if torch.is_grad_enabled() or any(ctx.needs_input_grad):
             ctx.save_for_backward(xf, a1, mu1, rs1, qkv, o, lse, h, mu2, rs2, gp, a_all, bq, bk, bv)
             ctx.block = block
+            ctx.lora = (aq, bq, ak, bk, av, bv)
             ctx.dims = (B, N, D, H, hd, M, r, r8, T, Tp, scale)
             ctx.gen = fz.gen if SHARE_PACK else None
         return out.view(B, N, D)
@@ -300,7 +305,22 @@ class _FusedLayer(torch.autograd.Function):
         ops.gemm_splitk_group([(dqkv, a1[:, D:], wsB, D, r, Tp, dict(kw, lda=3 * D, ldb=Kq, ldc=r, a_bs=D, b_bs=r8,
                                                                       split_k=sB)),
                                (v_all, a1, wsA, r, D, Tp, dict(kw, lda=KX, ldb=Kq, ldc=D, a_bs=r8, split_k=sA))])
-        ops.splitk_reduce_group([(wsB, 3, sB, D, r, dB, r, D * r, False), (wsA, 3, sA, r, D, dA, D, r * D, False)])
+        # each factor's gradient straight into its flat .grad view where it has one (no AccumulateGrad add), else
+        # into dA / dB
+        marks, jobs, grads = [], [], []
+        for z in range(3):
+            for ws_, s_, M_, N_, full, p_, nd in ((wsA, sA, r, D, dA, ctx.lora[2 * z], need[1 + 2 * z]),
+                                                   (wsB, sB, D, r, dB, ctx.lora[2 * z + 1], need[2 + 2 * z])):
+                slab = ws_[z * s_ * M_ * N_:(z + 1) * s_ * M_ * N_]
+                sk = _flat.grad_sink(p_, nd) if LORA_SINK else None
+                if sk is not None:
+                    jobs.append((slab, 1, s_, M_, N_, sk, N_, 0, True))
+                    marks.append(p_)
+                    grads.append(None)
+                else:
+                    jobs.append((slab, 1, s_, M_, N_, full[z], N_, 0, False))
+                    grads.append(full[z] if nd else None)
+        ops.splitk_reduce_group(jobs)
         # q|k|v data gradient: dqkv W_qkv + v A (f32), then LN1 backward with the residual gradient
         dy1 = torch.empty(T, D, device=dev)
         ops.gemm(v_all, a_all, dy1, T, D, KX, a_layout=K_CONTIG, b_layout=MN_CONTIG, lda=KX, ldb=D, ldc=D,
@@ -312,9 +332,7 @@ class _FusedLayer(torch.autograd.Function):
             dx = torch.empty(T, D, device=dev)
             ops.layernorm_bwd(dy1, D, xf, D, mu1, rs1, n1.weight, dx, D, part, T, D, dres=dh, lddres=D)
             dx = dx.view(B, N, D)
-        grads = []
-        for z in range(3):
-            grads += [dA[z] if need[1 + 2 * z] else None, dB[z] if need[2 + 2 * z] else None]
+        _sunk(marks)
         return (dx, *grads, None, None, None)
 
 
