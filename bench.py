@@ -338,11 +338,12 @@ def main():
     # launches (K = the b cls rows padded to 64) are reported beside it, not averaged in
     full_w = [p_ for p_ in probe_w if p_[3] >= T]
     pr_w = [p_ for p_ in probe_w if p_[3] < T]
-    wg_ms = [s_.elapsed_time(e_) for s_, e_, _, _ in full_w]
+    wg_ms = [p_[0].elapsed_time(p_[1]) for p_ in full_w]
+    n_group = sum(1 for p_ in full_w if p_[4])
     wg_flop = sum(p_[2] * T / p_[3] for p_ in full_w)  # algorithmic: the T real rows, not the padding
     wg_tflops = wg_flop / (sum(wg_ms) * 1e-3) / 1e12 if wg_ms else 0.0
     wg_avg_ms = sum(wg_ms) / max(1, len(wg_ms))
-    pr_ms = sum(s_.elapsed_time(e_) for s_, e_, _, _ in pr_w)
+    pr_ms = sum(p_[0].elapsed_time(p_[1]) for p_ in pr_w)
     imgs = args.steps * b * world
     value = imgs / dt
     fpi = train_flops_per_image(arch, args.image_size, args.num_classes)
@@ -355,7 +356,18 @@ def main():
     fpe = fpi - ((3 * 2 * (N_ - 1) * (D_ * D_ + 2 * D_ * M_) + 3 * 4 * (N_ - q_kept) * N_ * D_)
                  if eng.prune_last else 0)
     traffic = pmc_traffic() if args.arch == "b16" and b == 256 else None
-    traffic_w = pmc_traffic("gemm_pp2_kernel<false, false, 7,") if args.arch == "b16" and b == 256 else None
+    traffic_w = None
+    if args.arch == "b16" and b == 256:
+        # per-launch HBM bytes of the two weight-gradient kernels from their committed PMC passes, averaged over this
+        # step's launches of each (fc1 / fc2: gemm_pp2_kernel; out-proj + q|k|v: the grouped kernel)
+        t_pp2, t_grp = pmc_traffic("gemm_pp2_kernel<false, false, 7,"), pmc_traffic("gemm_pp2_group_kernel")
+        n_all = len(full_w)
+        if t_pp2 and (t_grp or n_group == 0) and n_all:
+            tb = (t_pp2["bytes"] * (n_all - n_group) + (t_grp["bytes"] if t_grp else 0) * n_group) / n_all
+            traffic_w = {"bytes": round(tb), "per_kernel": {"gemm_pp2_kernel<false, false, 7>": t_pp2,
+                                                            "gemm_pp2_group_kernel": t_grp},
+                         "launches": {"gemm_pp2_kernel<false, false, 7>": n_all - n_group,
+                                      "gemm_pp2_group_kernel": n_group}}
     step_tflops_per_gpu = value / world * fpi / 1e12
     out = {
         "metric": "images/sec training step, ViT-B/16 224px bf16, 1/2/4/8 MI355X" if args.arch == "b16" and

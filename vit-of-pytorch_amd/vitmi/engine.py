@@ -302,7 +302,7 @@ class ViTEngine:
         self._side = None
         self._ev_pool, self._ev_next = [], 0
         self.probe = None  # list: (start, end) HIP events around every fc1 forward GEMM launch
-        self.probe_wgrad = None  # list: (start, end, flop, K) around every split-K weight-gradient GEMM launch
+        self.probe_wgrad = None  # list: (start, end, flop, K, grouped) around every split-K weight-gradient GEMM launch
         # dropout (nn.Dropout of PositionEmbs / EncoderBlock / MlpBlock, reference src/model.py:19-20,
         # 46-49, 124-125): counter-based Philox masks keyed by (seed, per-forward offset, site, row,
         # col), regenerated by the backward instead of stored. Seeded from torch's initial seed.
@@ -395,7 +395,7 @@ class ViTEngine:
         if self.probe_wgrad is not None:
             ev1 = torch.cuda.Event(enable_timing=True)
             ev1.record()
-            self.probe_wgrad.append((ev0, ev1, 2.0 * M * N * K * batch, K))
+            self.probe_wgrad.append((ev0, ev1, 2.0 * M * N * K * batch, K, False))
         ops.splitk_reduce(ws, batch, s, M, N, out, ldo, out_bs)
 
     def _wgrad_group(self, specs):
@@ -423,7 +423,7 @@ class ViTEngine:
         if self.probe_wgrad is not None:
             ev1 = torch.cuda.Event(enable_timing=True)
             ev1.record()
-            self.probe_wgrad.append((ev0, ev1, sum(2.0 * sp[4] * sp[5] * K * sp[9] for sp in specs), K))
+            self.probe_wgrad.append((ev0, ev1, sum(2.0 * sp[4] * sp[5] * K * sp[9] for sp in specs), K, True))
         ops.splitk_reduce_group([(w, sp[9], s, sp[4], sp[5], sp[7], sp[8], sp[11], False) for sp, w in zip(specs, views)])
 
     # ---- forward -------------------------------------------------------------------------------
