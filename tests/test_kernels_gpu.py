@@ -246,6 +246,13 @@ def test_segment_colsum_and_router_dx_gate():
     rb = -(-rows_pad // nb)  # rows per partial block
     assert rb * nb == rows_pad
     assert torch.allclose(part, full.view(nb, rb, C).sum(1), rtol=1e-5, atol=1e-4)
+    # the branch-free column-pair kernel (even width, no padding columns): the same values
+    out2 = torch.full((rows_pad, C), float("nan"), device=DEV).bfloat16()
+    gp2 = gp[:, :C].contiguous()
+    part2 = torch.full((nb, C), float("nan"), device=DEV)
+    ops.router_dx_gate(dx, C, gs, C, scale, gp2, C, T, N, reserve, C, out2, C, part2, C)
+    assert torch.equal(out2[:T], ref) and (out2[T:].float() == 0).all()
+    assert torch.equal(part2, part)
 
 
 @pytest.mark.parametrize("tile", [1, 2, 6, 9])

@@ -1044,11 +1044,11 @@ __global__ void __launch_bounds__(256) router_dx_gate_kernel(const float* __rest
           dv[k] = *reinterpret_cast<const float2*>(d);
           if (pos >= reserve) {
             const float2 gg = *reinterpret_cast<const float2*>(gr);
-            gv[k] = float2{g_scale * gg.x, g_scale * gg.y};
+            gv[k] = float2{__fmul_rn(g_scale, gg.x), __fmul_rn(g_scale, gg.y)};
           }
         } else {
           dv[k].x = d[0];
-          if (pos >= reserve) gv[k].x = g_scale * gr[0];
+          if (pos >= reserve) gv[k].x = __fmul_rn(g_scale, gr[0]);
         }
         gu[k] = *reinterpret_cast<const unsigned*>(gp + (t + k) * ldgp + c);
       }
@@ -1062,8 +1062,8 @@ __global__ void __launch_bounds__(256) router_dx_gate_kernel(const float* __rest
       if (t + k >= r1) break;
       unsigned o = 0u;
       if (ok[k]) {
-        const bf16_t o0 = f2bf((dv[k].x + gv[k].x) * bf2f((bf16_t)(gu[k] & 0xffff)));
-        const bf16_t o1 = c1v ? f2bf((dv[k].y + gv[k].y) * bf2f((bf16_t)(gu[k] >> 16))) : (bf16_t)0;
+        const bf16_t o0 = f2bf(__fmul_rn(__fadd_rn(dv[k].x, gv[k].x), bf2f((bf16_t)(gu[k] & 0xffff))));
+        const bf16_t o1 = c1v ? f2bf(__fmul_rn(__fadd_rn(dv[k].y, gv[k].y), bf2f((bf16_t)(gu[k] >> 16)))) : (bf16_t)0;
         a0 += bf2f(o0);
         a1 += bf2f(o1);
         o = (unsigned)o0 | ((unsigned)o1 << 16);
@@ -1074,6 +1074,60 @@ __global__ void __launch_bounds__(256) router_dx_gate_kernel(const float* __rest
   if (col_partial) {
     if (c0v) col_partial[blockIdx.y * ldp + c] = a0;
     if (c1v) col_partial[blockIdx.y * ldp + c + 1] = a1;
+  }
+}
+
+// the common case of router_dx_gate_kernel (cols even and equal to cols_pad, T >= 1): no per-row branch, every load of
+// a group of RDG_U rows issued unconditionally (rows past T clamped to row T - 1 and their results discarded), so the
+// loads of a group are in flight together
+__global__ void __launch_bounds__(256) router_dx_gate_pair_kernel(const float* __restrict__ dx, long ldx,
+                                                                  const float* __restrict__ g, long ldg,
+                                                                  float g_scale, const bf16_t* __restrict__ gp,
+                                                                  long ldgp, long T, long N, long reserve, int cols,
+                                                                  bf16_t* __restrict__ out, long ldo, long rows_pad,
+                                                                  float* __restrict__ col_partial, long ldp) {
+  const int c = (blockIdx.x * 256 + threadIdx.x) * 2;
+  if (c >= cols) return;
+  const long r0 = (long)blockIdx.y * RDG_RB;
+  const long r1 = r0 + RDG_RB < rows_pad ? r0 + RDG_RB : rows_pad;
+  const long tlast = T - 1, ilast = (T - 1) / N;
+  long img = r0 / N, pos = r0 - img * N;
+  float a0 = 0.f, a1 = 0.f;
+  for (long t = r0; t < r1; t += RDG_U) {
+    float2 dv[RDG_U], gg[RDG_U];
+    unsigned gu[RDG_U];
+    float gs[RDG_U];
+#pragma unroll
+    for (int k = 0; k < RDG_U; ++k) {
+      const long rr = t + k < tlast ? t + k : tlast;
+      const long ii = img < ilast ? img : ilast;
+      dv[k] = *reinterpret_cast<const float2*>(dx + rr * ldx + c);
+      gg[k] = *reinterpret_cast<const float2*>(g + ii * ldg + c);
+      gu[k] = *reinterpret_cast<const unsigned*>(gp + rr * ldgp + c);
+      gs[k] = pos >= reserve ? g_scale : 0.f;
+      if (++pos == N) {
+        pos = 0;
+        ++img;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < RDG_U; ++k) {
+      if (t + k >= r1) break;
+      const bool ok = t + k < T;
+      // (no fma contraction: the same two roundings as (dx + s * g) * gp in f32 elsewhere)
+      const bf16_t o0 = f2bf(__fmul_rn(__fadd_rn(dv[k].x, __fmul_rn(gs[k], gg[k].x)), bf2f((bf16_t)(gu[k] & 0xffff))));
+      const bf16_t o1 = f2bf(__fmul_rn(__fadd_rn(dv[k].y, __fmul_rn(gs[k], gg[k].y)), bf2f((bf16_t)(gu[k] >> 16))));
+      const unsigned o = ok ? ((unsigned)o0 | ((unsigned)o1 << 16)) : 0u;
+      if (ok) {
+        a0 += bf2f(o0);
+        a1 += bf2f(o1);
+      }
+      *reinterpret_cast<unsigned*>(out + (t + k) * ldo + c) = o;
+    }
+  }
+  if (col_partial) {
+    col_partial[blockIdx.y * ldp + c] = a0;
+    col_partial[blockIdx.y * ldp + c + 1] = a1;
   }
 }
 }  // namespace
@@ -1110,6 +1164,12 @@ extern "C" int vit_router_dx_gate(const float* dx, int64_t ldx, const float* g, 
                 "wide as the padded output)");
   if (rows_pad == 0) return VIT_OK;
   const dim3 grid((unsigned)((cols_pad / 2 + 255) / 256), (unsigned)vit_router_dx_gate_partial_rows(rows_pad));
+  if (cols % 2 == 0 && cols == cols_pad && T >= 1) {
+    hipLaunchKernelGGL(router_dx_gate_pair_kernel, grid, dim3(256), 0, (hipStream_t)stream, dx, (long)ldx, g,
+                       (long)ldg, g_scale, (const bf16_t*)gp, (long)ldgp, (long)T, (long)N, (long)reserve, (int)cols,
+                       (bf16_t*)out, (long)ldo, (long)rows_pad, col_partial, (long)ldp);
+    VIT_LAUNCH_CHECK("vit_router_dx_gate");
+  }
   hipLaunchKernelGGL(router_dx_gate_kernel, grid, dim3(256), 0, (hipStream_t)stream, dx, (long)ldx, g, (long)ldg,
                      g_scale, (const bf16_t*)gp, (long)ldgp, (long)T, (long)N, (long)reserve, (int)cols, (bf16_t*)out,
                      (long)ldo, (long)rows_pad, (int)cols_pad, col_partial, (long)ldp);

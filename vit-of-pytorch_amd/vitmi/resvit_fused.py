@@ -595,13 +595,26 @@ def _mlp_backward(d2, T, xb, acts, ws, w1, w2, w3, need_dx, params, need, marks)
     g1, gp1, g2, gp2 = acts
     rp, kp, h1p, h2p = xb.shape[0], xb.shape[1], g1.shape[1], g2.shape[1]
     H1, H2, O, K1 = w1.shape[0], w2.shape[0], w3.shape[0], w1.shape[1]
-    db3 = _colsum(d2, T, O, O, params[5], need[5], marks)
     dlb = _pad_bf16(d2, rp, _rup(O, 64))
     du2, (p2, r2) = _dgrad_mul(dlb, ws[2], h2p, H2, T, gp2, h2p)
     du1, (p1, r1) = _dgrad_mul(du2, ws[1], h1p, H1, T, gp1, h1p)
     dx = _dgrad_f32(du1, ws[0], kp, K1, T) if need_dx else None
     wgrads = [(dlb, dlb.shape[1], g2, h2p, O, H2, 4), (du2, h2p, g1, h1p, H2, H1, 2), (du1, h1p, xb, kp, H1, K1, 0)]
     biases = [(p2, r2, H2, 3), (p1, r1, H1, 1)]
+    if O % 2 == 0:
+        # the output bias gradient (column sums of the f32 dY [T][O], O = 2): 64-row segment sums, summed with the
+        # other bias partials in _finish_grads' one column-sum launch (the generic narrow-column reduction took
+        # two launches and ~30 us at T = 25 216)
+        nseg, tail = T // 64, T % 64
+        p3 = torch.empty(nseg + (1 if tail else 0) or 1, O, device=d2.device, dtype=F32)
+        if nseg:
+            ops.segment_colsum(d2, O, nseg, 64, O, p3, O)
+        if tail:
+            ops.segment_colsum(d2[nseg * 64:], O, 1, tail, O, p3[nseg:], O)
+        biases.append((p3, nseg + (1 if tail else 0), O, 5))
+        db3 = None  # (in _finish_grads' result, index 5)
+    else:
+        db3 = _colsum(d2, T, O, O, params[5], need[5], marks)
     return dx, du1, wgrads, biases, db3
 
 
@@ -637,7 +650,8 @@ class _RouterMLP(torch.autograd.Function):
                                                    ctx.needs_input_grad[0], ctx.params, need, marks)
         g = _finish_grads(xb.shape[0], wgrads, biases, ctx.params, need, marks, d2.device)
         _sunk(marks)
-        return (dx.reshape(*lead, K1) if dx is not None else None, g[0], g[1], g[2], g[3], g[4], db3)
+        return (dx.reshape(*lead, K1) if dx is not None else None, g[0], g[1], g[2], g[3], g[4],
+                g[5] if db3 is None else db3)
 
 
 class _RouterNet(torch.autograd.Function):
@@ -726,7 +740,8 @@ class _RouterNet(torch.autograd.Function):
         dg = gb[:D] if need_ln else None
         dbt = gb[D:] if need_ln else None
         _sunk(marks)
-        return (dx.view(B, N, D), dg, dbt, g[0], g[1], g[2], g[3], g[4], g[5], g[6], db3, None, None)
+        return (dx.view(B, N, D), dg, dbt, g[0], g[1], g[2], g[3], g[4], g[5], g[6], g[7] if db3 is None else db3,
+                None, None)
 
 
 def router_mlp_supported(seq, x):
