@@ -394,6 +394,10 @@ class BlockPathApproximators(nn.Module):
 
 # the routed student's where(active, layer(x), x) folded into the fused layer node (False: torch.where after it)
 FOLD_SELECT = True
+# where the teacher's input is the student's (the first routed layer), one grad-enabled layer forward gives both the
+# teacher output (detached) and the student's (row selection after it) instead of a no-grad teacher pass plus a
+# folded student pass (False: the two passes)
+SHARE_TEACHER = True
 
 
 def _select_rows(mask, a, b):
@@ -467,6 +471,11 @@ class TransformerBlock(nn.Module):
                                                           torch.int64))
 
         if self.training:
+            if (SHARE_TEACHER and (teacher_x is None or teacher_x is x) and self.fused and x.dim() == 3 and x.is_cuda
+                    and _fused.supported(self)):
+                # the teacher's input is the student's (the first routed layer): one layer forward serves both
+                teacher_out, student_out = _fused.teacher_and_student(self, x, active)
+                return teacher_out, approximators(student_out, router_indices, lra_lora), w, block_info
             # teacher: every token, every layer. Its outputs reach the loss only through DistillLoss's
             # .detach() (res-vit/model.py:40-59), so no gradient flows through it: run without autograd
             with torch.no_grad():

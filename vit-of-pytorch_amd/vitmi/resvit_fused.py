@@ -350,6 +350,40 @@ def full_layer(block, x, packed=False, active=None):
                              None if active is None else active.contiguous())
 
 
+class _RowsSelect(torch.autograd.Function):
+    """where(active, full, x) for [B, N, D] f32 rows (active: bool [B, N, 1]) on vit_rows_select: forward a copy of
+    full with x's rows where inactive, backward dout's active rows to full and its inactive rows to x"""
+
+    @staticmethod
+    def forward(ctx, full, x, active):
+        B, N, D = full.shape
+        m = active.reshape(B * N).contiguous()
+        out = full.contiguous().clone()
+        ops.rows_select(out.view(B * N, D), m, x.contiguous().view(B * N, D))
+        ctx.save_for_backward(m)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        (m,) = ctx.saved_tensors
+        B, N, D = dout.shape
+        d = dout.contiguous()
+        dfull = d.clone()
+        ops.rows_select(dfull.view(B * N, D), m)  # inactive rows: 0
+        dx = d.clone()
+        ops.rows_select(dx.view(B * N, D), torch.logical_not(m))  # active rows: 0
+        return dfull, dx, None
+
+
+def teacher_and_student(block, x, active):
+    """The first routed layer, whose teacher input is the student's (res-vit/model.py:496-512 with teacher_x = x):
+    the full layer runs once with autograd, the teacher output is its detached value and the student output
+    where(active, it, x) — the same values as a no-grad teacher pass plus a folded student pass, one layer forward
+    fewer"""
+    full = full_layer(block, x)
+    return full.detach(), _RowsSelect.apply(full, x, active)
+
+
 # ---- routed low-rank approximator step (res-vit/model.py:319-368) ------------------------------------
 class _ApproxStep(torch.autograd.Function):
     """x_new = where(sel, x + up(down(x)), x) for one approximator of BlockPathApproximators (training path),
