@@ -328,6 +328,16 @@ int vit_cast_f32_bf16(const float* in, void* out, int64_t n, vit_stream_t stream
 /* out bf16 [rows][ldo] <- in f32 [rows][cols]; columns cols..ldo-1 are zeroed. */
 int vit_cast_pad_rows(const float* in, int64_t rows, int64_t cols, void* out, int64_t ldo,
                       vit_stream_t stream);
+/* up to VIT_CAST_BATCH_MAX casts in ONE launch: out[r*ldo + c] (bf16) = in[r*ldi + c] for r < rows, c < cols, zero for
+ * the rest of [rows_pad][cols_pad] (small weight / operand casts of the Res-ViT nodes, one launch per node) */
+#define VIT_CAST_BATCH_MAX 8
+typedef struct vit_cast_job {
+  const float* in;
+  int64_t rows, cols, ldi;
+  void* out;
+  int64_t ldo, rows_pad, cols_pad;
+} vit_cast_job;
+int vit_cast_pad_batch(const vit_cast_job* jobs, int32_t njobs, vit_stream_t stream);
 /* out[r*ldo + z*cols + c] = in[z*zstride + r*ldi + c]  (z < Z), as bf16 (out_bf16) or f32.
  * Packs q/k/v LinearGeneral weights [D][H,hd] (src/model.py:73-75) into one [D][3D] operand. */
 int vit_pack_cols(const float* in, int64_t zstride, int64_t ldi, int64_t rows, int64_t cols, int64_t Z,

@@ -211,6 +211,26 @@ def test_splitk_reduce_group_equals_single_reductions():
         assert acc or torch.equal(a, b)
 
 
+def test_cast_pad_batch_matches_single_casts():
+    """vit_cast_pad_batch: jobs of different shapes (a strided column block, row and column padding, an empty
+    source) in one launch equal their bf16 casts with zeros in the padding, bit for bit"""
+    g = torch.Generator(device="cpu").manual_seed(13)
+    src = [torch.randn(5, 37, generator=g).to(DEV), torch.randn(64, 8, generator=g).to(DEV)[:, :6],
+           torch.randn(3, 100, generator=g).to(DEV)]
+    outs = [torch.full((8, 64), float("nan"), device=DEV).bfloat16(), torch.full((64, 16), float("nan"),
+                                                                                  device=DEV).bfloat16(),
+            torch.full((4, 128), float("nan"), device=DEV).bfloat16()]
+    jobs = [(src[0], 5, 37, 37, outs[0], 64, 8, 64), (src[1], 64, 6, 8, outs[1], 16, 64, 8),
+            (src[2], 0, 0, 100, outs[2], 128, 4, 100)]
+    ops.cast_pad_batch(jobs)
+    ref0 = torch.zeros(8, 64, device=DEV).bfloat16()
+    ref0[:5, :37] = src[0].bfloat16()
+    assert torch.equal(outs[0], ref0)
+    assert torch.equal(outs[1][:, :6], src[1].bfloat16()) and (outs[1][:, 6:8].float() == 0).all()
+    assert torch.isnan(outs[1][:, 8:].float()).all()  # past cols_pad: untouched
+    assert (outs[2][:, :100].float() == 0).all() and torch.isnan(outs[2][:, 100:].float()).all()
+
+
 def test_segment_colsum_and_router_dx_gate():
     """the Res-ViT router backward helpers against torch: per-image token sums (bf16 and f32 inputs), and
     bf16((dx + [t % N >= reserve] s g[t // N]) * gp) with zero padding and per-row-block column partials of the

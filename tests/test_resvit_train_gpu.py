@@ -578,6 +578,30 @@ def test_grad_sinks_only_inside_training_backward(gold):
     assert float(opt.flat.grad.abs().sum()) == 0.0  # nothing was sunk into the flat gradient
 
 
+def test_each_parameter_counted_once_per_backward(gold):
+    """The data-parallel bucket count (FlatParams.on_grad) sees every trainable parameter exactly once per training
+    backward, although the fused nodes sink their gradients into the flat .grad views and autograd's post hook
+    still runs for the None they return (round 5: counted in both places, the reducer launched buckets early), and
+    every parameter that took a gradient is flagged used."""
+    from collections import Counter
+    from vitmi.optim import AdamW
+    from vitmi.resvit_train import train_step
+    m = build(gold).train()
+    opt = AdamW(m.parameters(), lr=1e-4, weight_decay=0.05, max_grad_norm=1.0)
+    seen = []
+    opt.flat.on_grad = seen.append
+    x = torch.from_numpy(gold["s0/x"]).cuda()
+    y = torch.from_numpy(gold["s0/y"]).cuda()
+    train_step(m, x, y, opt, None, 10.0, 1.0, 10.0, True, None)
+    torch.cuda.synchronize()
+    c = Counter(seen)
+    assert c and max(c.values()) == 1, {i: n for i, n in c.items() if n > 1}
+    names = {id(p): n for n, p in m.named_parameters()}
+    sunk_kinds = [names[id(opt.flat.params[i])] for i in c]
+    assert any("lora_A" in n for n in sunk_kinds) and any("router" in n for n in sunk_kinds)
+    assert all(opt.flat.used_host[i] for i in c)
+
+
 def test_zero_grad_clears_stale_gates():
     """flat.gate ORs a forward's participation flag into an existing entry; FlatParams.zero_grad drops the
     entries of its parameters, so a flag left by a forward no step consumed cannot mark the next step used."""

@@ -726,6 +726,55 @@ extern "C" int vit_cast_pad_rows(const float* in, int64_t rows, int64_t cols, vo
   VIT_LAUNCH_CHECK("vit_cast_pad_rows");
 }
 
+// ---- batched f32 -> bf16 casts into zero-padded operands: several small weight / operand casts in one launch -----
+namespace {
+struct CastJobDev {
+  const float* in;
+  bf16_t* out;
+  long rows, cols, ldi, ldo, rows_pad, cols_pad;
+  int blk0, nb;
+};
+struct CastBatchDev {
+  CastJobDev j[VIT_CAST_BATCH_MAX];
+  int n;
+};
+__global__ void __launch_bounds__(256) cast_pad_batch_kernel(const CastBatchDev bt) {
+  int jx = 0;
+#pragma unroll
+  for (int k = 1; k < VIT_CAST_BATCH_MAX; ++k)
+    if (k < bt.n && (int)blockIdx.x >= bt.j[k].blk0) jx = k;
+  const CastJobDev& J = bt.j[jx];
+  const long total = J.rows_pad * J.cols_pad;
+  for (long i = (long)(blockIdx.x - J.blk0) * 256 + threadIdx.x; i < total; i += (long)J.nb * 256) {
+    const long r = i / J.cols_pad, c = i - r * J.cols_pad;
+    J.out[r * J.ldo + c] = r < J.rows && c < J.cols ? f2bf(J.in[r * J.ldi + c]) : (bf16_t)0;
+  }
+}
+}  // namespace
+
+extern "C" int vit_cast_pad_batch(const vit_cast_job* jobs, int32_t njobs, vit_stream_t stream) {
+  VIT_CHECK_ARG(jobs && njobs >= 1 && njobs <= VIT_CAST_BATCH_MAX, "vit_cast_pad_batch: 1..%d jobs, got %d",
+                VIT_CAST_BATCH_MAX, (int)njobs);
+  CastBatchDev bt{};
+  long blk = 0;
+  for (int k = 0; k < njobs; ++k) {
+    const vit_cast_job& j = jobs[k];
+    VIT_CHECK_ARG(j.in && j.out && j.rows >= 0 && j.cols >= 0 && j.ldi >= j.cols && j.rows_pad >= j.rows &&
+                      j.cols_pad >= j.cols && j.ldo >= j.cols_pad,
+                  "vit_cast_pad_batch: job %d: bad shape", k);
+    long nb = (j.rows_pad * j.cols_pad + 255) / 256;
+    if (nb > 2048) nb = 2048;
+    if (nb < 1) nb = 1;
+    CastJobDev& d = bt.j[k];
+    d.in = j.in; d.out = (bf16_t*)j.out; d.rows = j.rows; d.cols = j.cols; d.ldi = j.ldi; d.ldo = j.ldo;
+    d.rows_pad = j.rows_pad; d.cols_pad = j.cols_pad; d.blk0 = (int)blk; d.nb = (int)nb;
+    blk += nb;
+  }
+  bt.n = njobs;
+  hipLaunchKernelGGL(cast_pad_batch_kernel, dim3((unsigned)blk), dim3(256), 0, (hipStream_t)stream, bt);
+  VIT_LAUNCH_CHECK("vit_cast_pad_batch");
+}
+
 extern "C" int vit_axpby(const float* x, float* y, int64_t n, float a, float b, vit_stream_t stream) {
   VIT_CHECK_ARG(x && y && n >= 0, "vit_axpby: bad args");
   if (n == 0) return VIT_OK;

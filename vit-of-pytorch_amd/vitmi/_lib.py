@@ -17,7 +17,7 @@ c_i32 = ctypes.c_int32
 c_f32 = ctypes.c_float
 c_vp = ctypes.c_void_p
 
-ABI_VERSION = 13  # vit_abi_version() of the library these prototypes describe
+ABI_VERSION = 14  # vit_abi_version() of the library these prototypes describe
 
 # enum vit_layout / vit_epilogue (include/vit_hip.h)
 K_CONTIG, MN_CONTIG = 0, 1
@@ -63,6 +63,15 @@ class SplitkJob(ctypes.Structure):
 
 SPLITK_GROUP_MAX = 8  # VIT_SPLITK_GROUP_MAX
 
+
+class CastJob(ctypes.Structure):
+    """struct vit_cast_job (include/vit_hip.h)"""
+    _fields_ = [("inp", c_vp), ("rows", c_i64), ("cols", c_i64), ("ldi", c_i64), ("out", c_vp), ("ldo", c_i64),
+                ("rows_pad", c_i64), ("cols_pad", c_i64)]
+
+
+CAST_BATCH_MAX = 8  # VIT_CAST_BATCH_MAX
+
 # name -> (restype, argtypes)
 _SIGS = {
     "vit_last_error": (ctypes.c_char_p, []),
@@ -78,6 +87,7 @@ _SIGS = {
     "vit_router_dx_gate": (c_i32, [c_vp, c_i64, c_vp, c_i64, c_f32, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp,
                                    c_i64, c_i64, c_i64, c_vp, c_i64, c_vp]),
     "vit_splitk_reduce_group": (c_i32, [ctypes.POINTER(SplitkJob), c_i32, c_vp]),
+    "vit_cast_pad_batch": (c_i32, [ctypes.POINTER(CastJob), c_i32, c_vp]),
     "vit_splitk_reduce": (c_i32, [c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_i64, c_i64, c_i32, c_vp]),
     "vit_layernorm_fwd": (c_i32, [c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_i32, c_vp, c_vp, c_i64, c_i64, c_f32, c_vp]),
     "vit_layernorm_bwd_partial_rows": (c_i64, [c_i64]),

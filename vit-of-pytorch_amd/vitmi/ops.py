@@ -277,6 +277,19 @@ def cast_pad_rows(inp, rows, cols, out, ldo):
     check(lib().vit_cast_pad_rows(_p(inp), rows, cols, _p(out), ldo, _stream()), "vit_cast_pad_rows")
 
 
+def cast_pad_batch(jobs):
+    """several f32 -> bf16 casts into zero-padded buffers in one launch per 8 (vit_cast_pad_batch); jobs: [(inp f32
+    [rows][>= cols] row stride ldi, rows, cols, ldi, out bf16 (row stride ldo), ldo, rows_pad, cols_pad)]"""
+    for k in range(0, len(jobs), _lib.CAST_BATCH_MAX):
+        part = jobs[k:k + _lib.CAST_BATCH_MAX]
+        arr = (_lib.CastJob * len(part))()
+        for i, (inp, rows, cols, ldi, out, ldo, rows_pad, cols_pad) in enumerate(part):
+            _chk(inp, F32, "inp")
+            _chk(out, BF16, "out")
+            arr[i] = _lib.CastJob(_p(inp), rows, cols, ldi, _p(out), ldo, rows_pad, cols_pad)
+        check(lib().vit_cast_pad_batch(arr, len(part), _stream()), "vit_cast_pad_batch")
+
+
 def axpby(x, y, n, a, b):
     check(lib().vit_axpby(_p(x), _p(y), n, a, b, _stream()), "vit_axpby")
 

@@ -118,10 +118,12 @@ class _Frozen:
         Kq = D + KX
         if self.a_all is None or self.a_all.shape != (KX, D) or self.a_all.device != aq.device:
             self.a_all = torch.zeros(KX, D, device=aq.device, dtype=BF16)
-        for z, A in enumerate((aq, ak, av)):
-            ops.cast_pad_rows(A.detach().float().contiguous(), r, D, self.a_all[z * r8:], D)
-        for z, Bz in enumerate((bq, bk, bv)):
-            ops.pack_cols(Bz.detach().float().contiguous(), 0, r, D, r, 1, self.wcat[z * D:, D + z * r8:], Kq)
+        # A_z into rows z*r8.. of A_all, B_z into columns D + z*r8.. of wcat: one launch
+        jobs = [(A.detach().float().contiguous(), r, D, D, self.a_all[z * r8:], D, r, D)
+                for z, A in enumerate((aq, ak, av))]
+        jobs += [(Bz.detach().float().contiguous(), D, r, r, self.wcat[z * D:, D + z * r8:], Kq, D, r)
+                 for z, Bz in enumerate((bq, bk, bv))]
+        ops.cast_pad_batch(jobs)
         self.gen += 1
         return self.a_all
 
@@ -287,8 +289,8 @@ class _FusedLayer(torch.autograd.Function):
         ops.attention_bwd(qkv, o, dO, lse, dqkv, B, N, H, hd, scale)
         # LoRA: v_z = dq_z B_z (batched), dB_z = dq_z^T u_z, dA_z = v_z^T LN1(x)
         b_all = torch.empty(3, D, r8, device=dev, dtype=BF16)  # rows written whole (zero-padded to r8) below
-        for z, Bz in enumerate((bq, bk, bv)):
-            ops.cast_pad_rows(Bz.detach().float().contiguous(), D, r, b_all[z], r8)
+        ops.cast_pad_batch([(Bz.detach().float().contiguous(), D, r, r, b_all[z], r8, D, r8)
+                            for z, Bz in enumerate((bq, bk, bv))])
         v_all = torch.empty(Tp, KX, device=dev, dtype=BF16)
         ops.zero_(v_all)
         ops.gemm(dqkv, b_all, v_all, T, r, D, a_layout=K_CONTIG, b_layout=MN_CONTIG, lda=3 * D, ldb=r8, ldc=KX,
@@ -403,19 +405,15 @@ class _ApproxStep(torch.autograd.Function):
         kp, rp, rk = _rup(D, 64), _rup(max(T, 1), 64), _rup(r, 64)
         dev = x.device
         x2 = x.contiguous().float().view(T, D)
-        xb = torch.empty(rp, kp, device=dev, dtype=BF16)
-        ops.cast_pad_rows(x2, T, D, xb, kp)
-        if rp > T:
-            ops.zero_(xb[T:])
-        # Wd [r][D] and Wu [D][r] as bf16, rows and columns padded to 64 with zeros: the forward's K-contiguous B
-        # operands, and unchanged the backward's M/N-contiguous ones (cast once per step)
-        wdb = _pad_bf16(wd.detach().float().contiguous(), rk, kp)  # B(k, n) = Wd[n][k]: K-contiguous
+        # x, and Wd [r][D] and Wu [D][r], as bf16 with rows and columns padded to 64 with zeros, in one launch: the
+        # forward's operands (Wd, Wu K-contiguous B) and, unchanged, the backward's M/N-contiguous ones
+        xb, wdb, wub = _pad_bf16_many([(x2, rp, kp), (wd.detach().float().contiguous(), rk, kp),
+                                       (wu.detach().float().contiguous(), kp, rk)])
         hb = _alloc_pad(rp, rk, T, r, dev)
         ops.gemm(xb, wdb, hb, T, r, kp, a_layout=K_CONTIG, b_layout=K_CONTIG, lda=kp, ldb=kp, ldc=rk,
                  epilogue=EPI_BF16)
         selb = sel.reshape(T, 1).to(BF16)
         hb[:T].mul_(selb)  # unselected rows: h = 0 (exact)
-        wub = _pad_bf16(wu.detach().float().contiguous(), kp, rk)  # B(k, n) = Wu[n][k]: K-contiguous over r
         out = torch.empty(T, D, device=dev, dtype=F32)
         ops.gemm(hb, wub, out, T, D, rk, a_layout=K_CONTIG, b_layout=K_CONTIG, lda=rk, ldb=rk, ldc=D,
                  epilogue=EPI_BIAS_RESID_F32, bias=_zero_row(D, dev), aux=x2, ldaux=D)
@@ -431,10 +429,7 @@ class _ApproxStep(torch.autograd.Function):
         kp, rp, rk = xb.shape[1], xb.shape[0], hb.shape[1]
         dev = dout.device
         d2 = dout.contiguous().float().view(T, D)
-        db = torch.empty(rp, kp, device=dev, dtype=BF16)
-        ops.cast_pad_rows(d2, T, D, db, kp)
-        if rp > T:
-            ops.zero_(db[T:])
+        (db,) = _pad_bf16_many([(d2, rp, kp)])
         # dh = dout Wu: B(kk = n, n' = j) = Wu[n][j], M/N-contiguous (the forward's padded [kp][rk] copy), rounded to
         # the bf16 operand by the GEMM's epilogue (the same RNE rounding as a cast of the f32 product)
         dhb = _alloc_pad(rp, rk, T, r, dev)
@@ -470,6 +465,18 @@ def approx_step(m, x, sel):
 
 
 # ---- router MLP (RouterModule.out_conv, res-vit/model.py:150-156,190) ----------------------------------
+def _pad_bf16_many(items):
+    """[_pad_bf16(x2, rows_p, cols_p) for each item] in one launch (vit_cast_pad_batch per 8)"""
+    outs, jobs = [], []
+    for x2, rows_p, cols_p in items:
+        rows, cols = x2.shape
+        out = torch.empty(rows_p, cols_p, device=x2.device, dtype=BF16)
+        outs.append(out)
+        jobs.append((x2, rows, cols, x2.stride(0), out, cols_p, rows_p, cols_p))
+    ops.cast_pad_batch(jobs)
+    return outs
+
+
 def _pad_bf16(x2, rows_p, cols_p):
     rows, cols = x2.shape
     out = torch.empty(rows_p, cols_p, device=x2.device, dtype=BF16)
@@ -517,18 +524,19 @@ def _weight_pads(w1, w2, w3, kp, h1p, h2p):
     B operands and, unchanged, the backward's M/N-contiguous B operands of the data gradients (K = the padded output
     rows)"""
     H1, H2, O = w1.shape[0], w2.shape[0], w3.shape[0]
-    return [_pad_bf16(w.detach().float().contiguous(), _rup(n, 64), k)
-            for w, n, k in ((w1, H1, kp), (w2, H2, h1p), (w3, O, h2p))]
+    return _pad_bf16_many([(w.detach().float().contiguous(), _rup(n, 64), k)
+                           for w, n, k in ((w1, H1, kp), (w2, H2, h1p), (w3, O, h2p))])
 
 
-def _mlp_forward(xb, T, kp, w1, b1, w2, b2, w3, b3):
+def _mlp_forward(xb, T, kp, w1, b1, w2, b2, w3, b3, ws=None):
     """the router's out_conv on a bf16 operand xb [rp][kp] (T valid rows): hidden layers as one GEMM each whose
     epilogue writes GELU(u) (the next operand) and GELU'(u) (kept for the backward); returns (logits f32 [T][O],
     saved activations, padded bf16 weights)"""
     rp, dev = xb.shape[0], xb.device
     H1, H2, O = w1.shape[0], w2.shape[0], w3.shape[0]
     h1p, h2p = _rup(H1, 64), _rup(H2, 64)
-    ws = _weight_pads(w1, w2, w3, kp, h1p, h2p)
+    if ws is None:
+        ws = _weight_pads(w1, w2, w3, kp, h1p, h2p)
     acts = []
     a_in, k_in = xb, kp
     for (b, n, npad), wb in zip(((b1, H1, h1p), (b2, H2, h2p)), ws[:2]):
@@ -629,7 +637,7 @@ def _mlp_backward(d2, T, xb, acts, ws, w1, w2, w3, need_dx, params, need, marks)
     g1, gp1, g2, gp2 = acts
     rp, kp, h1p, h2p = xb.shape[0], xb.shape[1], g1.shape[1], g2.shape[1]
     H1, H2, O, K1 = w1.shape[0], w2.shape[0], w3.shape[0], w1.shape[1]
-    dlb = _pad_bf16(d2, rp, _rup(O, 64))
+    (dlb,) = _pad_bf16_many([(d2, rp, _rup(O, 64))])
     du2, (p2, r2) = _dgrad_mul(dlb, ws[2], h2p, H2, T, gp2, h2p)
     du1, (p1, r1) = _dgrad_mul(du2, ws[1], h1p, H1, T, gp1, h1p)
     dx = _dgrad_f32(du1, ws[0], kp, K1, T) if need_dx else None
@@ -715,7 +723,12 @@ class _RouterNet(torch.autograd.Function):
         if T:
             ops.layernorm_fwd(x2, D, ln_w.detach().float().contiguous(), ln_b.detach().float().contiguous(), lnb, dp,
                               mean, rstd, T, D, eps)
-        w0b = _pad_bf16(w0.detach().float().contiguous(), h0p, dp)
+        # in_conv's and out_conv's padded bf16 weights: one launch
+        H1, H2, O = w1.shape[0], w2.shape[0], w3.shape[0]
+        h1p, h2p = _rup(H1, 64), _rup(H2, 64)
+        w0b, *ws = _pad_bf16_many([(w0.detach().float().contiguous(), h0p, dp)] +
+                                  [(w.detach().float().contiguous(), _rup(n, 64), k)
+                                   for w, n, k in ((w1, H1, kp), (w2, H2, h1p), (w3, O, h2p))])
         xcat = _alloc_pad(rp, kp, T, K1, dev)  # [x_embed | global] operand of out_conv
         gp0 = _alloc_pad(rp, h0p, T, Hh, dev)
         if T:
@@ -725,7 +738,7 @@ class _RouterNet(torch.autograd.Function):
         glob = torch.empty(B, Hh, device=dev, dtype=F32)  # [B][h]: mean of the bf16 x_embed values, reserved tokens out
         ops.segment_colsum(xcat, kp, B, N - reserve, Hh, glob, Hh, seg_stride=N, row0=reserve, scale=1.0 / (N - reserve))
         xc[:, :, Hh:K1].copy_(glob.to(BF16)[:, None, :])
-        out, acts, ws = _mlp_forward(xcat, T, kp, w1, b1, w2, b2, w3, b3)
+        out, acts, ws = _mlp_forward(xcat, T, kp, w1, b1, w2, b2, w3, b3, ws=ws)
         ctx.save_for_backward(x2, mean, rstd, ln_w, lnb, gp0, xcat, *acts, w0b, *ws, w1)
         ctx.params = (w0, b0, w1, b1, w2, b2, w3, b3)
         ctx.dims = (B, N, D, T, Hh, K1, reserve)
