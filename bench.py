@@ -507,6 +507,8 @@ def bench_resvit(args, world, rank, dev, backend, comm):
     if os.environ.get("VITMI_RESVIT_PACK_EACH", "0") != "0":  # A/B: LoRA operands packed on every layer call
         from vitmi import resvit_fused
         resvit_fused.SHARE_PACK = False
+    if os.environ.get("VITMI_RESVIT_NO_CLS_TAP", "0") != "0":  # A/B: cls-row slices and the all-row final norm
+        resvit.CLS_TAP = False
     if os.environ.get("VITMI_RESVIT_TEACHER_PASS", "0") != "0":  # A/B: a separate no-grad teacher pass everywhere
         resvit.SHARE_TEACHER = False
     if os.environ.get("VITMI_RESVIT_WHERE_OPS", "0") != "0":  # A/B: the routed row selection as torch.where

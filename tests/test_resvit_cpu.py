@@ -74,6 +74,11 @@ def test_b16_constructor_and_rescale_match_reference_fingerprints(golden_dir):
     tame(m)
     sd = m.state_dict()
     assert sorted(k[3:] for k in g.files if k.startswith("fp/")) == sorted(sd.keys())
+    # f64 reductions of the same tensor differ in the last bits with the host's thread count / vector width (seen on
+    # the GPU box: 255.9355755825659 vs 255.93557558256592), so compare to 1e-12 relative: a different initialiser
+    # or rescale moves these by many orders more.
     for k, v in sd.items():
         t = v.double()
-        assert float(t.sum()) == float(g["fp/" + k][0]) and float((t * t).sum()) == float(g["fp/" + k][1]), k
+        fs, fq = float(g["fp/" + k][0]), float(g["fp/" + k][1])
+        assert abs(float(t.sum()) - fs) <= 1e-12 * max(1.0, float(t.abs().sum())), k
+        assert abs(float((t * t).sum()) - fq) <= 1e-12 * max(1.0, fq), k

@@ -27,7 +27,7 @@ y = torch.randint(0, 100, (128,), device="cuda", generator=g)
 for _ in range(3):
     train_step(model, x, y, opt, sched, 1e-4, 1e-2, 1.0, True, None)
 torch.cuda.synchronize()
-with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], with_stack=True) as prof:
+with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], with_stack=True, record_shapes=True) as prof:
     for _ in range(2):
         train_step(model, x, y, opt, sched, 1e-4, 1e-2, 1.0, True, None)
     torch.cuda.synchronize()
@@ -41,3 +41,10 @@ for e in rows[:45]:
     frames = [f for f in e.stack if "vitmi" in f or "bench" in f][:4]
     print(f"{e.key:12s} n={e.count:4d} dev={e.self_device_time_total / 1e3:7.3f} ms  " + " <- ".join(
         f.split("/")[-1] for f in frames), flush=True)
+
+# the glue ops by input shape (which tensors they touch: the backward's ops carry no Python frames)
+shp = [e for e in prof.key_averages(group_by_input_shape=True) if e.key in ("aten::copy_", "aten::add", "aten::add_",
+                                                                           "aten::fill_", "aten::mean", "aten::mul")]
+shp.sort(key=lambda e: -e.self_device_time_total)
+for e in shp[:40]:
+    print(f"{e.key:12s} n={e.count:4d} dev={e.self_device_time_total / 1e3:7.3f} ms  {str(e.input_shapes)[:150]}", flush=True)

@@ -398,6 +398,9 @@ FOLD_SELECT = True
 # teacher output (detached) and the student's (row selection after it) instead of a no-grad teacher pass plus a
 # folded student pass (False: the two passes)
 SHARE_TEACHER = True
+# the distillation loss's cls rows taken through vitmi.resvit_fused.cls_tap (their gradient added in place), and the
+# final LayerNorm on the cls rows only (False: the slices and the all-row norm as written)
+CLS_TAP = True
 
 
 def _select_rows(mask, a, b):
@@ -558,7 +561,11 @@ class Transformer(nn.Module):
             if self.use_reslr and layer.layer_id >= layer.dynamic_start_layer:
                 if self.training:
                     teacher_out, student_out, w, block_info = layer(student_x, teacher_x, block_info, self.LRA_mask)
-                    d_loss = d_loss + self.criterion_distill(student_out[:, 0, :], teacher_out[:, 0, :])
+                    if CLS_TAP and student_out.is_cuda:
+                        student_out, s_cls = _fused.cls_tap(student_out)
+                    else:
+                        s_cls = student_out[:, 0, :]
+                    d_loss = d_loss + self.criterion_distill(s_cls, teacher_out[:, 0, :])
                     if layer.is_block_head:
                         bid = layer.current_block_id
                         r_entropy = r_entropy + block_info[f"block_{bid}_router_entropy"]
@@ -577,7 +584,12 @@ class Transformer(nn.Module):
                 else:
                     student_x, w, block_info = layer(student_x, None, block_info)
             self.acts.append(w)
-        student_x = self.norm(student_x)
+        # the final LayerNorm is row-local and only the cls row reaches the classifier (res-vit/model.py:686-689):
+        # normalise that row alone (same values; the other rows' zero gradient through the norm is exactly zero)
+        if CLS_TAP:
+            student_x = self.norm(student_x[:, 0:1])
+        else:
+            student_x = self.norm(student_x)
         activation = torch.cat(self.acts, dim=-1)
         output = self.classifier(student_x[:, 0])
         self.logits = output

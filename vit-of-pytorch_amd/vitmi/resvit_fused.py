@@ -377,6 +377,31 @@ class _RowsSelect(torch.autograd.Function):
         return dfull, dx, None
 
 
+class _ClsTap(torch.autograd.Function):
+    """(x, x[:, 0, :]) with the cls rows' gradient added into x's incoming gradient in place: autograd's own slice
+    backward materialises a zero [B, N, D] tensor, copies the rows in and adds it to the layer gradient (three
+    passes over T x D f32 per routed layer, for the distillation loss on the cls token)"""
+
+    @staticmethod
+    def forward(ctx, x):
+        ctx.shape = x.shape
+        return x.view(x.shape), x[:, 0, :].clone()
+
+    @staticmethod
+    def backward(ctx, dx, dcls):
+        if dx is None:
+            dx = torch.zeros(ctx.shape, device=dcls.device, dtype=dcls.dtype)
+        if dcls is not None:
+            dx = dx.contiguous()
+            dx[:, 0, :] += dcls
+        return dx
+
+
+def cls_tap(x):
+    """x, and its cls rows x[:, 0, :] for a loss, without the full-size zero gradient of a slice (_ClsTap)"""
+    return _ClsTap.apply(x)
+
+
 def teacher_and_student(block, x, active):
     """The first routed layer, whose teacher input is the student's (res-vit/model.py:496-512 with teacher_x = x):
     the full layer runs once with autograd, the teacher output is its detached value and the student output
