@@ -399,6 +399,21 @@ int64_t vit_router_dx_gate_partial_rows(int64_t rows_pad);
 int vit_router_dx_gate(const float* dx, int64_t ldx, const float* g, int64_t ldg, float g_scale, const void* gp,
                        int64_t ldgp, int64_t T, int64_t N, int64_t reserve, int64_t cols, void* out, int64_t ldo,
                        int64_t rows_pad, int64_t cols_pad, float* col_partial, int64_t ldp, vit_stream_t stream);
+/* Res-ViT router head (res-vit/model.py:191-211, RouterModule.forward after out_conv), logits f32 [T][bs][2], T = B*N:
+ *   soft = softmax(logits); entropy[0] = -(sum over tokens t % N >= reserve of p log(p + 1e-8)) / norm (per-block
+ *   partials in ent_part[vit_router_head_partials(T)], then a fixed-order sum); training: y_soft = softmax(logits + g),
+ *   g = noise (noise_mode 1) or -log(noise) (2: exponential draws) or 0 (0), hard = (y_hard - y_soft) + y_soft with
+ *   y_hard = yhard_in or the one-hot of argmax y_soft; evaluation: hard = yhard_in or the one-hot of argmax soft;
+ *   rows of reserved tokens (t % N < reserve) = (0, 1); indices[t] = sum_i hard[t][i][1] 2^(bs-1-i).
+ * vit_router_head_bwd: dlogits from dsoft, the entropy gradient dent[0] and (training) the straight-through
+ *   gradients dhard / dind through y_soft; any of dsoft / dhard / dind / dent may be NULL. */
+int64_t vit_router_head_partials(int64_t T);
+int vit_router_head_fwd(const float* logits, const float* noise, int32_t noise_mode, const float* yhard_in, int64_t T,
+                        int64_t N, int32_t bs, int64_t reserve, int32_t training, float norm, float* soft, float* ysoft,
+                        float* hard, float* indices, float* ent_part, float* entropy, vit_stream_t stream);
+int vit_router_head_bwd(const float* soft, const float* ysoft, const float* dsoft, const float* dhard, const float* dind,
+                        const float* dent, float norm, int64_t T, int64_t N, int32_t bs, int64_t reserve,
+                        int32_t training, float* dlogits, vit_stream_t stream);
 /* out[r*ldo + c] = f32(in[r*ldi + c]) for bf16 `in` (attention outputs / gradients back to f32 modules) */
 int vit_unpack_bf16_f32(const void* in, int64_t ldi, int64_t rows, int64_t cols, float* out, int64_t ldo,
                         vit_stream_t stream);

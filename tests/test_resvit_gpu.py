@@ -211,3 +211,46 @@ def test_b16_train_step_matches_reference(golden_b16):
             bad.append((n, mine, ref))
     assert not bad, bad
     assert all(p.grad is None for n, p in m.named_parameters() if not p.requires_grad)
+
+
+@pytest.mark.parametrize("bs,reserve,training", [(1, 1, True), (2, 1, True), (4, 0, True), (1, 1, False),
+                                                 (2, 2, False)])
+@pytest.mark.parametrize("mode", ["gumbel", "expo", "override"])
+def test_router_head_matches_per_op(bs, reserve, training, mode):
+    """the fused router head (vitmi.resvit_fused.router_head: softmax, entropy, Gumbel straight-through decision,
+    reserved rows, pattern index in one node) against RouterModule's per-op head on the same logits and draws: soft,
+    hard and indices bit-identical, the entropy to f32 summation order; the logits' gradient from the soft
+    probabilities, the entropy and (training) the straight-through outputs within 1e-5"""
+    from vitmi import resvit
+    torch.manual_seed(5)
+    B, N = 3, 37
+    r = resvit.RouterModule(64, 32, reserve, 1e-5, block_size=bs).cuda().train(training)
+    base = torch.randn(B, N, bs, 2, device="cuda") * 3
+    base[0, 5] = 0.0  # tied logits: argmax takes the first index
+    g = -torch.empty_like(base).exponential_().log()
+    yh = torch.zeros_like(base).scatter_(-1, torch.randint(0, 2, (B, N, bs, 1), device="cuda"), 1.0)
+    w_soft, w_hard, w_idx = (torch.randn(B, N, bs, 2, device="cuda"), torch.randn(B, N, bs, 2, device="cuda"),
+                             torch.randn(B, N, 1, device="cuda"))
+    outs = {}
+    for fused in (False, True):
+        resvit.FUSED_HEAD = fused
+        try:
+            r.gumbel_noise = (lambda lg: g) if mode == "gumbel" else None
+            r.hard_override = (lambda lg: yh) if mode == "override" else None
+            logits = base.clone().requires_grad_(True)
+            torch.cuda.manual_seed(11)  # the same exponential draws for both paths (mode "expo")
+            hard, idx, ent, soft = r.head(logits)
+            loss = (soft * w_soft).sum() + 0.7 * ent
+            if training:
+                loss = loss + (hard * w_hard).sum() + (idx * w_idx).sum()
+            loss.backward()
+            outs[fused] = [t.detach() for t in (hard, idx, ent, soft)] + [logits.grad]
+        finally:
+            resvit.FUSED_HEAD = True
+    (h0, i0, e0, s0, d0), (h1, i1, e1, s1, d1) = outs[False], outs[True]
+    assert h1.shape == h0.shape and i1.shape == i0.shape and e1.shape == e0.shape and s1.shape == s0.shape
+    assert torch.equal(s1, s0)
+    assert torch.equal(h1, h0)
+    assert torch.equal(i1, i0)
+    assert abs(float(e1) - float(e0)) <= 1e-6 * abs(float(e0)) + 1e-7
+    assert rel(d1, d0) < 1e-5

@@ -4,4 +4,4 @@ set -o pipefail
 export TMPDIR=/tmp
 O=gpurun_out/r05n; mkdir -p $O
 timeout -k 10 400 python3 -u tools/resvit_prof.py > $O/resvit_prof.txt 2>&1 || { tail -20 $O/resvit_prof.txt; exit 1; }
-tail -50 $O/resvit_prof.txt
+tail -120 $O/resvit_prof.txt

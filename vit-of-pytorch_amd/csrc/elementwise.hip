@@ -1245,3 +1245,182 @@ extern "C" int vit_unpack_bf16_f32(const void* in, int64_t ldi, int64_t rows, in
                      (const bf16_t*)in, (long)ldi, (long)rows, (int)cols, out, (long)ldo);
   VIT_LAUNCH_CHECK("vit_unpack_bf16_f32");
 }
+
+// ---- Res-ViT router head (res-vit/model.py:191-211: RouterModule.forward after out_conv) ----------------------------
+// Per token t and block position i (logits [T][bs][2], T = B * N rows): soft = softmax(logits) in the arithmetic of
+// torch's two-element warp softmax (max, exp(x - max), sum, x / sum); the entropy term p log(p + 1e-8) summed over the
+// non-reserved tokens (block partials, then one fixed-order sum); in training y_soft = softmax(logits + g) with the
+// Gumbel noise g given (noise_mode 1) or as -log of the exponential draws (noise_mode 2), the one-hot of its argmax (or
+// the caller's y_hard) and the straight-through value (y_hard - y_soft) + y_soft; in evaluation the one-hot of argmax
+// soft; reserved tokens' rows set to (0, 1); the pattern index sum_i hard[t][i][1] 2^(bs-1-i). Replaces ~25 ATen launches
+// per routed layer.
+namespace {
+constexpr int RH_THREADS = 256;
+constexpr int RH_BS_MAX = 8;
+
+__device__ __forceinline__ void softmax2(float a, float b, float& p0, float& p1) {
+  const float m = a >= b ? a : b;
+  const float e0 = expf(a - m), e1 = expf(b - m);
+  const float s = e0 + e1;
+  p0 = e0 / s;
+  p1 = e1 / s;
+}
+
+__global__ void __launch_bounds__(RH_THREADS) router_head_fwd_kernel(const float* __restrict__ logits,
+                                                                     const float* __restrict__ noise, int noise_mode,
+                                                                     const float* __restrict__ yhard_in, long T, int N,
+                                                                     int bs, int reserve, int training,
+                                                                     float* __restrict__ soft, float* __restrict__ ysoft,
+                                                                     float* __restrict__ hard,
+                                                                     float* __restrict__ indices,
+                                                                     float* __restrict__ ent_part) {
+  __shared__ float red[RH_THREADS];
+  const long t = (long)blockIdx.x * RH_THREADS + threadIdx.x;
+  float ent = 0.f;
+  if (t < T) {
+    const bool res = (int)(t % N) < reserve;
+    float idx = 0.f;
+    for (int i = 0; i < bs; ++i) {
+      const long q = (t * bs + i) * 2;
+      const float l0 = logits[q], l1 = logits[q + 1];
+      float p0, p1;
+      softmax2(l0, l1, p0, p1);
+      soft[q] = p0;
+      soft[q + 1] = p1;
+      if (!res) ent += p0 * logf(p0 + 1e-8f) + p1 * logf(p1 + 1e-8f);
+      float h0, h1;
+      if (training) {
+        float g0 = 0.f, g1 = 0.f;
+        if (noise_mode == 1) {
+          g0 = noise[q];
+          g1 = noise[q + 1];
+        } else if (noise_mode == 2) {
+          g0 = -logf(noise[q]);
+          g1 = -logf(noise[q + 1]);
+        }
+        float y0, y1;
+        softmax2(l0 + g0, l1 + g1, y0, y1);
+        ysoft[q] = y0;
+        ysoft[q + 1] = y1;
+        float yh0, yh1;
+        if (yhard_in) {
+          yh0 = yhard_in[q];
+          yh1 = yhard_in[q + 1];
+        } else {
+          yh1 = y1 > y0 ? 1.f : 0.f;  // (the first index on a tie, as torch's max)
+          yh0 = 1.f - yh1;
+        }
+        h0 = (yh0 - y0) + y0;
+        h1 = (yh1 - y1) + y1;
+      } else if (yhard_in) {
+        h0 = yhard_in[q];
+        h1 = yhard_in[q + 1];
+      } else {
+        h1 = p1 > p0 ? 1.f : 0.f;
+        h0 = 1.f - h1;
+      }
+      if (res) {
+        h0 = 0.f;
+        h1 = 1.f;
+      }
+      hard[q] = h0;
+      hard[q + 1] = h1;
+      idx = fmaf(h1, (float)(1 << (bs - 1 - i)), idx);
+    }
+    indices[t] = idx;
+  }
+  red[threadIdx.x] = ent;
+  __syncthreads();
+  for (int s = RH_THREADS / 2; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) ent_part[blockIdx.x] = red[0];
+}
+
+// entropy[0] = -(sum of the block partials, fixed order) / norm
+__global__ void __launch_bounds__(RH_THREADS) router_head_ent_kernel(const float* __restrict__ part, int n, float norm,
+                                                                     float* __restrict__ entropy) {
+  __shared__ float red[RH_THREADS];
+  float s = 0.f;
+  for (int k = threadIdx.x; k < n; k += RH_THREADS) s += part[k];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int w = RH_THREADS / 2; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) entropy[0] = -red[0] / norm;
+}
+
+// dlogits: the softmax backward of (dsoft + the entropy term's gradient) and, in training, of the straight-through
+// path (dhard, and dindices through the pattern index) on y_soft; reserved tokens' hard rows take no gradient
+__global__ void __launch_bounds__(RH_THREADS) router_head_bwd_kernel(const float* __restrict__ soft,
+                                                                     const float* __restrict__ ysoft,
+                                                                     const float* __restrict__ dsoft,
+                                                                     const float* __restrict__ dhard,
+                                                                     const float* __restrict__ dind,
+                                                                     const float* __restrict__ dent, float norm, long T,
+                                                                     int N, int bs, int reserve, int training,
+                                                                     float* __restrict__ dlogits) {
+  const long t = (long)blockIdx.x * RH_THREADS + threadIdx.x;
+  if (t >= T) return;
+  const bool res = (int)(t % N) < reserve;
+  const float ge = dent && !res ? -dent[0] / norm : 0.f;  // d entropy / d (sum of p log(p + 1e-8))
+  for (int i = 0; i < bs; ++i) {
+    const long q = (t * bs + i) * 2;
+    const float p0 = soft[q], p1 = soft[q + 1];
+    float d0 = dsoft ? dsoft[q] : 0.f, d1 = dsoft ? dsoft[q + 1] : 0.f;
+    if (ge != 0.f) {
+      d0 += ge * (logf(p0 + 1e-8f) + p0 / (p0 + 1e-8f));
+      d1 += ge * (logf(p1 + 1e-8f) + p1 / (p1 + 1e-8f));
+    }
+    const float sd = d0 * p0 + d1 * p1;
+    float o0 = p0 * (d0 - sd), o1 = p1 * (d1 - sd);
+    if (training && ysoft && !res && (dhard || dind)) {
+      float h0 = dhard ? dhard[q] : 0.f, h1 = dhard ? dhard[q + 1] : 0.f;
+      if (dind) h1 += dind[t] * (float)(1 << (bs - 1 - i));
+      const float y0 = ysoft[q], y1 = ysoft[q + 1];
+      const float sy = h0 * y0 + h1 * y1;
+      o0 += y0 * (h0 - sy);
+      o1 += y1 * (h1 - sy);
+    }
+    dlogits[q] = o0;
+    dlogits[q + 1] = o1;
+  }
+}
+}  // namespace
+
+extern "C" int64_t vit_router_head_partials(int64_t T) { return (T + RH_THREADS - 1) / RH_THREADS; }
+
+extern "C" int vit_router_head_fwd(const float* logits, const float* noise, int32_t noise_mode, const float* yhard_in,
+                                   int64_t T, int64_t N, int32_t bs, int64_t reserve, int32_t training, float norm,
+                                   float* soft, float* ysoft, float* hard, float* indices, float* ent_part,
+                                   float* entropy, vit_stream_t stream) {
+  VIT_CHECK_ARG(logits && soft && hard && indices && ent_part && entropy && T >= 0 && N > 0 && reserve >= 0 &&
+                    bs >= 1 && bs <= RH_BS_MAX && noise_mode >= 0 && noise_mode <= 2 && (noise_mode == 0 || noise) &&
+                    (!training || ysoft) && norm > 0.f && T < (1L << 40),
+                "vit_router_head_fwd: bad args (bs 1..%d, noise_mode 0..2 with noise, ysoft in training, norm > 0)",
+                RH_BS_MAX);
+  const long nb = (long)vit_router_head_partials(T);
+  if (nb > 0)
+    hipLaunchKernelGGL(router_head_fwd_kernel, dim3((unsigned)nb), dim3(RH_THREADS), 0, (hipStream_t)stream, logits,
+                       noise, (int)noise_mode, yhard_in, (long)T, (int)N, (int)bs, (int)reserve, (int)training, soft,
+                       ysoft, hard, indices, ent_part);
+  hipLaunchKernelGGL(router_head_ent_kernel, dim3(1), dim3(RH_THREADS), 0, (hipStream_t)stream, ent_part, (int)nb, norm,
+                     entropy);
+  VIT_LAUNCH_CHECK("vit_router_head_fwd");
+}
+
+extern "C" int vit_router_head_bwd(const float* soft, const float* ysoft, const float* dsoft, const float* dhard,
+                                   const float* dind, const float* dent, float norm, int64_t T, int64_t N, int32_t bs,
+                                   int64_t reserve, int32_t training, float* dlogits, vit_stream_t stream) {
+  VIT_CHECK_ARG(soft && dlogits && T >= 0 && N > 0 && reserve >= 0 && bs >= 1 && bs <= RH_BS_MAX && norm > 0.f &&
+                    (!training || ysoft),
+                "vit_router_head_bwd: bad args");
+  if (T == 0) return VIT_OK;
+  hipLaunchKernelGGL(router_head_bwd_kernel, dim3((unsigned)vit_router_head_partials(T)), dim3(RH_THREADS), 0,
+                     (hipStream_t)stream, soft, ysoft, dsoft, dhard, dind, dent, norm, (long)T, (int)N, (int)bs,
+                     (int)reserve, (int)training, dlogits);
+  VIT_LAUNCH_CHECK("vit_router_head_bwd");
+}

@@ -377,6 +377,41 @@ def router_dx_gate(dx, ldx, g, ldg, g_scale, gp, ldgp, T, N, reserve, cols, out,
           "vit_router_dx_gate")
 
 
+def router_head_fwd(logits, noise, noise_mode, yhard, N, reserve, training, norm):
+    """the Res-ViT router head on logits f32 [T][bs][2] (vit_router_head_fwd): returns (soft, y_soft or None, hard,
+    indices [T], entropy [] ) as new f32 tensors; noise_mode 1: noise = Gumbel g, 2: noise = exponential draws"""
+    _chk(logits, F32, "logits")
+    T, bs = logits.shape[0], logits.shape[1]
+    for t, n in ((noise, "noise"), (yhard, "yhard")):
+        if t is not None:
+            _chk(t, F32, n)
+            if tuple(t.shape) != tuple(logits.shape):
+                raise ValueError(f"router_head_fwd: {n} shape {tuple(t.shape)} != logits {tuple(logits.shape)}")
+    dev = logits.device
+    soft, hard = torch.empty_like(logits), torch.empty_like(logits)
+    ysoft = torch.empty_like(logits) if training else None
+    idx = torch.empty(T, device=dev, dtype=F32)
+    part = torch.empty(max(int(lib().vit_router_head_partials(T)), 1), device=dev, dtype=F32)
+    ent = torch.empty((), device=dev, dtype=F32)
+    check(lib().vit_router_head_fwd(_p(logits), _p(noise), int(noise_mode), _p(yhard), T, N, bs, reserve, int(training),
+                                    float(norm), _p(soft), _p(ysoft), _p(hard), _p(idx), _p(part), _p(ent), _stream()),
+          "vit_router_head_fwd")
+    return soft, ysoft, hard, idx, ent
+
+
+def router_head_bwd(soft, ysoft, dsoft, dhard, dind, dent, N, reserve, training, norm):
+    """dlogits f32 [T][bs][2] of router_head_fwd's outputs (vit_router_head_bwd); any gradient may be None"""
+    _chk(soft, F32, "soft")
+    for t, n in ((ysoft, "ysoft"), (dsoft, "dsoft"), (dhard, "dhard"), (dind, "dind"), (dent, "dent")):
+        if t is not None:
+            _chk(t, F32, n)
+    T, bs = soft.shape[0], soft.shape[1]
+    dl = torch.empty_like(soft)
+    check(lib().vit_router_head_bwd(_p(soft), _p(ysoft), _p(dsoft), _p(dhard), _p(dind), _p(dent), float(norm), T, N,
+                                    bs, reserve, int(training), _p(dl), _stream()), "vit_router_head_bwd")
+    return dl
+
+
 def unpack_bf16_f32(inp, ldi, rows, cols, out, ldo):
     """out[r*ldo + c] = f32(inp[r*ldi + c])"""
     _chk(inp, BF16, "inp")

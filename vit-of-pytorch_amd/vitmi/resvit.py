@@ -242,6 +242,23 @@ class RouterModule(nn.Module):
                 logits = _fused.router_mlp(self.out_conv, fused).view(B, N, self.block_size, 2)
             else:
                 logits = self.out_conv(fused).view(B, N, self.block_size, 2)
+        return self.head(logits)
+
+    def head(self, logits):
+        """(hard, indices, entropy, soft) from the router's logits [B, N, block_size, 2] (res-vit/model.py:191-211)"""
+        B, N = logits.shape[:2]
+        r = self.reserve_initials
+        if FUSED_HEAD and self.fused_mlp and _fused.router_head_supported(logits, r):
+            # softmax, entropy, Gumbel hard routing, reserved rows and the pattern index as one node
+            noise, mode, yh = None, 0, None
+            if self.training:
+                if self.gumbel_noise is not None:
+                    noise, mode = self.gumbel_noise(logits), 1
+                else:  # the same draws as the per-op path; -log is taken inside the node
+                    noise, mode = torch.empty_like(logits).exponential_(), 2
+            if self.hard_override is not None:
+                yh = self.hard_override(logits)
+            return _fused.router_head(logits, noise, mode, yh, r, self.training, B * (N - r) * self.block_size)
         soft = F.softmax(logits, dim=-1)
         probs = soft[:, r:]
         entropy = -torch.sum(probs * torch.log(probs + 1e-8)) / (B * (N - r) * self.block_size)
@@ -401,6 +418,9 @@ SHARE_TEACHER = True
 # the distillation loss's cls rows taken through vitmi.resvit_fused.cls_tap (their gradient added in place), and the
 # final LayerNorm on the cls rows only (False: the slices and the all-row norm as written)
 CLS_TAP = True
+# the router's softmax / entropy / Gumbel hard routing / pattern index as one fused node (vitmi.resvit_fused.router_head;
+# False: the per-op path as written)
+FUSED_HEAD = True
 
 
 def _select_rows(mask, a, b):

@@ -402,6 +402,49 @@ def cls_tap(x):
     return _ClsTap.apply(x)
 
 
+class _RouterHead(torch.autograd.Function):
+    """RouterModule.forward after out_conv (res-vit/model.py:191-211) as one node: softmax, the entropy, the Gumbel
+    hard decision with its straight-through value, the reserved tokens' rows and the pattern index in one launch (plus
+    the entropy's fixed-order sum), one launch backward (vit_router_head_fwd / _bwd). The ~25 ATen launches it replaces
+    per routed layer (softmax, log, mul, sum, neg, div, log, neg, add, softmax, max, zeros, scatter, sub, add, clone,
+    two fills, a cast and the index matmul) each move a few hundred KB. Same arithmetic per element as those ops (soft,
+    y_soft, hard and the index bit-identical); the entropy is summed in a different order."""
+
+    @staticmethod
+    def forward(ctx, logits, noise, noise_mode, yhard, reserve, training, norm):
+        ctx.set_materialize_grads(False)
+        B, N, bs, _ = logits.shape
+        l2 = logits.detach().contiguous().view(B * N, bs, 2)
+        nz = noise.detach().float().contiguous().view(B * N, bs, 2) if noise is not None else None
+        yh = yhard.detach().float().contiguous().view(B * N, bs, 2) if yhard is not None else None
+        soft, ysoft, hard, idx, ent = ops.router_head_fwd(l2, nz, noise_mode, yh, N, reserve, training, norm)
+        ctx.save_for_backward(soft, ysoft)
+        ctx.dims = (B, N, bs, reserve, bool(training), float(norm))
+        if not training:
+            ctx.mark_non_differentiable(hard, idx)
+        return hard.view(B, N, bs, 2), idx.view(B, N, 1), ent, soft.view(B, N, bs, 2)
+
+    @staticmethod
+    def backward(ctx, dhard, didx, dent, dsoft):
+        soft, ysoft = ctx.saved_tensors
+        B, N, bs, reserve, training, norm = ctx.dims
+        f = lambda t, *shape: t.float().contiguous().reshape(shape) if t is not None else None
+        dl = ops.router_head_bwd(soft, ysoft, f(dsoft, B * N, bs, 2), f(dhard, B * N, bs, 2), f(didx, B * N),
+                                 f(dent), N, reserve, training, norm)
+        return dl.view(B, N, bs, 2), None, None, None, None, None, None
+
+
+def router_head_supported(logits, reserve):
+    B, N, bs, two = logits.shape
+    return logits.is_cuda and logits.dtype == F32 and two == 2 and 1 <= bs <= 8 and B * (N - reserve) * bs > 0
+
+
+def router_head(logits, noise, noise_mode, yhard, reserve, training, norm):
+    """(hard, indices, entropy, soft) of RouterModule.forward from its logits [B, N, bs, 2] as one node (_RouterHead);
+    noise_mode 1: noise is the Gumbel noise, 2: exponential draws (g = -log), 0: none (evaluation)"""
+    return _RouterHead.apply(logits, noise, int(noise_mode), yhard, int(reserve), bool(training), float(norm))
+
+
 def teacher_and_student(block, x, active):
     """The first routed layer, whose teacher input is the student's (res-vit/model.py:496-512 with teacher_x = x):
     the full layer runs once with autograd, the teacher output is its detached value and the student output
