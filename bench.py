@@ -507,6 +507,8 @@ def bench_resvit(args, world, rank, dev, backend, comm):
     if os.environ.get("VITMI_RESVIT_PACK_EACH", "0") != "0":  # A/B: LoRA operands packed on every layer call
         from vitmi import resvit_fused
         resvit_fused.SHARE_PACK = False
+    if os.environ.get("VITMI_RESVIT_NO_FUSED_DISTILL", "0") != "0":  # A/B: cls_tap + torch's mse_loss per layer
+        resvit.FUSED_DISTILL = False
     if os.environ.get("VITMI_RESVIT_NO_FUSED_HEAD", "0") != "0":  # A/B: the router head as separate ATen ops
         resvit.FUSED_HEAD = False
     if os.environ.get("VITMI_RESVIT_NO_CLS_TAP", "0") != "0":  # A/B: cls-row slices and the all-row final norm

@@ -395,6 +395,11 @@ int vit_add_bcast_f32(const float* x, const float* y, float* out, int64_t outer,
  *   (vit_router_dx_gate_partial_rows(rows_pad) blocks; reduce with vit_colsum_batch) */
 int vit_segment_colsum(const void* in, int32_t in_bf16, int64_t ld, int64_t segs, int64_t seg_stride, int64_t row0,
                        int64_t seg_rows, int64_t cols, float scale, float* out, int64_t ldo, vit_stream_t stream);
+/* vit_segment_colsum, and each segment's result rounded to bf16 into rows [s*seg_stride, + bc_rows) of bc (ld ldbc):
+ * the router's per-image token mean broadcast into the global half of out_conv's operand (res-vit/model.py:188-189) */
+int vit_segment_colsum_bcast(const void* in, int32_t in_bf16, int64_t ld, int64_t segs, int64_t seg_stride,
+                             int64_t row0, int64_t seg_rows, int64_t cols, float scale, float* out, int64_t ldo,
+                             void* bc, int64_t ldbc, int64_t bc_rows, vit_stream_t stream);
 int64_t vit_router_dx_gate_partial_rows(int64_t rows_pad);
 int vit_router_dx_gate(const float* dx, int64_t ldx, const float* g, int64_t ldg, float g_scale, const void* gp,
                        int64_t ldgp, int64_t T, int64_t N, int64_t reserve, int64_t cols, void* out, int64_t ldo,
@@ -414,6 +419,13 @@ int vit_router_head_fwd(const float* logits, const float* noise, int32_t noise_m
 int vit_router_head_bwd(const float* soft, const float* ysoft, const float* dsoft, const float* dhard, const float* dind,
                         const float* dent, float norm, int64_t T, int64_t N, int32_t bs, int64_t reserve,
                         int32_t training, float* dlogits, vit_stream_t stream);
+/* Res-ViT distillation loss on the cls rows (res-vit/model.py:40-59: mse_loss(student[:, 0], teacher[:, 0])):
+ * vit_cls_mse: e[b][d] = x[b*ldx + d] - t[b*ldt + d], loss[0] = (sum of e^2, per-row partials part[B] then a fixed
+ *   order) / (B D); vit_cls_mse_bwd: dx[b*lddx + d] += ((2 / (B D)) e[b][d]) g[0] (device scalar g). */
+int vit_cls_mse(const float* x, int64_t ldx, const float* t, int64_t ldt, int64_t B, int64_t D, float* e, float* part,
+                float* loss, vit_stream_t stream);
+int vit_cls_mse_bwd(float* dx, int64_t lddx, const float* e, int64_t B, int64_t D, const float* g,
+                    vit_stream_t stream);
 /* out[r*ldo + c] = f32(in[r*ldi + c]) for bf16 `in` (attention outputs / gradients back to f32 modules) */
 int vit_unpack_bf16_f32(const void* in, int64_t ldi, int64_t rows, int64_t cols, float* out, int64_t ldo,
                         vit_stream_t stream);

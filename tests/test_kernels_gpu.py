@@ -231,6 +231,28 @@ def test_cast_pad_batch_matches_single_casts():
     assert (outs[2][:, :100].float() == 0).all() and torch.isnan(outs[2][:, 100:].float()).all()
 
 
+@pytest.mark.parametrize("C", [200, 199])
+def test_segment_colsum_bcast(C):
+    """vit_segment_colsum_bcast (the router forward's token mean, broadcast as bf16 into the global half of out_conv's
+    operand): the means as segment_colsum's, bit for bit, and each image's rows of the right half equal to their bf16
+    rounding; the left half (the input) and the padding rows untouched"""
+    g = torch.Generator(device="cpu").manual_seed(6)
+    Bn, N, reserve, ld = 3, 50, 1, 2 * 256
+    buf = torch.randn(Bn * N + 6, ld, generator=g).bfloat16().to(DEV)
+    before = buf.clone()
+    ref = torch.empty(Bn, C, device=DEV)
+    ops.segment_colsum(buf, ld, Bn, N - reserve, C, ref, C, seg_stride=N, row0=reserve, scale=1.0 / (N - reserve))
+    out = torch.full((Bn, C), float("nan"), device=DEV)
+    ops.segment_colsum_bcast(buf, ld, Bn, N - reserve, C, out, C, buf[:, 256:], ld, N, seg_stride=N, row0=reserve,
+                             scale=1.0 / (N - reserve))
+    assert torch.equal(out, ref)
+    got = buf[:Bn * N, 256:256 + C].view(Bn, N, C)
+    assert torch.equal(got, ref.bfloat16()[:, None, :].expand(Bn, N, C))
+    assert torch.equal(buf[:, :256], before[:, :256])
+    assert torch.equal(buf[Bn * N:], before[Bn * N:])
+    assert torch.equal(buf[:, 256 + C:], before[:, 256 + C:])
+
+
 def test_segment_colsum_and_router_dx_gate():
     """the Res-ViT router backward helpers against torch: per-image token sums (bf16 and f32 inputs), and
     bf16((dx + [t % N >= reserve] s g[t // N]) * gp) with zero padding and per-row-block column partials of the

@@ -254,3 +254,30 @@ def test_router_head_matches_per_op(bs, reserve, training, mode):
     assert torch.equal(i1, i0)
     assert abs(float(e1) - float(e0)) <= 1e-6 * abs(float(e0)) + 1e-7
     assert rel(d1, d0) < 1e-5
+
+
+def test_cls_distill_matches_per_op():
+    """the fused distillation loss (vitmi.resvit_fused.cls_distill: MSE of the cls rows, its gradient added in place
+    into the student's) against cls_tap + torch's mse_loss: loss to f32 summation order, x's gradient within 1e-6,
+    also when only the loss reaches x"""
+    import torch.nn.functional as F
+    from vitmi import resvit_fused as rf
+    torch.manual_seed(3)
+    B, N, D = 5, 17, 300
+    x0, t, w = (torch.randn(B, N, D, device="cuda") for _ in range(3))
+    for with_out in (True, False):
+        res = []
+        for fused in (False, True):
+            x = x0.clone().requires_grad_(True)
+            if fused:
+                y, loss = rf.cls_distill(x, t)
+            else:
+                y, s = rf.cls_tap(x)
+                loss = F.mse_loss(s, t[:, 0, :])
+            total = 3.0 * loss + ((y * w).sum() if with_out else 0.0)
+            total.backward()
+            res.append((float(loss), x.grad.clone()))
+        (l0, g0), (l1, g1) = res
+        assert abs(l1 - l0) <= 1e-6 * l0
+        assert rel(g1, g0) < 1e-6
+        assert torch.equal(g1[:, 1:], g0[:, 1:])

@@ -733,6 +733,7 @@ struct CastJobDev {
   bf16_t* out;
   long rows, cols, ldi, ldo, rows_pad, cols_pad;
   int blk0, nb;
+  int vec;  // 4-column pieces (float4 in, 8-B out): every width / leading dimension a multiple of 4, aligned rows
 };
 struct CastBatchDev {
   CastJobDev j[VIT_CAST_BATCH_MAX];
@@ -744,6 +745,20 @@ __global__ void __launch_bounds__(256) cast_pad_batch_kernel(const CastBatchDev 
   for (int k = 1; k < VIT_CAST_BATCH_MAX; ++k)
     if (k < bt.n && (int)blockIdx.x >= bt.j[k].blk0) jx = k;
   const CastJobDev& J = bt.j[jx];
+  if (J.vec) {  // (the big operand casts: 32-bit index math, 16 B read and 8 B written per thread and step)
+    const unsigned cq = (unsigned)(J.cols_pad >> 2), tq = (unsigned)(J.rows_pad * cq);
+    for (unsigned q = (blockIdx.x - J.blk0) * 256u + threadIdx.x; q < tq; q += (unsigned)J.nb * 256u) {
+      const unsigned r = q / cq, c = (q - r * cq) << 2;
+      uint2 o = {0u, 0u};
+      if (r < J.rows && c < J.cols) {
+        const float4 v = *reinterpret_cast<const float4*>(J.in + r * J.ldi + c);
+        o.x = pack2bf(v.x, v.y);
+        o.y = pack2bf(v.z, v.w);
+      }
+      *reinterpret_cast<uint2*>(J.out + r * J.ldo + c) = o;
+    }
+    return;
+  }
   const long total = J.rows_pad * J.cols_pad;
   for (long i = (long)(blockIdx.x - J.blk0) * 256 + threadIdx.x; i < total; i += (long)J.nb * 256) {
     const long r = i / J.cols_pad, c = i - r * J.cols_pad;
@@ -762,12 +777,15 @@ extern "C" int vit_cast_pad_batch(const vit_cast_job* jobs, int32_t njobs, vit_s
     VIT_CHECK_ARG(j.in && j.out && j.rows >= 0 && j.cols >= 0 && j.ldi >= j.cols && j.rows_pad >= j.rows &&
                       j.cols_pad >= j.cols && j.ldo >= j.cols_pad,
                   "vit_cast_pad_batch: job %d: bad shape", k);
-    long nb = (j.rows_pad * j.cols_pad + 255) / 256;
+    const int vec = (j.cols | j.cols_pad | j.ldi | j.ldo) % 4 == 0 && (uintptr_t)j.in % 16 == 0 &&
+                    (uintptr_t)j.out % 8 == 0 && j.rows_pad * j.cols_pad / 4 < (1L << 31) ? 1 : 0;
+    long nb = (j.rows_pad * j.cols_pad / (vec ? 4 : 1) + 255) / 256;
     if (nb > 2048) nb = 2048;
     if (nb < 1) nb = 1;
     CastJobDev& d = bt.j[k];
     d.in = j.in; d.out = (bf16_t*)j.out; d.rows = j.rows; d.cols = j.cols; d.ldi = j.ldi; d.ldo = j.ldo;
     d.rows_pad = j.rows_pad; d.cols_pad = j.cols_pad; d.blk0 = (int)blk; d.nb = (int)nb;
+    d.vec = vec;
     blk += nb;
   }
   bt.n = njobs;
@@ -1012,7 +1030,8 @@ namespace {
 template <bool BF16>
 __global__ void __launch_bounds__(256) segment_colsum_kernel(const void* __restrict__ in, long ld, long seg_stride,
                                                              long row0, long seg_rows, int cols, float scale,
-                                                             float* __restrict__ out, long ldo) {
+                                                             float* __restrict__ out, long ldo,
+                                                             bf16_t* __restrict__ bc, long ldbc, long bc_rows) {
   __shared__ float2 red[4][64];
   const int cp = threadIdx.x & 63, lane_r = threadIdx.x >> 6;
   const int c = blockIdx.y * 128 + cp * 2;
@@ -1052,6 +1071,21 @@ __global__ void __launch_bounds__(256) segment_colsum_kernel(const void* __restr
     float* o = out + (long)blockIdx.x * ldo + c;
     o[0] = scale * t.x;
     if (c + 1 < cols) o[1] = scale * t.y;
+    red[0][cp] = float2{scale * t.x, scale * t.y};
+  }
+  if (bc) {  // the segment's result, rounded to bf16, into rows [s * seg_stride, + bc_rows) of bc
+    __syncthreads();
+    if (c < cols) {
+      const float2 v = red[0][cp];
+      const bf16_t b0 = f2bf(v.x), b1 = f2bf(v.y);
+      bf16_t* row = bc + (long)blockIdx.x * seg_stride * ldbc + c;
+      for (long r = lane_r; r < bc_rows; r += 4) {
+        if (c + 1 < cols)
+          *reinterpret_cast<unsigned*>(row + r * ldbc) = (unsigned)b0 | ((unsigned)b1 << 16);
+        else
+          row[r * ldbc] = b0;
+      }
+    }
   }
 }
 
@@ -1191,11 +1225,33 @@ extern "C" int vit_segment_colsum(const void* in, int32_t in_bf16, int64_t ld, i
   const dim3 grid((unsigned)segs, (unsigned)((cols + 127) / 128));
   if (in_bf16)
     hipLaunchKernelGGL(segment_colsum_kernel<true>, grid, dim3(256), 0, (hipStream_t)stream, in, (long)ld,
-                       (long)seg_stride, (long)row0, (long)seg_rows, (int)cols, scale, out, (long)ldo);
+                       (long)seg_stride, (long)row0, (long)seg_rows, (int)cols, scale, out, (long)ldo, nullptr, 0L, 0L);
   else
     hipLaunchKernelGGL(segment_colsum_kernel<false>, grid, dim3(256), 0, (hipStream_t)stream, in, (long)ld,
-                       (long)seg_stride, (long)row0, (long)seg_rows, (int)cols, scale, out, (long)ldo);
+                       (long)seg_stride, (long)row0, (long)seg_rows, (int)cols, scale, out, (long)ldo, nullptr, 0L,
+                       0L);
   VIT_LAUNCH_CHECK("vit_segment_colsum");
+}
+
+extern "C" int vit_segment_colsum_bcast(const void* in, int32_t in_bf16, int64_t ld, int64_t segs, int64_t seg_stride,
+                                        int64_t row0, int64_t seg_rows, int64_t cols, float scale, float* out,
+                                        int64_t ldo, void* bc, int64_t ldbc, int64_t bc_rows, vit_stream_t stream) {
+  VIT_CHECK_ARG(in && out && bc && segs >= 0 && seg_rows >= 0 && row0 >= 0 && seg_stride >= 0 && cols > 0 &&
+                    ld >= cols && ldo >= cols && ldbc >= cols && bc_rows >= 0 && bc_rows <= seg_stride &&
+                    cols < (1L << 30) && ld % 2 == 0 && ldbc % 2 == 0 && ((uintptr_t)bc % 4) == 0 &&
+                    ((uintptr_t)in % (in_bf16 ? 4 : 8)) == 0,
+                "vit_segment_colsum_bcast: bad args (even ld / ldbc, 2-element aligned rows, bc_rows <= seg_stride)");
+  if (segs == 0) return VIT_OK;
+  const dim3 grid((unsigned)segs, (unsigned)((cols + 127) / 128));
+  if (in_bf16)
+    hipLaunchKernelGGL(segment_colsum_kernel<true>, grid, dim3(256), 0, (hipStream_t)stream, in, (long)ld,
+                       (long)seg_stride, (long)row0, (long)seg_rows, (int)cols, scale, out, (long)ldo, (bf16_t*)bc,
+                       (long)ldbc, (long)bc_rows);
+  else
+    hipLaunchKernelGGL(segment_colsum_kernel<false>, grid, dim3(256), 0, (hipStream_t)stream, in, (long)ld,
+                       (long)seg_stride, (long)row0, (long)seg_rows, (int)cols, scale, out, (long)ldo, (bf16_t*)bc,
+                       (long)ldbc, (long)bc_rows);
+  VIT_LAUNCH_CHECK("vit_segment_colsum_bcast");
 }
 
 extern "C" int64_t vit_router_dx_gate_partial_rows(int64_t rows_pad) { return (rows_pad + RDG_RB - 1) / RDG_RB; }
@@ -1423,4 +1479,74 @@ extern "C" int vit_router_head_bwd(const float* soft, const float* ysoft, const 
                      (hipStream_t)stream, soft, ysoft, dsoft, dhard, dind, dent, norm, (long)T, (int)N, (int)bs,
                      (int)reserve, (int)training, dlogits);
   VIT_LAUNCH_CHECK("vit_router_head_bwd");
+}
+
+// ---- Res-ViT distillation loss on the cls rows (res-vit/model.py:40-59, DistillLoss = mse_loss(student[:, 0],
+// teacher[:, 0].detach()), applied after every routed layer) ------------------------------------------------------------
+// forward: e[b][d] = x[b*ldx + d] - t[b*ldt + d] (kept for the backward), per-row sums of e*e, then loss = sum / (B D)
+// in a fixed order; backward: dx[b*lddx + d] += ((2 / (B D)) e) g, torch's mse_loss_backward arithmetic, added in place
+// into the student's incoming gradient (no zero-filled slice gradient, no separate add)
+namespace {
+__global__ void __launch_bounds__(256) cls_mse_rows_kernel(const float* __restrict__ x, long ldx,
+                                                           const float* __restrict__ t, long ldt, int D,
+                                                           float* __restrict__ e, float* __restrict__ part) {
+  __shared__ float red[256];
+  const int b = blockIdx.x;
+  float s = 0.f;
+  for (int d = threadIdx.x; d < D; d += 256) {
+    const float v = x[b * ldx + d] - t[b * ldt + d];
+    e[(long)b * D + d] = v;
+    s += v * v;
+  }
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) part[b] = red[0];
+}
+
+__global__ void __launch_bounds__(256) cls_mse_final_kernel(const float* __restrict__ part, int B, float n,
+                                                            float* __restrict__ loss) {
+  __shared__ float red[256];
+  float s = 0.f;
+  for (int k = threadIdx.x; k < B; k += 256) s += part[k];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) loss[0] = red[0] / n;
+}
+
+__global__ void __launch_bounds__(256) cls_mse_bwd_kernel(float* __restrict__ dx, long lddx,
+                                                          const float* __restrict__ e, int D,
+                                                          const float* __restrict__ g, float norm) {
+  const int b = blockIdx.x;
+  const float gv = g[0];
+  for (int d = threadIdx.x; d < D; d += 256) dx[b * lddx + d] += (norm * e[(long)b * D + d]) * gv;
+}
+}  // namespace
+
+extern "C" int vit_cls_mse(const float* x, int64_t ldx, const float* t, int64_t ldt, int64_t B, int64_t D, float* e,
+                           float* part, float* loss, vit_stream_t stream) {
+  VIT_CHECK_ARG(x && t && e && part && loss && B > 0 && D > 0 && ldx >= D && ldt >= D && B < (1L << 31) &&
+                    D < (1L << 30),
+                "vit_cls_mse: bad args");
+  hipLaunchKernelGGL(cls_mse_rows_kernel, dim3((unsigned)B), dim3(256), 0, (hipStream_t)stream, x, (long)ldx, t,
+                     (long)ldt, (int)D, e, part);
+  hipLaunchKernelGGL(cls_mse_final_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, part, (int)B,
+                     (float)((double)B * (double)D), loss);
+  VIT_LAUNCH_CHECK("vit_cls_mse");
+}
+
+extern "C" int vit_cls_mse_bwd(float* dx, int64_t lddx, const float* e, int64_t B, int64_t D, const float* g,
+                               vit_stream_t stream) {
+  VIT_CHECK_ARG(dx && e && g && B > 0 && D > 0 && lddx >= D && B < (1L << 31) && D < (1L << 30),
+                "vit_cls_mse_bwd: bad args");
+  hipLaunchKernelGGL(cls_mse_bwd_kernel, dim3((unsigned)B), dim3(256), 0, (hipStream_t)stream, dx, (long)lddx, e,
+                     (int)D, g, (float)(2.0 / ((double)B * (double)D)));
+  VIT_LAUNCH_CHECK("vit_cls_mse_bwd");
 }

@@ -361,6 +361,17 @@ def segment_colsum(inp, ld, segs, seg_rows, cols, out, ldo, seg_stride=None, row
                                    _p(out), ldo, _stream()), "vit_segment_colsum")
 
 
+def segment_colsum_bcast(inp, ld, segs, seg_rows, cols, out, ldo, bc, ldbc, bc_rows, seg_stride=None, row0=0,
+                         scale=1.0):
+    """segment_colsum, and each segment's result as bf16 into rows [s*seg_stride, + bc_rows) of bc (bf16, ld ldbc)"""
+    _chk(out, F32, "out")
+    _chk(bc, BF16, "bc")
+    st = seg_rows if seg_stride is None else seg_stride
+    check(lib().vit_segment_colsum_bcast(_p(inp), int(inp.dtype == BF16), ld, segs, st, row0, seg_rows, cols,
+                                         float(scale), _p(out), ldo, _p(bc), ldbc, bc_rows, _stream()),
+          "vit_segment_colsum_bcast")
+
+
 def router_dx_gate_partial_rows(rows_pad):
     return int(lib().vit_router_dx_gate_partial_rows(rows_pad))
 
@@ -410,6 +421,26 @@ def router_head_bwd(soft, ysoft, dsoft, dhard, dind, dent, N, reserve, training,
     check(lib().vit_router_head_bwd(_p(soft), _p(ysoft), _p(dsoft), _p(dhard), _p(dind), _p(dent), float(norm), T, N,
                                     bs, reserve, int(training), _p(dl), _stream()), "vit_router_head_bwd")
     return dl
+
+
+def cls_mse(x, ldx, t, ldt, B, D):
+    """(loss [], e [B][D]) with e = x rows - t rows (row strides ldx / ldt floats) and loss = mean(e^2)
+    (vit_cls_mse)"""
+    _chk(x, F32, "x")
+    _chk(t, F32, "t")
+    e = torch.empty(B, D, device=x.device, dtype=F32)
+    part = torch.empty(B, device=x.device, dtype=F32)
+    loss = torch.empty((), device=x.device, dtype=F32)
+    check(lib().vit_cls_mse(_p(x), ldx, _p(t), ldt, B, D, _p(e), _p(part), _p(loss), _stream()), "vit_cls_mse")
+    return loss, e
+
+
+def cls_mse_bwd(dx, lddx, e, g):
+    """dx rows (stride lddx floats) += (2 / e.numel()) e g (vit_cls_mse_bwd; g a device scalar)"""
+    _chk(dx, F32, "dx")
+    _chk(e, F32, "e")
+    _chk(g, F32, "g")
+    check(lib().vit_cls_mse_bwd(_p(dx), lddx, _p(e), e.shape[0], e.shape[1], _p(g), _stream()), "vit_cls_mse_bwd")
 
 
 def unpack_bf16_f32(inp, ldi, rows, cols, out, ldo):

@@ -421,6 +421,9 @@ CLS_TAP = True
 # the router's softmax / entropy / Gumbel hard routing / pattern index as one fused node (vitmi.resvit_fused.router_head;
 # False: the per-op path as written)
 FUSED_HEAD = True
+# the distillation loss (MSE of the cls rows) as one node whose backward adds into the student's gradient in place
+# (vitmi.resvit_fused.cls_distill; False: cls_tap + DistillLoss)
+FUSED_DISTILL = True
 
 
 def _select_rows(mask, a, b):
@@ -581,11 +584,16 @@ class Transformer(nn.Module):
             if self.use_reslr and layer.layer_id >= layer.dynamic_start_layer:
                 if self.training:
                     teacher_out, student_out, w, block_info = layer(student_x, teacher_x, block_info, self.LRA_mask)
-                    if CLS_TAP and student_out.is_cuda:
-                        student_out, s_cls = _fused.cls_tap(student_out)
+                    if (FUSED_DISTILL and CLS_TAP and student_out.is_cuda and student_out.dtype == torch.float32
+                            and teacher_out.dtype == torch.float32 and type(self.criterion_distill) is DistillLoss):
+                        student_out, dl = _fused.cls_distill(student_out, teacher_out)
+                        d_loss = d_loss + dl
                     else:
-                        s_cls = student_out[:, 0, :]
-                    d_loss = d_loss + self.criterion_distill(s_cls, teacher_out[:, 0, :])
+                        if CLS_TAP and student_out.is_cuda:
+                            student_out, s_cls = _fused.cls_tap(student_out)
+                        else:
+                            s_cls = student_out[:, 0, :]
+                        d_loss = d_loss + self.criterion_distill(s_cls, teacher_out[:, 0, :])
                     if layer.is_block_head:
                         bid = layer.current_block_id
                         r_entropy = r_entropy + block_info[f"block_{bid}_router_entropy"]

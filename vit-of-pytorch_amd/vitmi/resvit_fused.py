@@ -402,6 +402,41 @@ def cls_tap(x):
     return _ClsTap.apply(x)
 
 
+class _ClsDistill(torch.autograd.Function):
+    """(x, mse_loss(x[:, 0, :], t[:, 0, :])) for the distillation loss after a routed layer (res-vit/model.py:40-59,
+    t the detached teacher output): forward one row-sum launch plus a fixed-order total (vit_cls_mse, which keeps
+    e = x_cls - t_cls), backward ((2 / (B D)) e) g added in place into x's incoming gradient's cls rows
+    (vit_cls_mse_bwd). Replaces the cls-row copy, the MSE forward (difference, square, mean) and its backward, and
+    the slice gradient's add"""
+
+    @staticmethod
+    def forward(ctx, x, t):
+        ctx.set_materialize_grads(False)
+        B, N, D = x.shape
+        xc, tc = x.detach().contiguous(), t.detach().contiguous()
+        loss, e = ops.cls_mse(xc, N * D, tc, tc.shape[1] * tc.shape[2], B, D)
+        ctx.save_for_backward(e)
+        ctx.shape = x.shape
+        return x.view(x.shape), loss
+
+    @staticmethod
+    def backward(ctx, dx, dloss):
+        (e,) = ctx.saved_tensors
+        B, N, D = ctx.shape
+        if dloss is None:
+            return dx, None
+        if dx is None:
+            dx = torch.zeros(ctx.shape, device=e.device, dtype=F32)
+        dx = dx.contiguous()
+        ops.cls_mse_bwd(dx, N * D, e, dloss.detach().float().contiguous())
+        return dx, None
+
+
+def cls_distill(x, t):
+    """x and mse_loss(x[:, 0, :], t[:, 0, :].detach()) as one node (_ClsDistill)"""
+    return _ClsDistill.apply(x, t)
+
+
 class _RouterHead(torch.autograd.Function):
     """RouterModule.forward after out_conv (res-vit/model.py:191-211) as one node: softmax, the entropy, the Gumbel
     hard decision with its straight-through value, the reserved tokens' rows and the pattern index in one launch (plus
@@ -458,9 +493,9 @@ def teacher_and_student(block, x, active):
 class _ApproxStep(torch.autograd.Function):
     """x_new = where(sel, x + up(down(x)), x) for one approximator of BlockPathApproximators (training path),
     as one node: x [T][D] f32, down_proj.weight Wd [r][D], up_proj.weight Wu [D][r] (nn.Linear layouts), sel
-    [T] bool. Forward: h = bf16(x) Wd^T written as bf16 by the GEMM epilogue, its unselected rows zeroed, then
-    x + h Wu^T by the bias + f32-residual epilogue — an unselected row gets x + 0 = x, so neither the per-op
-    path's f32 add nor its `where` pass remains. Backward: dh = (dout Wu) masked to the selected rows, dx =
+    [T] bool. Forward: h = bf16(x) Wd^T written as bf16 by the GEMM epilogue, its unselected rows zeroed
+    (vit_rows_select), then x + h Wu^T by the bias + f32-residual epilogue — an unselected row gets x + 0 = x,
+    so neither the per-op path's f32 add nor its `where` pass remains. Backward: dh = (dout Wu) masked to the selected rows, dx =
     dout + dh Wd (residual epilogue), dWu = dout^T h, dWd = dh^T bf16(x) (split-K over tokens). Same
     operands and roundings as the per-op path (vitmi.functional.HipLinear + add + where), so the results
     agree bit for bit (tests/test_resvit_train_gpu.py)."""
@@ -480,19 +515,19 @@ class _ApproxStep(torch.autograd.Function):
         hb = _alloc_pad(rp, rk, T, r, dev)
         ops.gemm(xb, wdb, hb, T, r, kp, a_layout=K_CONTIG, b_layout=K_CONTIG, lda=kp, ldb=kp, ldc=rk,
                  epilogue=EPI_BF16)
-        selb = sel.reshape(T, 1).to(BF16)
-        hb[:T].mul_(selb)  # unselected rows: h = 0 (exact)
+        selm = sel.reshape(T).to(torch.bool).contiguous()
+        ops.rows_select(hb[:T], selm)  # unselected rows: h = 0 (only their bytes written)
         out = torch.empty(T, D, device=dev, dtype=F32)
         ops.gemm(hb, wub, out, T, D, rk, a_layout=K_CONTIG, b_layout=K_CONTIG, lda=rk, ldb=rk, ldc=D,
                  epilogue=EPI_BIAS_RESID_F32, bias=_zero_row(D, dev), aux=x2, ldaux=D)
-        ctx.save_for_backward(xb, hb, wdb, wub, selb)
+        ctx.save_for_backward(xb, hb, wdb, wub, selm)
         ctx.params = (wd, wu)
         ctx.dims = (B, N, D, T, r)
         return out.view(B, N, D)
 
     @staticmethod
     def backward(ctx, dout):
-        xb, hb, wdb, wub, selb = ctx.saved_tensors
+        xb, hb, wdb, wub, selm = ctx.saved_tensors
         B, N, D, T, r = ctx.dims
         kp, rp, rk = xb.shape[1], xb.shape[0], hb.shape[1]
         dev = dout.device
@@ -503,7 +538,7 @@ class _ApproxStep(torch.autograd.Function):
         dhb = _alloc_pad(rp, rk, T, r, dev)
         ops.gemm(db, wub, dhb, T, r, kp, a_layout=K_CONTIG, b_layout=MN_CONTIG, lda=kp, ldb=rk, ldc=rk,
                  epilogue=EPI_BF16)
-        dhb[:T].mul_(selb)
+        ops.rows_select(dhb[:T], selm)
         dx = None
         if ctx.needs_input_grad[0]:
             # dx = dout + dh Wd: B(kk = j, n' = k) = Wd[j][k], M/N-contiguous (the forward's padded [rk][kp] copy)
@@ -802,10 +837,10 @@ class _RouterNet(torch.autograd.Function):
         if T:
             ops.gemm(lnb, w0b, gp0, T, Hh, dp, a_layout=K_CONTIG, b_layout=K_CONTIG, lda=dp, ldb=dp, ldc=h0p,
                      epilogue=EPI_BIAS_GELU_DGELU, bias=b0.detach().float().contiguous(), C2=xcat, ldc2=kp)
-        xc = xcat[:T].view(B, N, kp)
         glob = torch.empty(B, Hh, device=dev, dtype=F32)  # [B][h]: mean of the bf16 x_embed values, reserved tokens out
-        ops.segment_colsum(xcat, kp, B, N - reserve, Hh, glob, Hh, seg_stride=N, row0=reserve, scale=1.0 / (N - reserve))
-        xc[:, :, Hh:K1].copy_(glob.to(BF16)[:, None, :])
+        # the mean, and its bf16 broadcast into every token's global half, in one launch
+        ops.segment_colsum_bcast(xcat, kp, B, N - reserve, Hh, glob, Hh, xcat[:, Hh:], kp, N, seg_stride=N,
+                                 row0=reserve, scale=1.0 / (N - reserve))
         out, acts, ws = _mlp_forward(xcat, T, kp, w1, b1, w2, b2, w3, b3, ws=ws)
         ctx.save_for_backward(x2, mean, rstd, ln_w, lnb, gp0, xcat, *acts, w0b, *ws, w1)
         ctx.params = (w0, b0, w1, b1, w2, b2, w3, b3)
