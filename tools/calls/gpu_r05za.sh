@@ -1,5 +1,5 @@
 #!/bin/bash
-# round 5, call 28: kernel trace of the current Res-ViT-B/16 bs 128 step (what is left of the ATen glue)
+# round 5, call 28 (and 31): kernel trace of the current Res-ViT-B/16 bs 128 step (what is left of the ATen glue)
 set -o pipefail
 export TMPDIR=/tmp
 O=gpurun_out/r05za; mkdir -p $O
