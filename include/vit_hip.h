@@ -419,6 +419,12 @@ int vit_router_head_fwd(const float* logits, const float* noise, int32_t noise_m
 int vit_router_head_bwd(const float* soft, const float* ysoft, const float* dsoft, const float* dhard, const float* dind,
                         const float* dent, float norm, int64_t T, int64_t N, int32_t bs, int64_t reserve,
                         int32_t training, float* dlogits, vit_stream_t stream);
+/* Res-ViT routing masks from the pattern index (res-vit/model.py:486-512, 336-368), one workgroup:
+ * active[j*T + t] = (long)indices[t] in block position j's transformer set (bit v of active_masks[j], v < 32),
+ * sel[k*T + t] = (indices[t] == k) for approximator keys k < nkeys, any[k] = any token with sel; bytes 0 / 1
+ * (torch.bool storage). npos <= 8, nkeys <= 32. */
+int vit_router_select(const float* indices, int64_t T, int32_t npos, const uint32_t* active_masks, int32_t nkeys,
+                      void* active, void* sel, void* any, vit_stream_t stream);
 /* Res-ViT distillation loss on the cls rows (res-vit/model.py:40-59: mse_loss(student[:, 0], teacher[:, 0])):
  * vit_cls_mse: e[b][d] = x[b*ldx + d] - t[b*ldt + d], loss[0] = (sum of e^2, per-row partials part[B] then a fixed
  *   order) / (B D); vit_cls_mse_bwd: dx[b*lddx + d] += ((2 / (B D)) e[b][d]) g[0] (device scalar g). */

@@ -281,3 +281,30 @@ def test_cls_distill_matches_per_op():
         assert abs(l1 - l0) <= 1e-6 * l0
         assert rel(g1, g0) < 1e-6
         assert torch.equal(g1[:, 1:], g0[:, 1:])
+
+
+@pytest.mark.parametrize("bs", [1, 2, 4])
+def test_router_select_matches_torch(bs):
+    """vitmi.ops.router_select (one launch per routed block) against the per-layer torch ops it replaces:
+    isin(indices.long(), the position's transformer set), indices == key and its any(), on pattern indices that
+    include values just below an integer (the straight-through sum (1 - y) + y can land there: .long() truncates,
+    == does not match)"""
+    from vitmi import ops, resvit
+    torch.manual_seed(7)
+    T = 3 * 197
+    n = 2 ** bs
+    idx = torch.randint(0, n, (T,), device="cuda").float()
+    idx[::7] -= 6e-8  # 0.99999994-style values (and -6e-8 for 0)
+    idx[5] = float(n - 1)
+    lra = resvit.get_indices_from_LRA_mask(bs)
+    act, sel, anyf = ops.router_select(idx, [lra[j][1] for j in range(bs)], n - 1)
+    for j in range(bs):
+        ref = torch.isin(idx.long(), torch.tensor(lra[j][1], device="cuda"))
+        assert torch.equal(act[j], ref), j
+    for k in range(n - 1):
+        assert torch.equal(sel[k], idx == k), k
+        assert bool(anyf[k]) == bool((idx == k).any()), k
+    # a key no token takes
+    idx2 = torch.zeros(T, device="cuda")
+    _, sel2, any2 = ops.router_select(idx2, [], n - 1)
+    assert bool(any2[0]) and not any(bool(any2[k]) for k in range(1, n - 1))

@@ -1550,3 +1550,49 @@ extern "C" int vit_cls_mse_bwd(float* dx, int64_t lddx, const float* e, int64_t 
                      (int)D, g, (float)(2.0 / ((double)B * (double)D)));
   VIT_LAUNCH_CHECK("vit_cls_mse_bwd");
 }
+
+// ---- Res-ViT routing masks (res-vit/model.py:486-512, 336-368): from the pattern index of every token, which tokens run
+// each block position's full layer (isin(index.long(), that position's transformer set)) and which tokens each
+// approximator takes (index == key, exact float compare as the reference's), plus whether any token took it. One
+// workgroup (T is one batch of tokens); replaces the cast / compare / reduce launches per routed layer and per
+// approximator --------------------------------------------------------------------------------------------------------
+namespace {
+constexpr int RS_POS_MAX = 8, RS_KEYS_MAX = 32;
+struct RouterSelectArgs {
+  unsigned mask[RS_POS_MAX];
+};
+__global__ void __launch_bounds__(1024) router_select_kernel(const float* __restrict__ idx, long T, int npos,
+                                                             const RouterSelectArgs a, int nkeys,
+                                                             unsigned char* __restrict__ active,
+                                                             unsigned char* __restrict__ sel,
+                                                             unsigned char* __restrict__ any) {
+  __shared__ int anyf[RS_KEYS_MAX];
+  if ((int)threadIdx.x < RS_KEYS_MAX) anyf[threadIdx.x] = 0;
+  __syncthreads();
+  for (long t = threadIdx.x; t < T; t += 1024) {
+    const float v = idx[t];
+    const long lv = (long)v;  // torch's .long(): truncation toward zero
+    for (int j = 0; j < npos; ++j)
+      active[j * T + t] = (lv >= 0 && lv < 32 && ((a.mask[j] >> lv) & 1u)) ? 1 : 0;
+    for (int k = 0; k < nkeys; ++k) {
+      const bool s = v == (float)k;
+      sel[k * T + t] = s ? 1 : 0;
+      if (s) anyf[k] = 1;  // (every writer stores the same 1)
+    }
+  }
+  __syncthreads();
+  if ((int)threadIdx.x < nkeys) any[threadIdx.x] = anyf[threadIdx.x] ? 1 : 0;
+}
+}  // namespace
+
+extern "C" int vit_router_select(const float* indices, int64_t T, int32_t npos, const uint32_t* active_masks,
+                                 int32_t nkeys, void* active, void* sel, void* any, vit_stream_t stream) {
+  VIT_CHECK_ARG(indices && T >= 0 && T < (1L << 40) && npos >= 0 && npos <= RS_POS_MAX && nkeys >= 0 &&
+                    nkeys <= RS_KEYS_MAX && (npos == 0 || (active && active_masks)) && (nkeys == 0 || (sel && any)),
+                "vit_router_select: bad args (npos <= %d, nkeys <= %d)", RS_POS_MAX, RS_KEYS_MAX);
+  RouterSelectArgs a{};
+  for (int j = 0; j < npos; ++j) a.mask[j] = active_masks[j];
+  hipLaunchKernelGGL(router_select_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, indices, (long)T, (int)npos, a,
+                     (int)nkeys, (unsigned char*)active, (unsigned char*)sel, (unsigned char*)any);
+  VIT_LAUNCH_CHECK("vit_router_select");
+}

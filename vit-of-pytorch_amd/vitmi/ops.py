@@ -443,6 +443,31 @@ def cls_mse_bwd(dx, lddx, e, g):
     check(lib().vit_cls_mse_bwd(_p(dx), lddx, _p(e), e.shape[0], e.shape[1], _p(g), _stream()), "vit_cls_mse_bwd")
 
 
+def router_select(indices, active_sets, nkeys):
+    """(active bool [npos][T], sel bool [nkeys][T], any bool [nkeys]) from the pattern index f32 [T]
+    (vit_router_select): active[j] = isin(indices.long(), active_sets[j]) (values < 32), sel[k] = indices == k,
+    any[k] = sel[k].any()"""
+    _chk(indices, F32, "indices")
+    if not indices.is_contiguous():
+        raise ValueError("router_select: indices must be contiguous")
+    T, dev = indices.numel(), indices.device
+    masks = []
+    for st in active_sets:
+        m = 0
+        for v in st:
+            if not 0 <= int(v) < 32:
+                raise ValueError(f"router_select: index value {v} outside [0, 32)")
+            m |= 1 << int(v)
+        masks.append(m)
+    active = torch.empty(len(masks), T, device=dev, dtype=torch.bool)
+    sel = torch.empty(nkeys, T, device=dev, dtype=torch.bool)
+    anyf = torch.empty(nkeys, device=dev, dtype=torch.bool)
+    arr = (ctypes.c_uint32 * max(len(masks), 1))(*masks)
+    check(lib().vit_router_select(_p(indices), T, len(masks), arr, nkeys, _p(active), _p(sel), _p(anyf), _stream()),
+          "vit_router_select")
+    return active, sel, anyf
+
+
 def unpack_bf16_f32(inp, ldi, rows, cols, out, ldo):
     """out[r*ldo + c] = f32(inp[r*ldi + c])"""
     _chk(inp, BF16, "inp")

@@ -32,6 +32,7 @@ import torch.nn.functional as F
 
 from . import flat as _flat
 from . import functional as HF
+from . import ops as _ops
 from . import resvit_fused as _fused
 from .model import GELU, CrossEntropyLoss, LayerNorm as _HipLayerNorm, Linear
 
@@ -379,7 +380,8 @@ class BlockPathApproximators(nn.Module):
             if key != total - 1:
                 self.approximators[str(key)] = LowRankApproximator(dim, rank)
 
-    def forward(self, x, router_indices, LRA_mask):
+    def forward(self, x, router_indices, LRA_mask, sel=None):
+        """sel: (active, sel [nkeys][T], any [nkeys]) of vitmi.ops.router_select for router_indices, or None"""
         idx = router_indices.squeeze(-1)
         keys = [int(k) for k in (LRA_mask.tolist() if torch.is_tensor(LRA_mask) else LRA_mask)]
         if torch.is_grad_enabled():
@@ -390,13 +392,17 @@ class BlockPathApproximators(nn.Module):
             for key in keys:
                 if str(key) not in self.approximators:
                     continue
-                sel = (idx == key).unsqueeze(-1)
+                if sel is not None and key < sel[1].shape[0]:
+                    sk, anyk = sel[1][key].view(*idx.shape, 1), sel[2][key]
+                else:
+                    sk = (idx == key).unsqueeze(-1)
+                    anyk = sk.any()
                 m = self.approximators[str(key)]
                 if self.fused and _fused.approx_supported(m, x):
-                    x = _fused.approx_step(m, x, sel)  # same values, no f32 add / where passes
+                    x = _fused.approx_step(m, x, sk)  # same values, no f32 add / where passes
                 else:
-                    x = torch.where(sel, HF.add(m(x), x), x)
-                _flat.gate(m.parameters(), sel.any())
+                    x = torch.where(sk, HF.add(m(x), x), x)
+                _flat.gate(m.parameters(), anyk)
             return x
         for key in keys:
             if str(key) not in self.approximators:
@@ -424,6 +430,9 @@ FUSED_HEAD = True
 # the distillation loss (MSE of the cls rows) as one node whose backward adds into the student's gradient in place
 # (vitmi.resvit_fused.cls_distill; False: cls_tap + DistillLoss)
 FUSED_DISTILL = True
+# a routed block's per-position active masks and per-approximator selections (and their any-flags) from the pattern
+# index in one launch (vitmi.ops.router_select; False: isin / == / any per layer and approximator)
+FUSED_SELECT = True
 
 
 def _select_rows(mask, a, b):
@@ -487,21 +496,30 @@ class TransformerBlock(nn.Module):
                           f"block_{bid}_router_indices": router_indices,
                           f"block_{bid}_router_entropy": router_entropy,
                           f"block_{bid}_soft_routing": soft_routing[:, :, :, 1]}
+            if (FUSED_SELECT and LRA_mask is not None and router_indices.is_cuda
+                    and router_indices.dtype == torch.float32 and self.block_size <= 5):
+                block_info[f"block_{bid}_select"] = _ops.router_select(
+                    router_indices.reshape(-1).contiguous(), [LRA_mask[j][1] for j in range(self.block_size)],
+                    2 ** self.block_size - 1)
         approximators = block_info[f"block_{bid}_approximators"]
         block_routing = block_info[f"block_{bid}_routing"]
         router_indices = block_info[f"block_{bid}_router_indices"]
         w = block_routing[:, :, self.current_block_pos:self.current_block_pos + 1]
         assert LRA_mask is not None, "LRA_mask must be provided"
         lra_lora = list(LRA_mask[self.current_block_pos][0])
-        active = torch.isin(router_indices.long(), _const(tuple(LRA_mask[self.current_block_pos][1]), x.device,
-                                                          torch.int64))
+        sel_info = block_info.get(f"block_{bid}_select")
+        if sel_info is not None:
+            active = sel_info[0][self.current_block_pos].view(bsz, seqlen, 1)
+        else:
+            active = torch.isin(router_indices.long(), _const(tuple(LRA_mask[self.current_block_pos][1]), x.device,
+                                                              torch.int64))
 
         if self.training:
             if (SHARE_TEACHER and (teacher_x is None or teacher_x is x) and self.fused and x.dim() == 3 and x.is_cuda
                     and _fused.supported(self)):
                 # the teacher's input is the student's (the first routed layer): one layer forward serves both
                 teacher_out, student_out = _fused.teacher_and_student(self, x, active)
-                return teacher_out, approximators(student_out, router_indices, lra_lora), w, block_info
+                return teacher_out, approximators(student_out, router_indices, lra_lora, sel_info), w, block_info
             # teacher: every token, every layer. Its outputs reach the loss only through DistillLoss's
             # .detach() (res-vit/model.py:40-59), so no gradient flows through it: run without autograd
             with torch.no_grad():
@@ -511,7 +529,7 @@ class TransformerBlock(nn.Module):
                 student_out = self._full(x, packed=True, active=active)
             else:  # A/B (bench.py VITMI_RESVIT_WHERE_OPS=1): the layer node, then torch.where
                 student_out = _select_rows(active, self._full(x, packed=True), x)
-            return teacher_out, approximators(student_out, router_indices, lra_lora), w, block_info
+            return teacher_out, approximators(student_out, router_indices, lra_lora, sel_info), w, block_info
 
         # inference: only the active tokens query (ragged), every token is a key / value
         x_normed = self.attention_norm(x)
