@@ -633,3 +633,33 @@ def test_graphed_step_construction_leaves_state_untouched(gold):
     assert torch.equal(opt.flat.data, p0)
     assert opt.param_groups[0]["lr"] == lr0
     assert float(opt.flat.grad.abs().sum()) == 0.0
+
+
+def test_router_through_matches_autograd_add(gold, monkeypatch):
+    """RouterModule.forward_through: the routed block's input handed to the layer through the fused router node, so
+    the layer's input gradient is added inside the router's LayerNorm backward instead of by autograd — one reference
+    step's losses equal and every trainable gradient within 1e-5 (one f32 add of the same two values, inside or after
+    the LayerNorm backward's own arithmetic)"""
+    from vitmi import resvit
+    from vitmi.resvit_train import total_loss
+    h = hp(gold)
+    runs = []
+    for through in (False, True):
+        monkeypatch.setattr(resvit, "ROUTER_THROUGH", through)
+        m = build(gold).train()
+        for j, r in enumerate(l.router for l in m.layers if hasattr(l, "router")):
+            hh = torch.from_numpy(gold[f"s0/router{j}_hard"]).cuda()
+            gg = torch.from_numpy(gold[f"s0/gumbel{j}"]).cuda()
+            r.hard_override = lambda logits, hh=hh: hh
+            r.gumbel_noise = lambda logits, gg=gg: gg
+        x = torch.from_numpy(gold["s0/x"]).cuda()
+        y = torch.from_numpy(gold["s0/y"]).cuda()
+        c, a, d, ent, _ = m(x, y)
+        total = total_loss(m, c, a, d, h["la"], h["ld"], h["lc"])
+        total.backward()
+        runs.append((float(total), {n: p.grad.clone() for n, p in m.named_parameters() if p.grad is not None}))
+    (t0, g0), (t1, g1) = runs
+    assert t0 == t1
+    assert g0.keys() == g1.keys() and len(g0) > 0
+    for k in g0:
+        assert rel(g1[k], g0[k]) < 1e-5, (k, rel(g1[k], g0[k]))

@@ -229,6 +229,16 @@ class RouterModule(nn.Module):
         w = _const((tuple(2.0 ** (n - 1 - i) for i in range(n)),), keep.device, torch.float32).view(n, 1)
         return torch.matmul(keep.float(), w)
 
+    def forward_through(self, x):
+        """(x', forward(x)) where x' is x passed through the fused router node: feeding x' to the block's layer
+        routes the layer's input gradient through the router's LayerNorm backward, which adds it (no separate
+        autograd add of the two input gradients). Plain (x, forward(x)) where the fused router does not apply."""
+        B, N, _ = x.shape
+        if not (self.fused_mlp and _fused.router_net_supported(self, x)):
+            return x, self.forward(x)
+        logits, xt = _fused.router_net(self, x, through=True)
+        return xt, self.head(logits.view(B, N, self.block_size, 2))
+
     def forward(self, x):
         B, N, _ = x.shape
         r = self.reserve_initials
@@ -433,6 +443,9 @@ FUSED_DISTILL = True
 # a routed block's per-position active masks and per-approximator selections (and their any-flags) from the pattern
 # index in one launch (vitmi.ops.router_select; False: isin / == / any per layer and approximator)
 FUSED_SELECT = True
+# a routed block's input handed to its layer through the fused router node (RouterModule.forward_through), so the
+# router's LayerNorm backward adds the layer's input gradient (False: autograd adds the two)
+ROUTER_THROUGH = True
 
 
 def _select_rows(mask, a, b):
@@ -489,8 +502,12 @@ class TransformerBlock(nn.Module):
             return (out, out, w, block_info) if self.training else (out, w, block_info)
 
         bid = self.current_block_id
+        x_in = x  # (the caller's tensor: teacher_x is compared against it below)
         if self.is_block_head:
-            routing, router_indices, router_entropy, soft_routing = self.router(x)
+            if ROUTER_THROUGH and self.training and torch.is_grad_enabled():
+                x, (routing, router_indices, router_entropy, soft_routing) = self.router.forward_through(x)
+            else:
+                routing, router_indices, router_entropy, soft_routing = self.router(x)
             block_info = {f"block_{bid}_approximators": self.block_path_approximators,
                           f"block_{bid}_routing": routing[:, :, :, 1],
                           f"block_{bid}_router_indices": router_indices,
@@ -515,7 +532,7 @@ class TransformerBlock(nn.Module):
                                                               torch.int64))
 
         if self.training:
-            if (SHARE_TEACHER and (teacher_x is None or teacher_x is x) and self.fused and x.dim() == 3 and x.is_cuda
+            if (SHARE_TEACHER and (teacher_x is None or teacher_x is x_in) and self.fused and x.dim() == 3 and x.is_cuda
                     and _fused.supported(self)):
                 # the teacher's input is the student's (the first routed layer): one layer forward serves both
                 teacher_out, student_out = _fused.teacher_and_student(self, x, active)
