@@ -425,6 +425,11 @@ int vit_router_head_bwd(const float* soft, const float* ysoft, const float* dsof
  * (torch.bool storage). npos <= 8, nkeys <= 32. */
 int vit_router_select(const float* indices, int64_t T, int32_t npos, const uint32_t* active_masks, int32_t nkeys,
                       void* active, void* sel, void* any, vit_stream_t stream);
+/* out[r*ldo + c] (bf16) = in[r*ldi + c] for rows whose mask byte is non-zero (every row when mask is NULL), zeros for
+ * the other rows (not read): a routed layer's output gradient as the bf16 operand of its backward, on the active rows
+ * only (res-vit/model.py:507-512). cols, ldi, ldo multiples of 4. */
+int vit_cast_rows_masked(const float* in, int64_t ldi, int64_t rows, int64_t cols, const void* mask, void* out,
+                         int64_t ldo, vit_stream_t stream);
 /* Res-ViT distillation loss on the cls rows (res-vit/model.py:40-59: mse_loss(student[:, 0], teacher[:, 0])):
  * vit_cls_mse: e[b][d] = x[b*ldx + d] - t[b*ldt + d], loss[0] = (sum of e^2, per-row partials part[B] then a fixed
  *   order) / (B D); vit_cls_mse_bwd: dx[b*lddx + d] += ((2 / (B D)) e[b][d]) g[0] (device scalar g). */

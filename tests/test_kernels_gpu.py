@@ -231,6 +231,22 @@ def test_cast_pad_batch_matches_single_casts():
     assert (outs[2][:, :100].float() == 0).all() and torch.isnan(outs[2][:, 100:].float()).all()
 
 
+def test_cast_rows_masked():
+    """vit_cast_rows_masked: the bf16 rounding of the masked rows, zeros for the others (bit-identical to a cast then
+    vit_rows_select), the padding columns of the output untouched; no mask: every row"""
+    g = torch.Generator(device="cpu").manual_seed(8)
+    rows, cols, ldi, ldo = 301, 96, 100, 104
+    x = torch.randn(rows, ldi, generator=g).to(DEV)
+    mask = (torch.rand(rows, generator=g) < 0.6).to(DEV)
+    out = torch.full((rows, ldo), float("nan"), device=DEV).bfloat16()
+    ops.cast_rows_masked(x, ldi, rows, cols, mask, out, ldo)
+    ref = torch.where(mask[:, None], x[:, :cols], torch.zeros_like(x[:, :cols])).bfloat16()
+    assert torch.equal(out[:, :cols], ref)
+    assert torch.isnan(out[:, cols:].float()).all()
+    ops.cast_rows_masked(x, ldi, rows, cols, None, out, ldo)
+    assert torch.equal(out[:, :cols], x[:, :cols].bfloat16())
+
+
 @pytest.mark.parametrize("C", [200, 199])
 def test_segment_colsum_bcast(C):
     """vit_segment_colsum_bcast (the router forward's token mean, broadcast as bf16 into the global half of out_conv's

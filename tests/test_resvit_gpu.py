@@ -283,15 +283,15 @@ def test_cls_distill_matches_per_op():
         assert torch.equal(g1[:, 1:], g0[:, 1:])
 
 
+@pytest.mark.parametrize("T", [3 * 197, 4 * 197])
 @pytest.mark.parametrize("bs", [1, 2, 4])
-def test_router_select_matches_torch(bs):
+def test_router_select_matches_torch(bs, T):
     """vitmi.ops.router_select (one launch per routed block) against the per-layer torch ops it replaces:
     isin(indices.long(), the position's transformer set), indices == key and its any(), on pattern indices that
     include values just below an integer (the straight-through sum (1 - y) + y can land there: .long() truncates,
     == does not match)"""
     from vitmi import ops, resvit
     torch.manual_seed(7)
-    T = 3 * 197
     n = 2 ** bs
     idx = torch.randint(0, n, (T,), device="cuda").float()
     idx[::7] -= 6e-8  # 0.99999994-style values (and -6e-8 for 0)

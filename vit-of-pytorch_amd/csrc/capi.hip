@@ -23,5 +23,5 @@ int check_hip(hipError_t e, const char* what) {
 }  // namespace vit
 
 extern "C" const char* vit_last_error(void) { return vit::g_last_error; }
-extern "C" int vit_abi_version(void) { return 17; }
+extern "C" int vit_abi_version(void) { return 18; }
 extern "C" const char* vit_build_id(void) { return VIT_BUILD_ID; }

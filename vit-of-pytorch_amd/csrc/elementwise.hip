@@ -1569,15 +1569,37 @@ __global__ void __launch_bounds__(1024) router_select_kernel(const float* __rest
   __shared__ int anyf[RS_KEYS_MAX];
   if ((int)threadIdx.x < RS_KEYS_MAX) anyf[threadIdx.x] = 0;
   __syncthreads();
-  for (long t = threadIdx.x; t < T; t += 1024) {
-    const float v = idx[t];
-    const long lv = (long)v;  // torch's .long(): truncation toward zero
-    for (int j = 0; j < npos; ++j)
-      active[j * T + t] = (lv >= 0 && lv < 32 && ((a.mask[j] >> lv) & 1u)) ? 1 : 0;
+  // four tokens per thread and step (one 16-B load, one 4-B store per output row; T % 4 == 0 and 16-B aligned
+  // indices, else one token at a time): the loop is latency-bound in a single workgroup
+  const bool vec = T % 4 == 0 && ((uintptr_t)idx % 16) == 0 && ((uintptr_t)active % 4) == 0 &&
+                   ((uintptr_t)sel % 4) == 0;
+  const long step = vec ? 4 : 1;
+  for (long t = (long)threadIdx.x * step; t < T; t += 1024 * step) {
+    float v[4];
+    int n = 1;
+    if (vec) {
+      const float4 q = *reinterpret_cast<const float4*>(idx + t);
+      v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
+      n = 4;
+    } else {
+      v[0] = idx[t];
+    }
+    for (int j = 0; j < npos; ++j) {
+      unsigned w = 0;
+      for (int e = 0; e < n; ++e) {
+        const long lv = (long)v[e];  // torch's .long(): truncation toward zero
+        if (lv >= 0 && lv < 32 && ((a.mask[j] >> lv) & 1u)) w |= 1u << (8 * e);
+      }
+      if (vec) *reinterpret_cast<unsigned*>(active + j * T + t) = w;
+      else active[j * T + t] = (unsigned char)w;
+    }
     for (int k = 0; k < nkeys; ++k) {
-      const bool s = v == (float)k;
-      sel[k * T + t] = s ? 1 : 0;
-      if (s) anyf[k] = 1;  // (every writer stores the same 1)
+      unsigned w = 0;
+      for (int e = 0; e < n; ++e)
+        if (v[e] == (float)k) w |= 1u << (8 * e);
+      if (vec) *reinterpret_cast<unsigned*>(sel + k * T + t) = w;
+      else sel[k * T + t] = (unsigned char)w;
+      if (w) anyf[k] = 1;  // (every writer stores the same 1)
     }
   }
   __syncthreads();
@@ -1595,4 +1617,39 @@ extern "C" int vit_router_select(const float* indices, int64_t T, int32_t npos, 
   hipLaunchKernelGGL(router_select_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, indices, (long)T, (int)npos, a,
                      (int)nkeys, (unsigned char*)active, (unsigned char*)sel, (unsigned char*)any);
   VIT_LAUNCH_CHECK("vit_router_select");
+}
+
+// ---- f32 rows -> bf16 rows, rows whose mask byte is 0 written as zeros without reading them (Res-ViT's routed layer:
+// its output gradient enters the layer's backward as the bf16 operand of the fc2 data gradient on the active rows
+// only, res-vit/model.py:507-512) --------------------------------------------------------------------------------------
+namespace {
+__global__ void __launch_bounds__(256) cast_rows_masked_kernel(const float* __restrict__ in, long ldi, long rows,
+                                                               int cols, const unsigned char* __restrict__ mask,
+                                                               bf16_t* __restrict__ out, long ldo) {
+  const int cq = cols >> 2;
+  const long total = rows * cq;
+  for (long q = (long)blockIdx.x * 256 + threadIdx.x; q < total; q += (long)gridDim.x * 256) {
+    const long r = q / cq;
+    const int c = (int)(q - r * cq) << 2;
+    uint2 o = {0u, 0u};
+    if (!mask || mask[r]) {
+      const float4 v = *reinterpret_cast<const float4*>(in + r * ldi + c);
+      o.x = pack2bf(v.x, v.y);
+      o.y = pack2bf(v.z, v.w);
+    }
+    *reinterpret_cast<uint2*>(out + r * ldo + c) = o;
+  }
+}
+}  // namespace
+
+extern "C" int vit_cast_rows_masked(const float* in, int64_t ldi, int64_t rows, int64_t cols, const void* mask,
+                                    void* out, int64_t ldo, vit_stream_t stream) {
+  VIT_CHECK_ARG(in && out && rows >= 0 && cols > 0 && cols % 4 == 0 && ldi % 4 == 0 && ldo % 4 == 0 && ldi >= cols &&
+                    ldo >= cols && (uintptr_t)in % 16 == 0 && (uintptr_t)out % 8 == 0 && cols < (1L << 30),
+                "vit_cast_rows_masked: bad args (cols, ldi, ldo multiples of 4; 16-B aligned in, 8-B aligned out)");
+  if (rows == 0) return VIT_OK;
+  hipLaunchKernelGGL(cast_rows_masked_kernel, dim3(grid_for(rows * (cols / 4), 4)), dim3(256), 0,
+                     (hipStream_t)stream, in, (long)ldi, (long)rows, (int)cols, (const unsigned char*)mask,
+                     (bf16_t*)out, (long)ldo);
+  VIT_LAUNCH_CHECK("vit_cast_rows_masked");
 }

@@ -17,7 +17,7 @@ c_i32 = ctypes.c_int32
 c_f32 = ctypes.c_float
 c_vp = ctypes.c_void_p
 
-ABI_VERSION = 17  # vit_abi_version() of the library these prototypes describe
+ABI_VERSION = 18  # vit_abi_version() of the library these prototypes describe
 
 # enum vit_layout / vit_epilogue (include/vit_hip.h)
 K_CONTIG, MN_CONTIG = 0, 1
@@ -91,6 +91,7 @@ _SIGS = {
     "vit_splitk_reduce_group": (c_i32, [ctypes.POINTER(SplitkJob), c_i32, c_vp]),
     "vit_cast_pad_batch": (c_i32, [ctypes.POINTER(CastJob), c_i32, c_vp]),
     "vit_router_head_partials": (c_i64, [c_i64]),
+    "vit_cast_rows_masked": (c_i32, [c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_i64, c_vp]),
     "vit_router_select": (c_i32, [c_vp, c_i64, c_i32, ctypes.POINTER(ctypes.c_uint32), c_i32, c_vp, c_vp, c_vp, c_vp]),
     "vit_cls_mse": (c_i32, [c_vp, c_i64, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp]),
     "vit_cls_mse_bwd": (c_i32, [c_vp, c_i64, c_vp, c_i64, c_i64, c_vp, c_vp]),

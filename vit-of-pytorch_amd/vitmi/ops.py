@@ -468,6 +468,17 @@ def router_select(indices, active_sets, nkeys):
     return active, sel, anyf
 
 
+def cast_rows_masked(inp, ldi, rows, cols, mask, out, ldo):
+    """out rows (bf16) = inp rows (f32) where mask (bool [rows], or None = all) is set, zeros elsewhere
+    (vit_cast_rows_masked)"""
+    _chk(inp, F32, "inp")
+    _chk(out, BF16, "out")
+    if mask is not None and (mask.dtype != torch.bool or not mask.is_contiguous() or mask.numel() != rows):
+        raise ValueError("cast_rows_masked: mask must be a contiguous bool tensor of `rows` elements")
+    check(lib().vit_cast_rows_masked(_p(inp), ldi, rows, cols, _p(mask), _p(out), ldo, _stream()),
+          "vit_cast_rows_masked")
+
+
 def unpack_bf16_f32(inp, ldi, rows, cols, out, ldo):
     """out[r*ldo + c] = f32(inp[r*ldi + c])"""
     _chk(inp, BF16, "inp")

@@ -258,10 +258,9 @@ class _FusedLayer(torch.autograd.Function):
         n1, n2 = block.attention_norm.layer_norm, block.ffn_norm.layer_norm
         dout = dout.contiguous().float().view(T, D)
         dob = torch.empty(T, D, device=dev, dtype=BF16)
-        ops.cast_bf16(dout, dob, T * D)
         am = ctx.active
-        if am is not None:  # the layer's output gradient is dout on the active rows only
-            ops.rows_select(dob, am)
+        # the layer's output gradient is dout on the active rows only: one pass, the inactive rows not read
+        ops.cast_rows_masked(dout, D, T, D, am, dob, D)
         # fc2 data gradient x GELU'(fc1 pre-activation)
         dg = torch.empty(T, M, device=dev, dtype=BF16)
         ops.gemm(dob, fz.w2_t, dg, T, M, D, a_layout=K_CONTIG, b_layout=K_CONTIG, lda=D, ldb=D, ldc=M,
