@@ -379,7 +379,9 @@ class _RowsSelect(torch.autograd.Function):
 class _ClsTap(torch.autograd.Function):
     """(x, x[:, 0, :]) with the cls rows' gradient added into x's incoming gradient in place: autograd's own slice
     backward materialises a zero [B, N, D] tensor, copies the rows in and adds it to the layer gradient (three
-    passes over T x D f32 per routed layer, for the distillation loss on the cls token)"""
+    passes over T x D f32 per routed layer, for the distillation loss on the cls token). The incoming gradient of the
+    x output is updated in place: x's consumers must not hand that same tensor to another input as well (true of the
+    Res-ViT router / layer nodes and of slicing; an AddBackward-style consumer that aliases its grad would see it)"""
 
     @staticmethod
     def forward(ctx, x):
@@ -406,7 +408,7 @@ class _ClsDistill(torch.autograd.Function):
     t the detached teacher output): forward one row-sum launch plus a fixed-order total (vit_cls_mse, which keeps
     e = x_cls - t_cls), backward ((2 / (B D)) e) g added in place into x's incoming gradient's cls rows
     (vit_cls_mse_bwd). Replaces the cls-row copy, the MSE forward (difference, square, mean) and its backward, and
-    the slice gradient's add"""
+    the slice gradient's add. The incoming gradient of the x output is updated in place (see _ClsTap)"""
 
     @staticmethod
     def forward(ctx, x, t):
