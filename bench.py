@@ -507,6 +507,8 @@ def bench_resvit(args, world, rank, dev, backend, comm):
     if os.environ.get("VITMI_RESVIT_PACK_EACH", "0") != "0":  # A/B: LoRA operands packed on every layer call
         from vitmi import resvit_fused
         resvit_fused.SHARE_PACK = False
+    if os.environ.get("VITMI_RESVIT_NO_FUSED_EMBED", "0") != "0":  # A/B: conv, cat and position add as written
+        resvit.FUSED_EMBED = False
     if os.environ.get("VITMI_RESVIT_NO_ROUTER_THROUGH", "0") != "0":  # A/B: autograd adds the block input's gradients
         resvit.ROUTER_THROUGH = False
     if os.environ.get("VITMI_RESVIT_NO_FUSED_SELECT", "0") != "0":  # A/B: isin / == / any per layer and approximator

@@ -308,3 +308,37 @@ def test_router_select_matches_torch(bs, T):
     idx2 = torch.zeros(T, device="cuda")
     _, sel2, any2 = ops.router_select(idx2, [], n - 1)
     assert bool(any2[0]) and not any(bool(any2[k]) for k in range(1, n - 1))
+
+
+@pytest.mark.parametrize("img,patch", [(224, 16), (32, 8), (56, 14)])
+def test_embed_tokens_matches_per_op(img, patch):
+    """the fused token embedding (vitmi.resvit_fused.embed_tokens: im2col + one GEMM with the PATCH epilogue writing
+    cls + pos and conv + bias + pos) against Transformer.embed + cat + PositionEmbs (frozen conv and position
+    embeddings, the LoRA configuration): token rows within 1e-5 (the same bf16 GEMM operands; the cls rows exact)
+    and the cls token's gradient within 1e-6"""
+    from vitmi import resvit
+    from vitmi import resvit_fused as rf
+    torch.manual_seed(11)
+    args = resvit.ModelArgs(dim=128, mlp_dim=256, n_layers=1, n_heads=2, n_kv_heads=2, lora_rank=4, use_lora=True,
+                            use_reslr=False, image_size=(img, img), patch_size=(patch, patch), num_classes=10)
+    m = resvit.Transformer(args).cuda()
+    assert not m.embedding.weight.requires_grad and m.cls_token.requires_grad
+    x = torch.randn(3, 3, img, img, device="cuda")
+    assert rf.embed_supported(m, x)
+    w = torch.randn(3, (img // patch) ** 2 + 1, 128, device="cuda")
+    outs = []
+    for fused in (False, True):
+        m.cls_token.grad = None
+        if fused:
+            t = rf.embed_tokens(m, x)
+        else:
+            t = m.embed(x)
+            t = torch.cat([m.cls_token.expand(t.shape[0], 1, -1), t], dim=1)
+            t = m.pos_embedding(t)
+        (t * w).sum().backward()
+        outs.append((t.detach(), m.cls_token.grad.clone()))
+    (t0, g0), (t1, g1) = outs
+    assert t1.shape == t0.shape
+    assert torch.equal(t1[:, 0], t0[:, 0])
+    assert rel(t1, t0) < 1e-5  # (the same bf16 operands and k order; the adds of bias and pos in the same order)
+    assert rel(g1, g0) < 1e-6

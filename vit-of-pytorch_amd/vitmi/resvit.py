@@ -446,6 +446,9 @@ FUSED_SELECT = True
 # a routed block's input handed to its layer through the fused router node (RouterModule.forward_through), so the
 # router's LayerNorm backward adds the layer's input gradient (False: autograd adds the two)
 ROUTER_THROUGH = True
+# the token embedding (patch conv, cls, position embeddings) as one GEMM with the engine's PATCH epilogue where the conv
+# and the position embeddings are frozen (vitmi.resvit_fused.embed_tokens; False: conv, cat, add as written)
+FUSED_EMBED = True
 
 
 def _select_rows(mask, a, b):
@@ -605,9 +608,12 @@ class Transformer(nn.Module):
     def forward(self, x: torch.Tensor, labels: torch.Tensor):
         device = self.cls_token.device
         x, labels = x.to(device), labels.to(device)
-        x = self.embed(x)
-        x = torch.cat([self.cls_token.expand(x.shape[0], 1, -1), x], dim=1)
-        x = self.pos_embedding(x)
+        if FUSED_EMBED and _fused.embed_supported(self, x):
+            x = _fused.embed_tokens(self, x)  # conv + cls + position embeddings: one GEMM (PATCH epilogue)
+        else:
+            x = self.embed(x)
+            x = torch.cat([self.cls_token.expand(x.shape[0], 1, -1), x], dim=1)
+            x = self.pos_embedding(x)
         self.acts = []
         self.soft_routing_probs = []
         self.routing_maps = {}

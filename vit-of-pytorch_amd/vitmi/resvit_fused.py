@@ -33,7 +33,7 @@ import torch
 from . import flat as _flat
 from . import ops
 from ._lib import (EPI_BF16, EPI_BIAS_BF16, EPI_BIAS_GELU_DGELU, EPI_BIAS_RESID_F32, EPI_F32, EPI_MUL_BF16,
-                   EPI_SPLITK, K_CONTIG, MN_CONTIG)
+                   EPI_PATCH, EPI_SPLITK, K_CONTIG, MN_CONTIG)
 
 BF16, F32 = torch.bfloat16, torch.float32
 KX = 64  # extra K columns of the q|k|v operand (LoRA down-projections, zero padded)
@@ -401,6 +401,66 @@ class _ClsTap(torch.autograd.Function):
 def cls_tap(x):
     """x, and its cls rows x[:, 0, :] for a loss, without the full-size zero gradient of a slice (_ClsTap)"""
     return _ClsTap.apply(x)
+
+
+class _EmbedTokens(torch.autograd.Function):
+    """patch embedding, cls token and position embeddings (res-vit/model.py:629-633: conv, cat(cls, ...), + pos) as
+    one GEMM: the images' im2col in bf16 (the cls rows left zero) times the conv weight with the PATCH epilogue, which
+    writes every token row in f32 — cls + pos[0] on the cls rows, conv + bias + pos[t] on the others — the engine's
+    embedding (src/model.py:197-204). For the LoRA configuration (frozen conv weight / bias and position embeddings):
+    the backward gives only the cls token its gradient, the column sum of the cls rows' gradient over the batch.
+    Replaces the f32 im2col, the patch-row copy, the operand cast, the concatenation and the position add."""
+
+    @staticmethod
+    def forward(ctx, x, w, bias, cls, pos, patch):
+        B, _, hh, _ = x.shape
+        g = hh // patch
+        N = g * g + 1
+        K = 3 * patch * patch
+        kpad = _rup(K, 64)
+        D = w.shape[0]
+        T = B * N
+        dev = x.device
+        cols = torch.empty(T, kpad, device=dev, dtype=BF16)
+        ops.im2col(x.detach().float().contiguous(), cols, B, hh, patch, kpad)
+        (wb,) = _pad_bf16_many([(w.detach().float().reshape(D, K).contiguous(), D, kpad)])
+        out = torch.empty(B, N, D, device=dev, dtype=F32)
+        ops.gemm(cols, wb, out, T, D, kpad, a_layout=K_CONTIG, b_layout=K_CONTIG, lda=kpad, ldb=kpad, ldc=D,
+                 epilogue=EPI_PATCH, bias=bias.detach().float().contiguous(),
+                 aux=pos.detach().float().contiguous().view(N, D), ldaux=D,
+                 aux2=cls.detach().float().contiguous().view(D), tokens=N)
+        ctx.dims = (B, N, D)
+        ctx.cls_shape = cls.shape
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        B, N, D = ctx.dims
+        dcls = None
+        if ctx.needs_input_grad[3]:
+            dcls = torch.empty(D, device=dout.device, dtype=F32)
+            d = dout.contiguous().float()
+            ops.segment_colsum(d, N * D, 1, B, D, dcls.view(1, D), D)  # sum over the images of row 0
+            dcls = dcls.view(ctx.cls_shape)
+        return None, None, None, dcls, None, None
+
+
+def embed_supported(model, x):
+    """the LoRA configuration's embedding: conv weight / bias and position embeddings frozen, square images of a
+    whole number of patches, as many tokens as position embeddings"""
+    e, pe = model.embedding, model.pos_embedding.pos_embedding
+    if not (x.is_cuda and x.dim() == 4 and x.shape[1] == 3 and x.shape[2] == x.shape[3] and e.bias is not None):
+        return False
+    if e.weight.requires_grad or e.bias.requires_grad or pe.requires_grad or x.requires_grad:
+        return False
+    g = x.shape[2] // model.patch
+    return x.shape[2] % model.patch == 0 and pe.shape[1] == g * g + 1 and pe.shape[2] == e.weight.shape[0]
+
+
+def embed_tokens(model, x):
+    """[B, N, D] f32 token rows (cls + patches, position embeddings added) as one node (_EmbedTokens)"""
+    return _EmbedTokens.apply(x, model.embedding.weight, model.embedding.bias, model.cls_token,
+                              model.pos_embedding.pos_embedding, int(model.patch))
 
 
 class _ClsDistill(torch.autograd.Function):
