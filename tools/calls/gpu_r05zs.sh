@@ -1,0 +1,7 @@
+#!/bin/bash
+# round 5, call 47: router_select with a range guard before the float -> int truncation: the Res-ViT tests
+set -o pipefail
+export TMPDIR=/tmp
+O=gpurun_out/r05zs; mkdir -p $O
+timeout -k 10 900 python -u -m pytest tests/test_resvit_gpu.py tests/test_resvit_train_gpu.py -x -q --timeout 300 --timeout-method thread > $O/tests.log 2>&1 || { tail -60 $O/tests.log; exit 1; }
+tail -1 $O/tests.log

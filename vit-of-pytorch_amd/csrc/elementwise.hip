@@ -1587,8 +1587,11 @@ __global__ void __launch_bounds__(1024) router_select_kernel(const float* __rest
     for (int j = 0; j < npos; ++j) {
       unsigned w = 0;
       for (int e = 0; e < n; ++e) {
-        const long lv = (long)v[e];  // torch's .long(): truncation toward zero
-        if (lv >= 0 && lv < 32 && ((a.mask[j] >> lv) & 1u)) w |= 1u << (8 * e);
+        // torch's .long(): truncation toward zero (so (-1, 0) -> 0); values whose truncation is outside [0, 32) (and
+        // NaN) are in no set, and are not converted (an out-of-range float -> integer conversion is undefined)
+        const bool in_range = v[e] > -1.f && v[e] < 32.f;
+        const int lv = in_range ? (int)v[e] : 0;
+        if (in_range && ((a.mask[j] >> lv) & 1u)) w |= 1u << (8 * e);
       }
       if (vec) *reinterpret_cast<unsigned*>(active + j * T + t) = w;
       else active[j * T + t] = (unsigned char)w;
