@@ -66,6 +66,25 @@ def pmc_traffic(kernel_tag="gemm_pp2_kernel<true, true, 8,"):
     return None
 
 
+def onecycle_hyper_table(total_steps, dev):
+    """{lr, momentum, first-step} of every bench step as a [steps][3] f32 device table: torch's OneCycleLR as the
+    reference configures it (src/train.py:159-163: max_lr .03, 500 warm-up of 15000 steps, cycle_momentum) driving
+    SGD(momentum .9). The SGD kernel of the timed step (vit_sgd_step_dev) reads its scalars from one row of it,
+    refreshed by a 12-byte device copy before each step, so the step can be one HIP graph
+    (tests/test_optim_dev_gpu.py pins this table and that kernel against the oracle)."""
+    from torch.optim.lr_scheduler import OneCycleLR
+    _p = torch.nn.Parameter(torch.zeros(1))
+    _opt = torch.optim.SGD([_p], lr=0.03, momentum=0.9)
+    sched = OneCycleLR(_opt, max_lr=0.03, pct_start=500 / 15000, total_steps=15000)
+    hp = []
+    for _ in range(total_steps):
+        hp.append((_opt.param_groups[0]["lr"], _opt.param_groups[0]["momentum"]))
+        _opt.step()
+        sched.step()
+    return torch.tensor([[lr_, mom_, 1.0 if k == 0 else 0.0] for k, (lr_, mom_) in enumerate(hp)],
+                        device=dev, dtype=torch.float32)
+
+
 def _cpu_model():
     try:
         for line in open("/proc/cpuinfo"):
@@ -233,21 +252,7 @@ def main():
     reducer = (GradAllReducer(eng, average=False, compress=compress).attach()  # CE pre-scaled by 1/(b*world)
                if world > 1 else None)
     total_steps = args.warmup + args.steps
-    # OneCycleLR schedule scalars as configured by reference src/train.py:159-163 (lr .03, 500 warmup/15000)
-    from torch.optim.lr_scheduler import OneCycleLR
-    _p = torch.nn.Parameter(torch.zeros(1))
-    _opt = torch.optim.SGD([_p], lr=0.03, momentum=0.9)
-    sched = OneCycleLR(_opt, max_lr=0.03, pct_start=500 / 15000, total_steps=15000)
-    hp = []
-    for _ in range(total_steps):
-        hp.append((_opt.param_groups[0]["lr"], _opt.param_groups[0]["momentum"]))
-        _opt.step()
-        sched.step()
-
-    # the schedule's {lr, momentum, first-step} of every step on the device: the SGD kernel reads them from
-    # `hyper`, refreshed by a 12-byte device copy before each step, so the step can be one HIP graph
-    hyper_all = torch.tensor([[lr_, mom_, 1.0 if k == 0 else 0.0] for k, (lr_, mom_) in enumerate(hp)],
-                             device=dev, dtype=torch.float32)
+    hyper_all = onecycle_hyper_table(total_steps, dev)
     hyper = hyper_all[0].clone()
 
     def step_body():

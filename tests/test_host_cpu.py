@@ -58,6 +58,10 @@ def test_library_with_foreign_build_id_is_refused(tmp_path):
     (tmp_path / "include").mkdir()
     shutil.copy(HEADER, tmp_path / "include" / "vit_hip.h")
     assert buildid.tree_id(str(pkg)) == buildid.tree_id()
+    # editor swap / backup files beside the sources are not sources: same id
+    (pkg / "csrc" / ".gemm.hip.swp").write_bytes(b"swap")
+    (pkg / "csrc" / "gemm.hip~").write_text("backup")
+    assert buildid.tree_id(str(pkg)) == buildid.tree_id()
     with open(pkg / "csrc" / "gemm.hip", "a") as f:
         f.write("\n// edited\n")
     other = buildid.tree_id(str(pkg))

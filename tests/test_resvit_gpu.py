@@ -283,6 +283,46 @@ def test_cls_distill_matches_per_op():
         assert torch.equal(g1[:, 1:], g0[:, 1:])
 
 
+class _AliasAdd(torch.autograd.Function):
+    """a + b whose backward hands both inputs ONE gradient object (as an AddBackward of the per-op layer path can)"""
+
+    @staticmethod
+    def forward(ctx, a, b):
+        return a + b
+
+    @staticmethod
+    def backward(ctx, g):
+        return g, g
+
+
+@pytest.mark.parametrize("node", ["distill", "tap"])
+def test_cls_nodes_copy_a_shared_gradient(node):
+    """The cls nodes' in-place gradient add (advisor, round 5): by default (inplace=False, what ResViT.forward passes
+    when the next consumer is not the fused layer node) the incoming gradient is copied before the cls rows are added,
+    so a consumer that gave the same gradient object to another input still sees its own values. The other input's
+    node is created first, so autograd runs the cls node's backward before it."""
+    import torch.nn.functional as F
+    from vitmi import resvit_fused as rf
+    torch.manual_seed(5)
+    B, N, D = 3, 9, 64
+    x0, t, w = (torch.randn(B, N, D, device="cuda") for _ in range(3))
+    v = torch.randn(B, N, D, device="cuda", requires_grad=True)
+    u = v * 3.0  # created before the cls node: its backward runs after it
+    x = x0.clone().requires_grad_(True)
+    if node == "distill":
+        y, loss = rf.cls_distill(x, t)
+    else:
+        y, s = rf.cls_tap(x)
+        loss = F.mse_loss(s, t[:, 0, :])
+    z = _AliasAdd.apply(y, u)
+    (2.0 * loss + (z * w).sum()).backward()
+    assert torch.equal(v.grad, 3.0 * w)  # not touched by the cls rows' loss gradient
+    dcls = 2.0 * 2.0 * (x0[:, 0, :] - t[:, 0, :]) / (B * D)
+    ref = w.clone()
+    ref[:, 0, :] += dcls
+    assert rel(x.grad, ref) < 1e-6
+
+
 @pytest.mark.parametrize("T", [3 * 197, 4 * 197])
 @pytest.mark.parametrize("bs", [1, 2, 4])
 def test_router_select_matches_torch(bs, T):

@@ -475,7 +475,7 @@ def test_fused_approximator_matches_per_op_path(B, N, r):
     assert torch.equal(res[True][0][~sel], x[~sel])  # unrouted rows pass through unchanged
 
 
-@pytest.mark.parametrize("B,N,hdim,bs", [(3, 197, 64, 1), (2, 17, 512, 2)])
+@pytest.mark.parametrize("B,N,hdim,bs", [(3, 197, 64, 1), (2, 17, 512, 2), (2, 17, 48, 1), (2, 17, 40, 1)])
 def test_fused_router_mlp_matches_per_op_path(B, N, hdim, bs):
     """vitmi.resvit_fused.router_mlp (RouterModule.out_conv as one node: GELU and GELU' written by the GEMM
     epilogues, GELU' multiplied in the data-gradient epilogues) against the per-op path (res-vit/model.py:
@@ -497,7 +497,11 @@ def test_fused_router_mlp_matches_per_op_path(B, N, hdim, bs):
         for p in params:
             p.grad = None
         from vitmi import resvit_fused
-        out = resvit_fused.router_mlp(r.out_conv, xi) if fused else r.out_conv(xi)
+        if fused and not resvit_fused.router_mlp_supported(r.out_conv, xi):
+            assert hdim % 16, hdim  # only widths the fused GEMM epilogues cannot take fall back
+            out = r.out_conv(xi)
+        else:
+            out = resvit_fused.router_mlp(r.out_conv, xi) if fused else r.out_conv(xi)
         (out * w).sum().backward()
         res[fused] = (out.detach(), xi.grad.detach(), [p.grad.detach().clone() for p in params])
     (o1, dx1, g1), (o0, dx0, g0) = res[True], res[False]
@@ -507,7 +511,8 @@ def test_fused_router_mlp_matches_per_op_path(B, N, hdim, bs):
         assert rel(a, b) < 2e-2, (rel(a, b), a.shape)
 
 
-@pytest.mark.parametrize("B,N,hdim,reserve", [(3, 197, 64, 1), (2, 17, 512, 0)])
+@pytest.mark.parametrize("B,N,hdim,reserve", [(3, 197, 64, 1), (2, 17, 512, 0), (2, 17, 48, 1), (2, 17, 40, 1),
+                                             (2, 17, 100, 1)])
 def test_fused_router_net_matches_per_op_path(B, N, hdim, reserve):
     """vitmi.resvit_fused.router_net (LN -> Linear -> GELU -> token mean -> concatenation -> out_conv as one node,
     the concatenated operand built in bf16 by the GEMM epilogue and a broadcast) against the per-op router
@@ -525,6 +530,9 @@ def test_fused_router_net_matches_per_op_path(B, N, hdim, reserve):
     x = torch.randn(B, N, 64, device="cuda", generator=g)
     w = torch.randn(B, N, 1, 2, device="cuda", generator=g)
     params = list(r.parameters())
+    from vitmi import resvit_fused
+    # hdim 40 / 100 (hidden widths not multiples of 8): the router runs the per-op path instead of raising
+    assert resvit_fused.router_net_supported(r, x) == (hdim % 16 == 0), hdim
     res = {}
     for fused in (True, False):
         r.fused_mlp = fused
@@ -663,3 +671,42 @@ def test_router_through_matches_autograd_add(gold, monkeypatch):
     assert g0.keys() == g1.keys() and len(g0) > 0
     for k in g0:
         assert rel(g1[k], g0[k]) < 1e-5, (k, rel(g1[k], g0[k]))
+
+
+def test_share_teacher_matches_two_pass(gold, monkeypatch):
+    """SHARE_TEACHER (advisor, round 5): the first routed layer's teacher output taken from the student's grad-enabled
+    layer forward equals the reference's separate teacher pass (res-vit/model.py:496-512) — the first routed layer's
+    teacher and student outputs bit-identical, one reference step's losses equal and every trainable gradient (LoRA,
+    router, approximators, head) within 1e-6 — while the layer is deterministic (no active dropout: the share is gated
+    on that, vitmi.resvit._active_dropout)"""
+    from vitmi import resvit
+    from vitmi.resvit_train import total_loss
+    h = hp(gold)
+    runs, outs = [], []
+    for share in (False, True):
+        monkeypatch.setattr(resvit, "SHARE_TEACHER", share)
+        m = build(gold).train()
+        assert not resvit._active_dropout(m.layers[0])
+        for j, r in enumerate(l.router for l in m.layers if hasattr(l, "router")):
+            hh = torch.from_numpy(gold[f"s0/router{j}_hard"]).cuda()
+            gg = torch.from_numpy(gold[f"s0/gumbel{j}"]).cuda()
+            r.hard_override = lambda logits, hh=hh: hh
+            r.gumbel_noise = lambda logits, gg=gg: gg
+        first = next(l for l in m.layers if l.use_reslr and l.layer_id >= l.dynamic_start_layer)
+        seen = []
+        hook = first.register_forward_hook(lambda mod, inp, out: seen.append((out[0].detach().clone(),
+                                                                              out[1].detach().clone())))
+        x = torch.from_numpy(gold["s0/x"]).cuda()
+        y = torch.from_numpy(gold["s0/y"]).cuda()
+        c, a, d, ent, _ = m(x, y)
+        hook.remove()
+        total = total_loss(m, c, a, d, h["la"], h["ld"], h["lc"])
+        total.backward()
+        outs.append(seen[0])
+        runs.append((float(total), {n: p.grad.clone() for n, p in m.named_parameters() if p.grad is not None}))
+    (t0, g0), (t1, g1) = runs
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    assert t0 == t1
+    assert g0.keys() == g1.keys() and len(g0) > 0
+    for k in g0:
+        assert rel(g1[k], g0[k]) < 1e-6, (k, rel(g1[k], g0[k]))

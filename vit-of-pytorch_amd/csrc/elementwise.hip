@@ -379,8 +379,28 @@ __global__ void __launch_bounds__(256) ce_kernel(const float* __restrict__ logit
 }
 
 // ---- SGD momentum (torch.optim.SGD, dampening 0, no nesterov), src/train.py:154-158 -------------
+// One body for both entry points: the scalars {lr, momentum, first} come either as kernel arguments (vit_sgd_step)
+// or from three floats in device memory (vit_sgd_step_dev: the step can sit in a captured HIP graph while the
+// schedule moves; the caller refreshes the floats before each launch).
+struct SgdHostScalars {
+  float lr, mom;
+  int first;
+  __device__ __forceinline__ void get(float& l, float& m, bool& f) const { l = lr; m = mom; f = first != 0; }
+};
+struct SgdDevScalars {
+  const float* hyper;
+  __device__ __forceinline__ void get(float& l, float& m, bool& f) const {
+    l = hyper[0];
+    m = hyper[1];
+    f = hyper[2] != 0.0f;
+  }
+};
+template <class S>
 __global__ void sgd_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ buf,
-                           bf16_t* __restrict__ pb, long n, float lr, float mom, float wd, int first) {
+                           bf16_t* __restrict__ pb, long n, const S sc, float wd) {
+  float lr, mom;
+  bool first;
+  sc.get(lr, mom, first);
   const long n4 = n / 4;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
     float4 pv = reinterpret_cast<float4*>(p)[i];
@@ -663,49 +683,14 @@ extern "C" int vit_cross_entropy(const float* logits, const int64_t* labels, int
   VIT_LAUNCH_CHECK("vit_cross_entropy");
 }
 
-// hyper = {lr, momentum, first (0 / 1)} in device memory: the step can sit in a captured HIP graph while the
-// schedule moves (the caller refreshes the three floats before each launch)
-__global__ void sgd_dev_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ buf,
-                               bf16_t* __restrict__ pb, long n, const float* __restrict__ hyper, float wd) {
-  const float lr = hyper[0], mom = hyper[1];
-  const bool first = hyper[2] != 0.0f;
-  const long n4 = n / 4;
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
-    float4 pv = reinterpret_cast<float4*>(p)[i];
-    const float4 gv = reinterpret_cast<const float4*>(g)[i];
-    float4 d = make_float4(gv.x + wd * pv.x, gv.y + wd * pv.y, gv.z + wd * pv.z, gv.w + wd * pv.w);
-    if (!first) {
-      const float4 bv = reinterpret_cast<float4*>(buf)[i];
-      d = make_float4(mom * bv.x + d.x, mom * bv.y + d.y, mom * bv.z + d.z, mom * bv.w + d.w);
-    }
-    reinterpret_cast<float4*>(buf)[i] = d;
-    pv = make_float4(pv.x - lr * d.x, pv.y - lr * d.y, pv.z - lr * d.z, pv.w - lr * d.w);
-    reinterpret_cast<float4*>(p)[i] = pv;
-    if (pb) {
-      uint2 u;
-      u.x = pack2bf(pv.x, pv.y);
-      u.y = pack2bf(pv.z, pv.w);
-      reinterpret_cast<uint2*>(pb)[i] = u;
-    }
-  }
-  const long t = n4 * 4 + (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (blockIdx.x == 0 && t < n) {
-    float d = g[t] + wd * p[t];
-    if (!first) d = mom * buf[t] + d;
-    buf[t] = d;
-    p[t] -= lr * d;
-    if (pb) pb[t] = f2bf(p[t]);
-  }
-}
-
 extern "C" int vit_sgd_step_dev(float* p, const float* g, float* buf, void* p_bf16, int64_t n, const float* hyper,
                                 float weight_decay, vit_stream_t stream) {
   VIT_CHECK_ARG(p && g && buf && hyper && n >= 0, "vit_sgd_step_dev: bad args");
   VIT_CHECK_ARG(((uintptr_t)p | (uintptr_t)g | (uintptr_t)buf) % 16 == 0 && ((uintptr_t)p_bf16 % 8 == 0),
                 "vit_sgd_step_dev: buffers must be 16-B aligned (bf16 mirror 8-B)");
   if (n == 0) return VIT_OK;
-  hipLaunchKernelGGL(sgd_dev_kernel, dim3(grid_for(n, 4)), dim3(256), 0, (hipStream_t)stream, p, g, buf,
-                     (bf16_t*)p_bf16, (long)n, hyper, weight_decay);
+  hipLaunchKernelGGL(sgd_kernel<SgdDevScalars>, dim3(grid_for(n, 4)), dim3(256), 0, (hipStream_t)stream, p, g, buf,
+                     (bf16_t*)p_bf16, (long)n, SgdDevScalars{hyper}, weight_decay);
   VIT_LAUNCH_CHECK("vit_sgd_step_dev");
 }
 
@@ -715,8 +700,8 @@ extern "C" int vit_sgd_step(float* p, const float* g, float* buf, void* p_bf16, 
   VIT_CHECK_ARG(((uintptr_t)p | (uintptr_t)g | (uintptr_t)buf) % 16 == 0 && ((uintptr_t)p_bf16 % 8 == 0),
                 "vit_sgd_step: buffers must be 16-B aligned (bf16 mirror 8-B)");
   if (n == 0) return VIT_OK;
-  hipLaunchKernelGGL(sgd_kernel, dim3(grid_for(n, 4)), dim3(256), 0, (hipStream_t)stream, p, g, buf, (bf16_t*)p_bf16,
-                     (long)n, lr, momentum, weight_decay, (int)first);
+  hipLaunchKernelGGL(sgd_kernel<SgdHostScalars>, dim3(grid_for(n, 4)), dim3(256), 0, (hipStream_t)stream, p, g, buf,
+                     (bf16_t*)p_bf16, (long)n, SgdHostScalars{lr, momentum, (int)first}, weight_decay);
   VIT_LAUNCH_CHECK("vit_sgd_step");
 }
 

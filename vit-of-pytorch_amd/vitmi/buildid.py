@@ -15,12 +15,17 @@ import sys
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
+SOURCE_SUFFIXES = (".hip", ".h", ".inc")  # what the Makefile compiles or includes from csrc/
+
+
 def source_files(pkg_root: str = PKG_ROOT) -> list[str]:
     """Every file the library is built from, relative to the package root, in a fixed order: the
-    Makefile, each file of csrc/, the C-ABI header."""
+    Makefile, each HIP source / header / include of csrc/ (not editor swap or backup files that may
+    sit beside them), the C-ABI header."""
     csrc = os.path.join(pkg_root, "csrc")
     files = ["Makefile"] + [os.path.join("csrc", f) for f in sorted(os.listdir(csrc))
-                            if os.path.isfile(os.path.join(csrc, f))]
+                            if f.endswith(SOURCE_SUFFIXES) and not f.startswith(".")
+                            and os.path.isfile(os.path.join(csrc, f))]
     return files + [os.path.join("..", "include", "vit_hip.h")]
 
 

@@ -431,6 +431,14 @@ FOLD_SELECT = True
 # teacher output (detached) and the student's (row selection after it) instead of a no-grad teacher pass plus a
 # folded student pass (False: the two passes)
 SHARE_TEACHER = True
+
+
+def _active_dropout(module):
+    """a dropout with p > 0 inside `module` in training mode: its forward is not deterministic, so a teacher output
+    taken from the student's pass would differ from the reference's separate teacher pass (SHARE_TEACHER's premise)"""
+    return module.training and any(isinstance(m, torch.nn.Dropout) and m.p > 0 for m in module.modules())
+
+
 # the distillation loss's cls rows taken through vitmi.resvit_fused.cls_tap (their gradient added in place), and the
 # final LayerNorm on the cls rows only (False: the slices and the all-row norm as written)
 CLS_TAP = True
@@ -486,6 +494,15 @@ class TransformerBlock(nn.Module):
                                            args.norm_eps, block_size=self.block_size, use_lora=args.use_lora)
                 self.block_path_approximators = BlockPathApproximators(args.dim, args.low_rank_dim, self.block_size)
 
+    def takes_fused_path(self, x):
+        """whether this layer consumes x only through fused nodes (the layer node and, on a block head, the fused
+        router), whose backwards return gradients no other input shares"""
+        if not (self.fused and x.dim() == 3 and x.is_cuda and _fused.supported(self)):
+            return False
+        if self.use_reslr and self.layer_id >= self.dynamic_start_layer and self.is_block_head:
+            return bool(self.router.fused_mlp and _fused.router_net_supported(self.router, x))
+        return True
+
     def _full(self, x, packed=False, active=None):
         """the full layer; with `active` (bool [B, N, 1]) where(active, layer(x), x), the routed student's rows"""
         if self.fused and x.dim() == 3 and x.is_cuda and _fused.supported(self):
@@ -536,7 +553,7 @@ class TransformerBlock(nn.Module):
 
         if self.training:
             if (SHARE_TEACHER and (teacher_x is None or teacher_x is x_in) and self.fused and x.dim() == 3 and x.is_cuda
-                    and _fused.supported(self)):
+                    and _fused.supported(self) and not _active_dropout(self)):
                 # the teacher's input is the student's (the first routed layer): one layer forward serves both
                 teacher_out, student_out = _fused.teacher_and_student(self, x, active)
                 return teacher_out, approximators(student_out, router_indices, lra_lora, sel_info), w, block_info
@@ -621,17 +638,21 @@ class Transformer(nn.Module):
         r_entropy = torch.zeros((), device=device)
         block_info = {}
         teacher_x, student_x = x, x
-        for layer in self.layers:
+        for li, layer in enumerate(self.layers):
             if self.use_reslr and layer.layer_id >= layer.dynamic_start_layer:
                 if self.training:
                     teacher_out, student_out, w, block_info = layer(student_x, teacher_x, block_info, self.LRA_mask)
+                    # the cls nodes may add into the incoming gradient in place only when every consumer of their
+                    # output returns a fresh gradient: the next layer's fused node (and router), or the final norm
+                    nxt = self.layers[li + 1] if li + 1 < len(self.layers) else None
+                    inplace = nxt is None or nxt.takes_fused_path(student_out)
                     if (FUSED_DISTILL and CLS_TAP and student_out.is_cuda and student_out.dtype == torch.float32
                             and teacher_out.dtype == torch.float32 and type(self.criterion_distill) is DistillLoss):
-                        student_out, dl = _fused.cls_distill(student_out, teacher_out)
+                        student_out, dl = _fused.cls_distill(student_out, teacher_out, inplace)
                         d_loss = d_loss + dl
                     else:
                         if CLS_TAP and student_out.is_cuda:
-                            student_out, s_cls = _fused.cls_tap(student_out)
+                            student_out, s_cls = _fused.cls_tap(student_out, inplace)
                         else:
                             s_cls = student_out[:, 0, :]
                         d_loss = d_loss + self.criterion_distill(s_cls, teacher_out[:, 0, :])

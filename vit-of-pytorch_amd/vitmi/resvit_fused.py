@@ -377,30 +377,35 @@ class _RowsSelect(torch.autograd.Function):
 
 
 class _ClsTap(torch.autograd.Function):
-    """(x, x[:, 0, :]) with the cls rows' gradient added into x's incoming gradient in place: autograd's own slice
-    backward materialises a zero [B, N, D] tensor, copies the rows in and adds it to the layer gradient (three
-    passes over T x D f32 per routed layer, for the distillation loss on the cls token). The incoming gradient of the
-    x output is updated in place: x's consumers must not hand that same tensor to another input as well (true of the
-    Res-ViT router / layer nodes and of slicing; an AddBackward-style consumer that aliases its grad would see it)"""
+    """(x, x[:, 0, :]) with the cls rows' gradient added into x's incoming gradient: autograd's own slice backward
+    materialises a zero [B, N, D] tensor, copies the rows in and adds it to the layer gradient (three passes over
+    T x D f32 per routed layer, for the distillation loss on the cls token). With inplace=True the incoming gradient
+    of the x output is updated in place, which is only safe when x's consumers hand no other input that same tensor:
+    the caller (ResViT.forward) sets it only when x feeds the fused layer node (and the fused router), whose
+    backwards return fresh gradients, or the final norm's slice; otherwise the gradient is copied first (an
+    AddBackward-style consumer, as the per-op layer's residual add, gives both its inputs one gradient object)."""
 
     @staticmethod
-    def forward(ctx, x):
+    def forward(ctx, x, inplace=False):
         ctx.shape = x.shape
+        ctx.inplace = bool(inplace)
         return x.view(x.shape), x[:, 0, :].clone()
 
     @staticmethod
     def backward(ctx, dx, dcls):
         if dx is None:
             dx = torch.zeros(ctx.shape, device=dcls.device, dtype=dcls.dtype)
+        elif dcls is not None and not ctx.inplace:
+            dx = dx.clone()
         if dcls is not None:
             dx = dx.contiguous()
             dx[:, 0, :] += dcls
-        return dx
+        return dx, None
 
 
-def cls_tap(x):
+def cls_tap(x, inplace=False):
     """x, and its cls rows x[:, 0, :] for a loss, without the full-size zero gradient of a slice (_ClsTap)"""
-    return _ClsTap.apply(x)
+    return _ClsTap.apply(x, inplace)
 
 
 class _EmbedTokens(torch.autograd.Function):
@@ -468,11 +473,13 @@ class _ClsDistill(torch.autograd.Function):
     t the detached teacher output): forward one row-sum launch plus a fixed-order total (vit_cls_mse, which keeps
     e = x_cls - t_cls), backward ((2 / (B D)) e) g added in place into x's incoming gradient's cls rows
     (vit_cls_mse_bwd). Replaces the cls-row copy, the MSE forward (difference, square, mean) and its backward, and
-    the slice gradient's add. The incoming gradient of the x output is updated in place (see _ClsTap)"""
+    the slice gradient's add. With inplace=True the incoming gradient of the x output is updated in place, else a
+    copy of it (the ownership rule of _ClsTap)"""
 
     @staticmethod
-    def forward(ctx, x, t):
+    def forward(ctx, x, t, inplace=False):
         ctx.set_materialize_grads(False)
+        ctx.inplace = bool(inplace)
         B, N, D = x.shape
         xc, tc = x.detach().contiguous(), t.detach().contiguous()
         loss, e = ops.cls_mse(xc, N * D, tc, tc.shape[1] * tc.shape[2], B, D)
@@ -485,17 +492,19 @@ class _ClsDistill(torch.autograd.Function):
         (e,) = ctx.saved_tensors
         B, N, D = ctx.shape
         if dloss is None:
-            return dx, None
+            return dx, None, None
         if dx is None:
             dx = torch.zeros(ctx.shape, device=e.device, dtype=F32)
+        elif not ctx.inplace:
+            dx = dx.clone()
         dx = dx.contiguous()
         ops.cls_mse_bwd(dx, N * D, e, dloss.detach().float().contiguous())
-        return dx, None
+        return dx, None, None
 
 
-def cls_distill(x, t):
+def cls_distill(x, t, inplace=False):
     """x and mse_loss(x[:, 0, :], t[:, 0, :].detach()) as one node (_ClsDistill)"""
-    return _ClsDistill.apply(x, t)
+    return _ClsDistill.apply(x, t, inplace)
 
 
 class _RouterHead(torch.autograd.Function):
@@ -962,7 +971,9 @@ class _RouterNet(torch.autograd.Function):
 
 
 def router_mlp_supported(seq, x):
-    """out_conv as built by RouterModule: Linear, GELU (exact), Linear, GELU, Linear, biases present"""
+    """out_conv as built by RouterModule: Linear, GELU (exact), Linear, GELU, Linear, biases present; both hidden widths
+    multiples of 8 (the data-gradient GEMMs of _dgrad_mul write the hidden-bias column partials, which the GEMM takes in
+    8-column chunks only). Any other --dynamic_router_hdim runs the per-op path."""
     from .model import GELU as _GELU, Linear as _Linear
     if not x.is_cuda or len(seq) != 5:
         return False
@@ -970,6 +981,8 @@ def router_mlp_supported(seq, x):
     if not all(type(l) is _Linear and l.bias is not None and l.weight.dtype == F32 for l in lins):
         return False
     if not all(type(g) is _GELU and g.approximate == "none" for g in gelus):
+        return False
+    if lins[0].weight.shape[0] % 8 or lins[1].weight.shape[0] % 8:
         return False
     return (lins[0].weight.shape[1] == x.shape[-1] and lins[1].weight.shape[1] == lins[0].weight.shape[0]
             and lins[2].weight.shape[1] == lins[1].weight.shape[0])
@@ -983,7 +996,8 @@ def router_mlp(seq, x):
 
 def router_net_supported(router, x):
     """RouterModule as built: in_conv = (LayerNorm, Linear, GELU exact), out_conv as router_mlp_supported, at least
-    one non-reserved token"""
+    one non-reserved token, an even in_conv width h (vit_router_dx_gate reads dX_embed in pairs, and the global half
+    of the concatenated operand starts at column h: vit_segment_colsum_bcast needs it 4-byte aligned)"""
     from .model import GELU as _GELU, Linear as _Linear
     ic = router.in_conv
     if len(ic) != 3 or not (x.is_cuda and x.dim() == 3 and x.shape[1] > router.reserve_initials):
@@ -993,7 +1007,7 @@ def router_net_supported(router, x):
         return False
     if not (type(ic[1]) is _Linear and ic[1].bias is not None and type(ic[2]) is _GELU and ic[2].approximate == "none"):
         return False
-    if ic[1].weight.shape[1] != x.shape[-1]:
+    if ic[1].weight.shape[1] != x.shape[-1] or ic[1].weight.shape[0] % 2:
         return False
     probe = torch.empty(0, 0, 2 * ic[1].weight.shape[0], device=x.device)
     return router_mlp_supported(router.out_conv, probe)
