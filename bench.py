@@ -318,6 +318,8 @@ def main():
     if world > 1:
         dist_check = replica_check(eng.flat, dt, args.steps, world, backend, dev)
         dt = dist_check.pop("_dt_max")
+        ops.copy2d(hyper, 12, hyper_all[total_steps - 1], 12, 12, 1)
+        dist_check["exchange"] = exchange_check(step_body, reducer, dt, args.steps, world, dev, barrier)
     fc1_ms = sum(s.elapsed_time(e) for s, e in probe) / max(1, len(probe))
     fd_ms = [s_.elapsed_time(e_) for s_, e_, _, _ in probe_fd]
     fd_flop = sum(p_[2] for p_ in probe_fd)
@@ -430,6 +432,15 @@ def main():
     }
     if dist_check is not None:
         out["dist_check"] = dist_check
+    if world == 1 and os.environ.get("VITMI_BENCH_TRAIN_EPOCH", "1") != "0":
+        # the drop-in path (train_epoch + vitmi.optim.SGD + OneCycleLR + metrics) at the same shape, after the engine
+        # loop: how much of `value` a user of the reference's entry point sees
+        te, te_res = time_train_epoch(model, b, args.image_size, args.num_classes, args.steps, args.warmup, dev)
+        out["train_epoch_img_s"] = round(te, 2)
+        out["train_epoch_vs_value"] = round(te / value, 4)
+        out["train_epoch_note"] = ("vitmi.train.train_epoch (src/train.py:12-37) + vitmi.optim.SGD + torch OneCycleLR + "
+                                   f"loss/acc1/acc5 metrics, {args.steps} synthetic HBM-resident batches of {b} after a "
+                                   f"{args.warmup}-batch epoch; last epoch loss {te_res['loss']:.4f}")
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(arch, args.image_size, args.num_classes, args.cpu_seconds)
     if rank == 0:
@@ -469,6 +480,71 @@ def replica_check(flat, dt, steps, world, backend, dev):
             "ms_per_step_spread_pct": round((max(per) - min(per)) / min(per) * 100, 2),
             "replicas_identical": same, "param_hash_rank0": [int(x) for x in hs[0].tolist()],
             "_dt_max": max(float(x) for x in ts)}
+
+
+def time_train_epoch(model, b, image_size, num_classes, steps, warmup, dev):
+    """The drop-in user path at the bench's shape: vitmi.train.train_epoch (reference src/train.py:12-37) driving the
+    model through autograd, vitmi.model.CrossEntropyLoss, vitmi.optim.SGD(momentum .9) + torch's OneCycleLR as
+    src/train.py:151-163 configure them, and the loss / top-1 / top-5 metrics, on a synthetic HBM-resident batch.
+    Returns images/s over `steps` batches after a `warmup`-batch epoch (its per-100-batch progress line goes to
+    stderr, keeping stdout the one JSON line)."""
+    import contextlib
+
+    from vitmi.model import CrossEntropyLoss
+    from vitmi.optim import SGD
+    from vitmi.train import MetricTracker, SyntheticDataLoader, train_epoch
+    crit = CrossEntropyLoss()
+    opt = SGD(model.parameters(), lr=0.03, momentum=0.9, weight_decay=0.0, model=model)
+    sched = torch.optim.lr_scheduler.OneCycleLR(opt, max_lr=0.03, pct_start=500 / 15000, total_steps=15000)
+    metrics = MetricTracker("loss", "acc1", "acc5")
+    model.train()
+    with contextlib.redirect_stdout(sys.stderr):
+        train_epoch(1, model, SyntheticDataLoader(b, image_size, num_classes, warmup, dev, seed=7), crit, opt, sched,
+                    metrics, dev)
+        torch.cuda.synchronize()
+        loader = SyntheticDataLoader(b, image_size, num_classes, steps, dev, seed=8)
+        t0 = time.perf_counter()
+        res = train_epoch(2, model, loader, crit, opt, sched, metrics, dev)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+    return steps * b / dt, res
+
+
+def exchange_check(step_fn, reducer, dt, steps, world, dev, sync, solo_steps=None):
+    """N > 1: what the gradient exchange costs per step, for a reader of the driver's 8-GPU line (is the
+    all-reduce hidden under the backward or serialised after it?). (1) One more step with the reducer's
+    accounting on: the per-step all-reduce time (HIP events around every bucket's collective on the exchange
+    stream, summed) and the bytes exchanged. (2) The same step WITHOUT the exchange (reducer detached, every rank
+    computing alone at the same time, same job and clocks), timed like the main loop (max over ranks): exposed
+    communication = the N-rank ms/step minus this solo ms/step. Runs after the replica check (the solo steps
+    apply unreduced gradients, so the replicas diverge from here on). Reference: src/train.py:128-129."""
+    import torch.distributed as dist
+    reducer.timing = []
+    step_fn()
+    sync()
+    ar_ms, buckets, elems = reducer.timing_summary()
+    reducer.timing = None
+    reducer.detach()
+    n = solo_steps or steps
+    step_fn()  # warm-up without the exchange
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(n):
+        step_fn()
+    sync()
+    solo = torch.tensor([time.perf_counter() - t0], device=dev, dtype=torch.float64)
+    dist.all_reduce(solo, op=dist.ReduceOp.MAX)
+    reducer.attach()
+    solo_ms = float(solo) / n * 1e3
+    step_ms = dt / steps * 1e3
+    bpe = 2 if reducer.compress else 4
+    return {"allreduce_ms_per_step": round(ar_ms, 3), "allreduce_buckets": buckets,
+            "allreduce_bytes_per_step": int(elems) * bpe,
+            "allreduce_algbw_gbs": round(int(elems) * bpe * 2 * (world - 1) / world / (ar_ms * 1e-3) / 1e9, 1)
+            if ar_ms > 0 else None,
+            "solo_ms_per_step": round(solo_ms, 3), "exposed_comm_ms_per_step": round(step_ms - solo_ms, 3),
+            "note": "allreduce_ms: sum of the per-bucket collectives on the exchange stream (overlapped with the backward "
+                    "where exposed_comm is small); solo: the same step with no exchange, every rank at once"}
 
 
 def resvit_flops_per_image(a, image_size, block_heads, active_ratio):

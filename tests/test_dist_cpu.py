@@ -118,3 +118,45 @@ def test_bench_replica_check_gloo(differ):
         assert o["_dt_max"] == 1.5
         assert o["ms_per_step_per_rank"] == [100.0, 150.0]
         assert o["replicas_identical"] is (not differ)
+
+
+def _exchange_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import bench
+    from vitmi.dist import GradAllReducer
+    sizes = [10, 100, 100, 100, 37]
+    eng = _FakeEngine(sizes)
+    red = GradAllReducer(eng, min_bucket_elems=50).attach()
+
+    def step():
+        eng.backward(rank)
+        red.finish()
+    out = bench.exchange_check(step, red, 0.5, 10, world, torch.device("cpu"), lambda: None, solo_steps=3)
+    attached = eng.grad_ready_hook is not None
+    q.put((rank, out, attached))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_bench_exchange_check_gloo():
+    """bench.py's N > 1 exchange accounting (2 gloo ranks on the CPU): one step with the reducer's accounting on
+    gives the all-reduced bytes of the whole flat buffer (four buckets: the head coalesced with the next layer),
+    a solo timing with the reducer detached, the exposed time as their difference; the reducer is re-attached."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_exchange_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = {r: (o, a) for r, o, a in (q.get(timeout=120) for _ in ps)}
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in (0, 1):
+        o, attached = res[r]
+        assert attached
+        assert o["allreduce_bytes_per_step"] == 4 * (10 + 100 + 100 + 100 + 37)
+        assert o["allreduce_ms_per_step"] >= 0.0 and o["solo_ms_per_step"] >= 0.0
+        assert abs(o["exposed_comm_ms_per_step"] - (50.0 - o["solo_ms_per_step"])) < 1e-2

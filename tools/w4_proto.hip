@@ -70,7 +70,7 @@ struct Args {
 // SG: sched_group_barrier interleave in the main loop (0 = compiler's order)
 // PERS: 0 = one tile per workgroup (grid = tiles, XCD-major), 1 = persistent: workgroup w takes tiles
 // w*per .. (the grid divides the tiles), 2 = persistent strided
-template <int SG, int PERS, int AM, int DG = 0>
+template <int SG, int PERS, int AM, int DG = 0, int PA = 1>
 __global__ void __launch_bounds__(256, 1) w4_kernel(const Args p) {
   constexpr int BK = 64, STAGE = 64 * 1024;  // A 32 KiB + B 32 KiB per k-tile image
   __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
@@ -106,6 +106,7 @@ __global__ void __launch_bounds__(256, 1) w4_kernel(const Args p) {
     const int a_st = __builtin_amdgcn_readfirstlane(32 * p.lda * 2), b_st = __builtin_amdgcn_readfirstlane(32 * p.ldb * 2);
 
     v4u st[16];
+    v4u sa2[8];  // PA = 2: the second A staging buffer (A of k-tile k lives in buffer k & 1: 0 = st[0..7], 1 = sa2)
     auto gload = [&](int kt) {
 #pragma unroll
       for (int i = 0; i < 8; ++i)
@@ -148,7 +149,19 @@ __global__ void __launch_bounds__(256, 1) w4_kernel(const Args p) {
     gload(0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     swrite(0);
-    if (nk > 1) gload(1);
+    if constexpr (PA == 2) {  // A1 -> buffer 1, B1, A2 -> buffer 0 (nk >= 4, even: host-checked)
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        sa2[i] = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(rA, a_vo, 128 + i * a_st, 0));
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        st[8 + i] = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(rB, b_vo, 128 + i * b_st, 0));
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        st[i] = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(rA, a_vo, 256 + i * a_st, 0));
+    } else {
+      if (nk > 1) gload(1);
+    }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     fread0(0);
@@ -163,8 +176,10 @@ __global__ void __launch_bounds__(256, 1) w4_kernel(const Args p) {
       else if (r < 9) bv[r - 1] = *LDS_PTR(const v8s, base + fb + (r - 1) * 2048);
       else av[r - 8] = *LDS_PTR(const v8s, base + fa + (r - 8) * 2048);
     };
-    auto step = [&](int t, auto more1_c, auto more2_c) {
+    auto step = [&](int t, auto more1_c, auto more2_c, auto more3_c, auto par_c) {
       constexpr bool MORE1 = decltype(more1_c)::value, MORE2 = decltype(more2_c)::value;
+      constexpr bool MORE3 = decltype(more3_c)::value;  // PA = 2: A of k-tile t+3 exists
+      constexpr int PB = decltype(par_c)::value;         // PA = 2: the A buffer of k-tile t+1 (= (t + 1) & 1)
       const int cur = t & 1, nxt = cur ^ 1;
       const char* bcur = smem + cur * STAGE;
       const char* bnxt = smem + nxt * STAGE;
@@ -176,15 +191,31 @@ __global__ void __launch_bounds__(256, 1) w4_kernel(const Args p) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) mfma_acc<AM>(acc[i][j0 + j], a0[i], b0[j0 + j]);
         __builtin_amdgcn_sched_barrier(0);
-        if constexpr (MORE1 && !(DG & 2)) {
-          if (q < 8) *LDS_PTR(v4u, wnxt + st_lds + q * 4096) = st[q];
-          else *LDS_PTR(v4u, wnxt + 32768 + st_lds + (q - 8) * 4096) = st[q];
-        }
-        if constexpr (MORE2 && !(DG & 1)) {
-          if (q < 8)
-            st[q] = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(rA, a_vo, (t + 2) * 128 + q * a_st, 0));
-          else
-            st[q] = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(rB, b_vo, (t + 2) * 128 + (q - 8) * b_st, 0));
+        if constexpr (PA == 2) {
+          if constexpr (MORE1 && !(DG & 2)) {
+            if (q < 8) *LDS_PTR(v4u, wnxt + st_lds + q * 4096) = PB ? sa2[q] : st[q];
+            else *LDS_PTR(v4u, wnxt + 32768 + st_lds + (q - 8) * 4096) = st[q];
+          }
+          if (q < 8) {
+            if constexpr (MORE3 && !(DG & 1)) {
+              const v4u v = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(rA, a_vo, (t + 3) * 128 + q * a_st, 0));
+              if constexpr (PB) sa2[q] = v; else st[q] = v;
+            }
+          } else {
+            if constexpr (MORE2 && !(DG & 1))
+              st[q] = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(rB, b_vo, (t + 2) * 128 + (q - 8) * b_st, 0));
+          }
+        } else {
+          if constexpr (MORE1 && !(DG & 2)) {
+            if (q < 8) *LDS_PTR(v4u, wnxt + st_lds + q * 4096) = st[q];
+            else *LDS_PTR(v4u, wnxt + 32768 + st_lds + (q - 8) * 4096) = st[q];
+          }
+          if constexpr (MORE2 && !(DG & 1)) {
+            if (q < 8)
+              st[q] = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(rA, a_vo, (t + 2) * 128 + q * a_st, 0));
+            else
+              st[q] = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(rB, b_vo, (t + 2) * 128 + (q - 8) * b_st, 0));
+          }
         }
         if constexpr (!(DG & 4)) rd(a1, b1, bcur, fa1, fb1, q);
         __builtin_amdgcn_sched_barrier(0);
@@ -211,9 +242,23 @@ __global__ void __launch_bounds__(256, 1) w4_kernel(const Args p) {
     };
     using T_ = std::true_type;
     using F_ = std::false_type;
-    for (int t = 0; t + 2 < nk; ++t) step(t, T_{}, T_{});
-    if (nk >= 2) step(nk - 2, T_{}, F_{});
-    step(nk - 1, F_{}, F_{});
+    if constexpr (PA == 2) {
+      using P0 = std::integral_constant<int, 0>;
+      using P1 = std::integral_constant<int, 1>;
+      for (int t = 0; t + 4 < nk; t += 2) {
+        step(t, T_{}, T_{}, T_{}, P1{});
+        step(t + 1, T_{}, T_{}, T_{}, P0{});
+      }
+      step(nk - 4, T_{}, T_{}, T_{}, P1{});
+      step(nk - 3, T_{}, T_{}, F_{}, P0{});
+      step(nk - 2, T_{}, F_{}, F_{}, P1{});
+      step(nk - 1, F_{}, F_{}, F_{}, P0{});
+    } else {
+      using Q0 = std::integral_constant<int, 0>;
+      for (int t = 0; t + 2 < nk; ++t) step(t, T_{}, T_{}, F_{}, Q0{});
+      if (nk >= 2) step(nk - 2, T_{}, F_{}, F_{}, Q0{});
+      step(nk - 1, F_{}, F_{}, F_{}, Q0{});
+    }
 
     if constexpr (AM == 1) asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");  // last MFMA's D -> epilogue reads
     // epilogue: bf16 C through a wave-private f32 staging image of 32 rows x 128 columns (+4 pad)
@@ -456,9 +501,9 @@ struct Variant {
   int grid;
 };
 
-template <int SG, int PERS, int AM = 1, int DG = 0>
+template <int SG, int PERS, int AM = 1, int DG = 0, int PA = 1>
 static void launch(const Args& a, hipStream_t s, int grid) {
-  hipLaunchKernelGGL((w4_kernel<SG, PERS, AM, DG>), dim3(grid), dim3(256), 0, s, a);
+  hipLaunchKernelGGL((w4_kernel<SG, PERS, AM, DG, PA>), dim3(grid), dim3(256), 0, s, a);
 }
 
 template <int PERS, int DG = 0>
@@ -497,6 +542,11 @@ int main(int argc, char** argv) {
   vs.push_back({"w4 one-shot", launch<0, 0>, a.ntiles});
   if (a.ntiles % 3 == 0) vs.push_back({"w4 pers tiles/3 (3 each)", launch<0, 1>, a.ntiles / 3});
   vs.push_back({"w4 pers 256 strided", launch<0, 2>, 256});
+  if ((K / 64) % 2 == 0 && K / 64 >= 4) {
+    vs.push_back({"w4p A 2-ahead one-shot", launch<0, 0, 1, 0, 2>, a.ntiles});
+    if (a.ntiles % 3 == 0) vs.push_back({"w4p A 2-ahead pers /3", launch<0, 1, 1, 0, 2>, a.ntiles / 3});
+    vs.push_back({"w4p A 2-ahead pers 256", launch<0, 2, 1, 0, 2>, 256});
+  }
   vs.push_back({"w4d dma one-shot", launchd<0>, a.ntiles});
   if (a.ntiles % 3 == 0) vs.push_back({"w4d dma pers tiles/3", launchd<1>, a.ntiles / 3});
   vs.push_back({"w4d dma pers 256 strided", launchd<2>, 256});

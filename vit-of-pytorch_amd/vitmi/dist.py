@@ -76,6 +76,11 @@ class GradAllReducer:
         self.min_bucket = min_bucket_elems
         self._pending = None  # (buf, start) of a bucket being coalesced with the next one
         self._works = []
+        # exchange accounting (bench.py's N > 1 dist_check): a list while enabled; per launched bucket
+        # ("events", start, end, elems) — HIP events on the exchange stream around its all-reduce — or, on the CPU
+        # (gloo async) path, ("host", ms waited in finish(), elems of the step)
+        self.timing = None
+        self._host_elems = 0
 
     def attach(self):
         self.engine.grad_ready_hook = self.hook
@@ -104,6 +109,9 @@ class GradAllReducer:
             for ev in events:  # the bucket's producers (main and side streams of the engine)
                 self.stream.wait_event(ev)
             with torch.cuda.stream(self.stream):
+                if self.timing is not None:
+                    e0 = torch.cuda.Event(enable_timing=True)
+                    e0.record(self.stream)
                 if self.compress:
                     from . import ops
                     tb = self._staging(buf, start, end)
@@ -112,6 +120,10 @@ class GradAllReducer:
                     ops.unpack_bf16_f32(tb, end - start, 1, end - start, t, end - start)
                 else:
                     dist.all_reduce(t, op=op, group=self.group)
+                if self.timing is not None:
+                    e1 = torch.cuda.Event(enable_timing=True)
+                    e1.record(self.stream)
+                    self.timing.append(("events", e0, e1, end - start))
         else:
             if self.compress:
                 tb = self._staging(buf, start, end)
@@ -119,6 +131,17 @@ class GradAllReducer:
                 self._widen.append((t, tb))
                 t = tb
             self._works.append(dist.all_reduce(t, op=op, group=self.group, async_op=True))
+            self._host_elems += end - start
+
+    def timing_summary(self):
+        """(all-reduce ms, buckets, elements) of the launches recorded since `timing` was set to []: the sum of the
+        per-bucket HIP-event spans on the exchange stream (each all-reduce as the exchange stream sees it, from its
+        launch after the bucket's producers to the collective's completion), or the CPU path's time waited"""
+        if not self.timing:
+            return 0.0, 0, 0
+        ms = sum(a.elapsed_time(b) if kind == "events" else a for kind, a, b, _ in self.timing)
+        n = sum(1 for kind, *_ in self.timing if kind == "events") or len(self.timing)
+        return ms, n, sum(e for *_, e in self.timing)
 
     def hook(self, buf, name, start, end, events=()):
         if self.world == 1:
@@ -138,9 +161,14 @@ class GradAllReducer:
         if self.cuda:
             torch.cuda.current_stream(self.engine.dev).wait_stream(self.stream)
         else:
+            import time
+            t0 = time.perf_counter()
             for w in self._works:
                 w.wait()
+            if self.timing is not None and self._works:
+                self.timing.append(("host", (time.perf_counter() - t0) * 1e3, None, self._host_elems))
             self._works = []
+            self._host_elems = 0
             for t, tb in self._widen:
                 t.copy_(tb)
             self._widen = []
