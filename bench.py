@@ -66,6 +66,27 @@ def pmc_traffic(kernel_tag="gemm_pp2_kernel<true, true, 8,"):
     return None
 
 
+def condition_init(model, seed=1):
+    """The bench's weights: the reference constructor's seed-42 draw (src/model.py:161-194, reference RNG order) with
+    the attention projections redrawn at N(0, 1/D) and the position embedding and classifier at N(0, 0.02^2), in
+    named-parameter order from Generator(seed) (the rescale of SURVEY.md §8c's parity protocol). Under the raw std-1
+    draw the first step's gradient norm is ~1e11 (layer 0's saturated attention) and the bf16 training step turns every
+    parameter into NaN from step 1 on (tools/dbg/bench_loss_trace.py, profiles/r06/bench_loss_trace.txt): a throughput
+    timed on NaN operands is not a training step (and DVFS runs constant bit patterns faster). VITMI_BENCH_INIT=reference
+    keeps the raw draw for A/B."""
+    import math
+    g = torch.Generator().manual_seed(seed)
+    sd = model.state_dict()
+    new = {}
+    for k, v in sd.items():
+        if ".attn." in k and k.endswith(".weight"):
+            D = v.shape[0] if not k.endswith("out.weight") else v.shape[-1]
+            new[k] = torch.randn(v.shape, generator=g) / math.sqrt(D)
+        elif k in ("transformer.pos_embedding.pos_embedding", "classifier.weight"):
+            new[k] = 0.02 * torch.randn(v.shape, generator=g)
+    model.load_state_dict(new, strict=False)
+
+
 def onecycle_hyper_table(total_steps, dev):
     """{lr, momentum, first-step} of every bench step as a [steps][3] f32 device table: torch's OneCycleLR as the
     reference configures it (src/train.py:159-163: max_lr .03, 500 warm-up of 15000 steps, cycle_momentum) driving
@@ -237,7 +258,11 @@ def main():
     model = VisionTransformer(image_size=(args.image_size, args.image_size),
                               patch_size=(arch["patch_size"], arch["patch_size"]), emb_dim=arch["emb_dim"],
                               mlp_dim=arch["mlp_dim"], num_heads=arch["num_heads"], num_layers=arch["num_layers"],
-                              num_classes=args.num_classes, attn_dropout_rate=0.0, dropout_rate=0.0).to(dev)
+                              num_classes=args.num_classes, attn_dropout_rate=0.0, dropout_rate=0.0)
+    init_kind = os.environ.get("VITMI_BENCH_INIT", "conditioned")
+    if init_kind != "reference":
+        condition_init(model)
+    model = model.to(dev)
     eng = model.engine()
     eng.refresh_mirror()
     if os.environ.get("VITMI_ATTN_FWD_PATH"):  # A/B: 3 = the one-shot attention forward instead of the persistent one
@@ -257,7 +282,8 @@ def main():
 
     def step_body():
         eng.forward(x)
-        dl, _ = eng.cross_entropy(y, grad_scale=1.0 / (b * world))
+        dl, st = eng.cross_entropy(y, grad_scale=1.0 / (b * world))
+        losses.append(st)
         eng.backward(dl)
         if reducer is not None:
             reducer.finish()
@@ -270,12 +296,17 @@ def main():
     use_graph = world == 1 and os.environ.get("VITMI_BENCH_GRAPH", "0") != "0"
     graph = None
 
+    losses = []  # the CE kernel's row-stats buffer (one persistent buffer, overwritten every step)
+    first_timed = []
+
     def step(k):
         ops.copy2d(hyper, 12, hyper_all[k], 12, 12, 1)
         if graph is not None:
             graph.replay()
         else:
             step_body()
+        if k == args.warmup and losses:  # the first timed step's mean loss, kept on the device (one tiny kernel)
+            first_timed.append(losses[-1][:, 0].mean())
 
     def barrier():
         if world > 1:
@@ -296,6 +327,8 @@ def main():
         step(k)
     barrier()
     dt = time.perf_counter() - t0
+    loss_last = float(losses[-1][:, 0].mean()) if losses else float("nan")
+    loss_first = float(first_timed[0]) if first_timed else float("nan")
     # HIP events around the roofline kernels' launches of one more (eager) step after the timed region,
     # on the stream the kernels run on (each event record costs the stream ~10 us of idle)
     probes = ([], [])
@@ -389,7 +422,10 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "bf16",
-        "data": "synthetic (N(0,1) images, uniform labels, seed-42 reference-order random init)",
+        "data": ("synthetic (N(0,1) images, uniform labels, seed-42 reference-order random init" +
+                 (", attention projections at N(0,1/D) and pos-emb / classifier at N(0,0.02^2): bench.condition_init)"
+                  if init_kind != "reference" else ")")),
+        "loss_first_timed_step": round(loss_first, 5), "loss_last_timed_step": round(loss_last, 5),
         "config": {"workload": f"ViT-{args.arch.upper()} @{args.image_size} train step (fwd+CE+bwd+"
                                f"{comm + ' all-reduce+' if world > 1 else ''}SGD-momentum/OneCycleLR)",
                    "model": f"ViT-{args.arch.upper()}", "image_size": args.image_size, "per_gpu_batch": b,
@@ -628,14 +664,19 @@ def bench_resvit(args, world, rank, dev, backend, comm):
     x = torch.randn(b, 3, args.image_size, args.image_size, device=dev, generator=g)
     y = torch.randint(0, 100, (b,), device=dev, generator=g)
     ratios = []
-    # one process: forward + backward replayed from a HIP graph (GraphedTrainStep), the optimizer eager;
-    # data parallel: op by op (the gradient all-reduce hooks run during the backward)
-    graphed = GraphedTrainStep(model, x, y, opt, sched, 1e-4, 1e-2, 1.0, True) if reducer is None else None
+    # forward + backward replayed from a HIP graph (GraphedTrainStep), the optimizer eager; data parallel: the
+    # flat gradient all-reduced after each replay (reducer.finish). VITMI_RESVIT_EAGER=1: op by op instead (the
+    # all-reduce hooks then run during the backward) — the A/B of profiles/r06/resvit_eager_vs_graph.txt
+    eager = os.environ.get("VITMI_RESVIT_EAGER", "0") != "0"
+    graphed = None if eager else GraphedTrainStep(model, x, y, opt, sched, 1e-4, 1e-2, 1.0, True, reducer=reducer)
+
+    totals = []
 
     def step():
         out = graphed.step() if graphed is not None else train_step(model, x, y, opt, sched, 1e-4, 1e-2, 1.0, True,
                                                                     reducer)
         ratios.append(out[5]["non_low_rank_ratio"].clone())
+        totals.append(out[0].detach().clone())
 
     def barrier():
         if world > 1:
@@ -677,6 +718,8 @@ def bench_resvit(args, world, rank, dev, backend, comm):
                      "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": None},
         "executed_gflop_per_image": round(fpi / 1e9, 3),
         "active_ratio": round(active, 4),
+        "loss_first_timed_step": round(float(totals[args.warmup]), 5),
+        "loss_last_timed_step": round(float(totals[-1]), 5),
     }
     if dist_check is not None:
         out["dist_check"] = dist_check

@@ -145,3 +145,21 @@ def test_splitk_factor_one_wave_splits_and_h14_tail():
     for M, N, K in [(768, 768, 50432), (64, 64, 1 << 20), (5120, 1280, 32896)]:
         s = f(M, N, K)
         assert 1 <= s <= 32 and (s == 1 or K // 64 // s >= 8)
+
+
+def test_bench_condition_init_is_the_parity_rescale():
+    """bench.condition_init (the bench's weights: seed-42 reference draw, attention projections and pos-emb /
+    classifier rescaled) equals the oracle's tame_params on the reference constructor's parameters, bit for bit"""
+    import sys
+    sys.path.insert(0, REPO)
+    import bench
+    from oracle.vit_oracle import tame_params
+    from vitmi.model import VisionTransformer
+    torch.manual_seed(42)
+    m = VisionTransformer(image_size=(32, 32), patch_size=(4, 4), emb_dim=128, mlp_dim=256, num_heads=2, num_layers=2,
+                          num_classes=10)
+    ref = tame_params(m.state_dict())
+    bench.condition_init(m)
+    sd = m.state_dict()
+    assert sd.keys() == ref.keys()
+    assert all(torch.equal(sd[k], ref[k]) for k in ref)

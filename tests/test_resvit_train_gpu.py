@@ -304,7 +304,8 @@ def test_adamw_state_dict_round_trip_and_gate_or():
 def test_resvit_data_parallel_two_ranks(tmp_path):
     """Res-ViT DP (new: the reference is single-device): 2 ranks on one GPU over gloo, 4 images each,
     FlatGradAllReducer on the LoRA / router / approximator / head gradients, vitmi AdamW with the clip
-    folded in. Both replicas end bit-identical, and (lambda_active = 0: the ratio loss is a non-linear
+    folded in. Both replicas end bit-identical, the graphed step (GraphedTrainStep with the reducer: the
+    exchange after each replay) equals the eager one bit for bit, and (lambda_active = 0: the ratio loss is a non-linear
     function of the per-rank mean) equal to one 8-image step of a single process within 2e-2 of the
     update."""
     script = tmp_path / "dp_resvit.py"
@@ -332,12 +333,18 @@ def make():
                                  nz[rank * 4:(rank + 1) * 4])(noise.cuda())
     return m
 
-def run(m, x, y, reducer=None):
+def run(m, x, y, reducer=None, graphed=False):
     opt = AdamW(m.parameters(), lr=1e-2, weight_decay=0.05, max_grad_norm=1.0)
     if reducer:
         red = FlatGradAllReducer(opt.flat, bucket_elems=2000).attach()
-    for _ in range(2):
-        train_step(m, x, y, opt, None, 0.0, 1e-2, 1.0, True, red if reducer else None)
+    if graphed:  # forward + backward replayed from a HIP graph, the exchange after each replay
+        from vitmi.resvit_train import GraphedTrainStep
+        gs = GraphedTrainStep(m, x, y, opt, None, 0.0, 1e-2, 1.0, True, reducer=red)
+        for _ in range(2):
+            gs.step()
+    else:
+        for _ in range(2):
+            train_step(m, x, y, opt, None, 0.0, 1e-2, 1.0, True, red if reducer else None)
     torch.cuda.synchronize()
     return torch.cat([p.detach().reshape(-1) for p in m.parameters()]).cpu()
 
@@ -345,6 +352,9 @@ m = make()
 flat = run(m, X[rank * 4:(rank + 1) * 4].cuda(), Y[rank * 4:(rank + 1) * 4].cuda(), reducer=True)
 out = [torch.zeros_like(flat) for _ in range(world)]
 dist.all_gather(out, flat)
+# the graphed data-parallel step (bench.py's default at N > 1): the same two steps, bit-identical to the eager one
+flat_g = run(make(), X[rank * 4:(rank + 1) * 4].cuda(), Y[rank * 4:(rank + 1) * 4].cuda(), reducer=True, graphed=True)
+assert torch.equal(flat_g, flat), float((flat_g - flat).abs().max())
 if rank == 0:
     assert torch.equal(out[0], out[1]), "replicas diverged"
     torch.manual_seed(42)

@@ -85,8 +85,13 @@ class GraphedTrainStep:
     train_step does; its inputs are the static `x` / `y` buffers (copy a new batch in with `step(x, y)`)
     and its outputs are static tensors overwritten by every replay.
 
-    Single process (no gradient all-reduce hooks: a data-parallel step stays on train_step); raises when a
-    torch.distributed group of more than one rank is initialised.
+    Data parallel (res-vit/train.py:23-68 on every rank): pass the rank's FlatGradAllReducer as `reducer`. Its
+    per-parameter hooks stay detached (no collective is captured); after each replay the whole flat gradient is
+    all-reduced bucket by bucket, with the used flags, by reducer.finish() before the clip + AdamW update. The
+    trainable set is small (LoRA, routers, approximators, head: a few MB), so the exchange after the backward costs
+    a fraction of a millisecond where the eager step's overlap would have hidden it, against the eager step's
+    host-bound launch gaps. Without a reducer it raises when a torch.distributed group of more than one rank is
+    initialised.
 
     Construction runs `warmup` forward + backward passes on `x` / `y` (no optimizer or scheduler step; the
     gradients are zeroed after them, and the torch CPU / CUDA RNG states are restored, so the Gumbel draws
@@ -95,13 +100,18 @@ class GraphedTrainStep:
     """
 
     def __init__(self, model, x, y, optimizer, lr_scheduler=None, lambda_active=10.0, lambda_distill=1.0,
-                 lambda_class=10.0, clip_grad_norm=True, warmup=1):
+                 lambda_class=10.0, clip_grad_norm=True, warmup=1, reducer=None):
         from . import flat as _flat
         if not isinstance(optimizer, AdamW):
             raise TypeError("GraphedTrainStep: vitmi.optim.AdamW (flat gradients at fixed addresses) expected")
-        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
-            raise RuntimeError("GraphedTrainStep is single-process: a data-parallel step (gradient all-reduce "
-                               "hooks in the backward) runs train_step with a FlatGradAllReducer")
+        if reducer is None and dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+            raise RuntimeError("GraphedTrainStep with more than one rank needs the rank's FlatGradAllReducer "
+                               "(reducer=...): the exchange runs after each replay")
+        if reducer is not None:
+            if reducer.flat is not optimizer.flat:
+                raise ValueError("GraphedTrainStep: the reducer must own the optimizer's flat gradient buffer")
+            reducer.detach()  # no collective inside the warm-up or the capture: finish() exchanges after the replay
+        self.reducer = reducer
         self.model, self.opt, self.sched = model, optimizer, lr_scheduler
         self.lambdas = (lambda_active, lambda_distill, lambda_class)
         self.clip = clip_grad_norm
@@ -151,6 +161,8 @@ class GraphedTrainStep:
         f.used_host = list(self.used)
         for p, flag in self.gates:
             self._flat._GATES[id(p)] = (weakref.ref(p), flag)
+        if self.reducer is not None:
+            self.reducer.finish()  # every bucket in order + the used flags over the ranks; the stream waits
         if self.clip and self.opt.max_grad_norm is None:
             clip_grad_norm_(None, max_norm=1.0, norm_type=2, flat=self.opt)
         self.opt.step()
