@@ -139,8 +139,10 @@ def _cpu_share():
 def cpu_baseline(arch, image_size, num_classes, seconds_budget=20.0):
     """Time the CPU oracle (restatement of reference src/train.py:train_epoch's step) on the host, on
     every core this process may run on, under both init protocols: the tamed rescale
-    (the parity protocol) and the reference's own std-1 init (slower on CPU: saturated softmax ->
-    subnormal floats). `value` is the reference-init rate, the reference's own configuration."""
+    (the parity protocol, = bench.condition_init: the weights the GPU line trains) and the reference's own std-1
+    init (slower on CPU: saturated softmax -> subnormal floats). `value` is the tamed-init rate, the same weights
+    as the GPU measurement (round 6; the GPU line moved off the std-1 draw, which trains on NaN from step 1);
+    `value_reference_init` keeps the std-1 rate."""
     from oracle.vit_oracle import OneCycle, ViTConfig, init_params, loss_and_grads, sgd_step, tame_params
     cores = _cpu_share()
     torch.set_num_threads(cores)
@@ -168,11 +170,11 @@ def cpu_baseline(arch, image_size, num_classes, seconds_budget=20.0):
         dt = time.perf_counter() - t0
         rates[proto] = (steps * bs / dt, steps, dt)
     r, t = rates["reference"], rates["tamed"]
-    return dict(value=round(r[0], 3), unit="images/sec", cores=cores, kind="port", cpu_model=_cpu_model(),
-                value_tamed_init=round(t[0], 3),
+    return dict(value=round(t[0], 3), unit="images/sec", cores=cores, kind="port", cpu_model=_cpu_model(),
+                value_reference_init=round(r[0], 3),
                 sample=f"oracle fp32 CPU train step (fwd+CE+bwd+SGD/OneCycleLR) on {cores} threads ({_cpu_model()}): "
-                       f"reference std-1 init, batch 16, {r[1]} steps in {r[2]:.1f} s; tamed init, batch 16, {t[1]} "
-                       f"steps in {t[2]:.1f} s; each after 1 warm-up step")
+                       f"tamed init (the GPU line's weights), batch 16, {t[1]} steps in {t[2]:.1f} s; reference std-1 "
+                       f"init, batch 16, {r[1]} steps in {r[2]:.1f} s; each after 1 warm-up step")
 
 
 def _free_port():
