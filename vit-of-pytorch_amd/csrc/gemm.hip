@@ -120,6 +120,15 @@ extern "C" int64_t vit_gemm_split_rows(const vit_gemm_args* a) {
   return wave_split_rows(a, pick_tile(a));
 }
 
+#ifdef VIT_PP2_STAMPS
+// diagnostic build: device buffer of 2 x 8 u64 for gemm_pp2's slot stamps (taken when VIT_GEMM_DIAG = 4)
+static unsigned long long* g_pp2_stamp_buf = nullptr;
+extern "C" int vit_gemm_set_stamps(void* dev_buf) {
+  g_pp2_stamp_buf = (unsigned long long*)dev_buf;
+  return 0;
+}
+#endif
+
 namespace {
 // validated device descriptor of a call's arguments; `empty`: M or N is 0 (nothing to launch)
 int make_dev(const vit_gemm_args* a, GemmDev& d, bool& empty) {
@@ -203,6 +212,9 @@ int make_dev(const vit_gemm_args* a, GemmDev& d, bool& empty) {
     d.split_xcd = env_sx;
     static const int env_prio = vit::knob("VIT_GEMM_PRIO", 1);
     d.prio = env_prio;
+#ifdef VIT_PP2_STAMPS
+    d.stamps = g_pp2_stamp_buf;
+#endif
   }
   return VIT_OK;
 }
