@@ -212,6 +212,8 @@ int make_dev(const vit_gemm_args* a, GemmDev& d, bool& empty) {
     d.split_xcd = env_sx;
     static const int env_prio = vit::knob("VIT_GEMM_PRIO", 1);
     d.prio = env_prio;
+    static const int env_ilv = vit::knob("VIT_GEMM_ILV", -1);
+    d.ilv = env_ilv;
 #ifdef VIT_PP2_STAMPS
     d.stamps = g_pp2_stamp_buf;
 #endif

@@ -51,6 +51,7 @@ struct GemmDev {
   int diag;            // diagnostics (VIT_GEMM_DIAG): 1 = skip the half-tile kernel's global stores, 2 = its epilogue
   int split_xcd;       // split-K grids: place each XCD's workgroups on one or two K-chunks (VIT_GEMM_SPLIT_XCD)
   int prio;            // s_setprio(1) around the ping-pong kernels' MFMA clusters (VIT_GEMM_PRIO)
+  int ilv;             // diagnostic builds: gemm_pp2's interleaved read slot, -1 auto (M/N-contiguous pairs), 0 off, 1 on
 #ifdef VIT_PP2_STAMPS
   unsigned long long* stamps;  // diagnostic build: gemm_pp2's slot stamps (VIT_GEMM_DIAG = 4, vit_gemm_set_stamps)
 #endif

@@ -71,6 +71,28 @@ __device__ __forceinline__ void stage_tile(char* smem, int lds_off, __amdgpu_buf
 }
 
 // 16 rows (r0..r0+15) x 32 k (kk*32..) MFMA fragment of this lane.
+// piece i (0 <= i < INSTR) of stage_tile's image alone
+template <int ROWS, int BK, bool KC, int NWAVE>
+__device__ __forceinline__ void stage_piece(char* smem, int lds_off, __amdgpu_buffer_rsrc_t rs, long ld, int kt,
+                                            int wave, int lane, int vbase, int i) {
+  constexpr int CPR = KC ? BK / 8 : ROWS * 2 / 16;
+  constexpr int RSTEP = NWAVE * 64 / CPR;
+  static_assert(RSTEP % 16 == 0, "swizzle must repeat between a wave's instructions");
+  const int c = wave * 64 + lane;
+  const int r = c / CPR, pc = c % CPR;
+  int lane_off, base;
+  if constexpr (KC) {
+    lane_off = (int)(r * ld * 2) + (pc ^ swz_k<BK>(r)) * 16;
+    base = kt * BK * 2 + vbase;
+  } else {
+    lane_off = (int)(r * ld * 2) + ((pc * 16) ^ (swz_mn(r) << 5));
+    base = (int)((long)kt * BK * ld * 2) + vbase;
+  }
+  base = __builtin_amdgcn_readfirstlane(base + i * (int)(RSTEP * ld * 2));
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, LDS_PTR(void, smem + lds_off + (i * NWAVE + wave) * 1024), 16,
+                                           lane_off + base, 0, 0, 0);
+}
+
 template <int ROWS, int BK, bool KC>
 __device__ __forceinline__ v8s read_frag(const char* smem, int lds_off, int r0, int kk, int lane) {
   if constexpr (KC) {
