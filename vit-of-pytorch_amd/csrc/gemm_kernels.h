@@ -71,7 +71,8 @@ __device__ __forceinline__ void stage_tile(char* smem, int lds_off, __amdgpu_buf
 }
 
 // 16 rows (r0..r0+15) x 32 k (kk*32..) MFMA fragment of this lane.
-// piece i (0 <= i < INSTR) of stage_tile's image alone
+// piece i (0 <= i < INSTR) of stage_tile's image alone (gemm_pp2's interleaved read slot). Same addressing as
+// stage_tile, which keeps its own loop so that the lane offset and the row step are computed once per image.
 template <int ROWS, int BK, bool KC, int NWAVE>
 __device__ __forceinline__ void stage_piece(char* smem, int lds_off, __amdgpu_buffer_rsrc_t rs, long ld, int kt,
                                             int wave, int lane, int vbase, int i) {
